@@ -1,0 +1,228 @@
+#!/usr/bin/env python
+"""Benchmark of the MI355X rdc allreduce path (BASELINE.json metric:
+"allreduce GB/s (device-resident fp32) at 1/2/4/8 GPUs; % xGMI roofline").
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Workload: a 1 GiB fp32 buffer per GPU (the cfg3 buffer), synthetic data
+from the device generator, resident in HBM before timing starts.
+  N = 1 : one "step" = the reduce kernel alone (op::Reducer<Sum,float>,
+          include/core/mpi.h:113-120): dst += src over the 1 GiB buffer —
+          the north star's 1-GPU data point (an allreduce over one rank moves
+          nothing).  HBM-bound: 3 x S algorithmic bytes per launch.
+  N > 1 : one step = one in-place allreduce of the buffer across the N ranks
+          (one process per GPU, HIP IPC over xGMI), bit-identical to the
+          reference's ring.  xGMI-bound: 2(N-1)/N x S egress bytes per GPU.
+value = bytes of input buffers all ranks reduced per second = N x S / t
+(t = wall time of the K timed steps, max over ranks, barrier+sync brackets).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_DIR_GBPS = 76.8     # one xGMI link, one direction (153.6 GB/s bidirectional)
+BIDIR_RING_GBPS = 153.6       # north-star roofline: two counter-rotating rings (busbw)
+DTYPES = {"float32": (6, 4), "float16": (10, 2), "bfloat16": (11, 2), "float64": (7, 8)}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--bytes", type=int, default=1 << 30, help="buffer size per GPU")
+    ap.add_argument("--dtype", default="float32", choices=sorted(DTYPES))
+    ap.add_argument("--algo", default="auto", choices=["auto", "mesh", "ring"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--no-check", action="store_true", help="skip the post-run oracle spot check")
+    return ap.parse_args()
+
+
+def load_traffic(kernel_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel_key)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(nbytes_workload, seconds):
+    """Reference op::Reducer<Sum,float> (oracle/_ref, the reference's own header
+    compiled -O2) or, if absent, the C oracle port, single thread, on a bounded
+    256 MiB sample of the same dst += src workload."""
+    import numpy as np
+    from oracle import oracle as O
+    if seconds <= 0:
+        return None
+    n = min(nbytes_workload, 256 << 20) // 4
+    dst = np.ones(n, dtype=np.float32)
+    src = np.full(n, 0.5, dtype=np.float32)
+    ref = O.ref() if O.ref_available() else None
+    fn = (lambda: ref.ref_reducer(dst.ctypes.data, src.ctypes.data, n, 6, 2)) if ref else \
+        (lambda: O.lib().rdc_oracle_reducer(dst.ctypes.data, src.ctypes.data, n, 6, 2))
+    fn()  # page in
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {
+        "value": round(n * 4 * reps / el / 1e9, 3),
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "reference" if ref else "port",
+        "sample": "op::Reducer<Sum,float> dst += src over a %d MiB fp32 buffer, %d reps in %.1f s, 1 thread "
+                  "(value = buffer bytes / time, same unit as the GPU line; HBM-equivalent traffic 3x)"
+                  % (n * 4 >> 20, reps, el),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import rdc_amd
+    from rdc_amd._lib import _LIB, check_call
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    dt_enum, esz = DTYPES[args.dtype]
+    count = args.bytes // esz
+    S = count * esz
+    torch.cuda.set_device(local)
+    tdtype = getattr(torch, args.dtype)
+    stream = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        rdc_amd.init([])          # RANK/WORLD_SIZE + MASTER_ADDR:MASTER_PORT+1 bootstrap
+        comm = rdc_amd.get_comm("main")
+        algo = {"auto": 0, "ring": 1, "mesh": 2}[args.algo]
+        buf = torch.empty(count, dtype=tdtype, device="cuda")
+        rdc_amd.fill_(buf, 0x5EED0000, rank)
+
+        def step():
+            check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), count, dt_enum, 2,
+                                               algo, sp))
+    else:
+        dst = torch.empty(count, dtype=tdtype, device="cuda")
+        src = torch.empty(count, dtype=tdtype, device="cuda")
+        rdc_amd.fill_(dst, 0x5EED0000, 0)
+        rdc_amd.fill_(src, 0x5EED0000, 1)
+
+        def step():
+            check_call(_LIB.RdcReduce(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()), count,
+                                      dt_enum, 2, sp))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        comm.check(sp)
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    if world > 1:
+        comm.check(sp)
+    wall = t1 - t0
+    kern_ms = e0.elapsed_time(e1) / args.steps
+    if world > 1:
+        tt = torch.tensor([wall, kern_ms], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall, kern_ms = float(tt[0]), float(tt[1])
+
+    # spot check (outside the timed region): N=1 reduce result vs oracle on a slice
+    check = None
+    if world == 1 and not args.no_check:
+        from oracle import oracle as O
+        import numpy as np
+        m = min(count, 1 << 16)
+        d0 = O.fill(m, dt_enum, 0x5EED0000, 0)  # the generator is position-keyed: first m elements
+        s0 = O.fill(m, dt_enum, 0x5EED0000, 1)
+        acc = d0.copy()
+        for _ in range(args.warmup + args.steps):
+            O.reducer(s0, acc, dt_enum, 2)
+        got = dst[:m].cpu().numpy()
+        check = bool(got.tobytes() == acc.tobytes())
+
+    if rank != 0:
+        dist.barrier()
+        rdc_amd.finalize()
+        return
+    value = world * S / wall * args.steps / 1e9
+    algbw = S / (kern_ms * 1e-3) / 1e9
+    if world == 1:
+        achieved = 3 * S / (kern_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": load_traffic("reduce_sum_f32_%d" % S), "kernel": "k_reduce<Sum,float>",
+                "algorithmic_bytes_per_launch": 3 * S, "kernel_avg_ms": round(kern_ms, 4)}
+        workload = "reduce kernel alone (n=1): dst += src, %s, %d MiB per buffer" % (args.dtype, S >> 20)
+        par = "single GPU"
+    else:
+        busbw = algbw * 2 * (world - 1) / world
+        algo_name = args.algo if args.algo != "auto" else "mesh"
+        peak = XGMI_LINK_DIR_GBPS * ((world - 1) if algo_name == "mesh" else 1)
+        roof = {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 1), "unit": "GB/s",
+                "frac": round(busbw / peak, 4), "traffic": None,
+                "kernel": "k_%s<Sum,%s>" % (algo_name, args.dtype),
+                "algorithmic_bytes_per_launch": int(2 * (world - 1) * S // world), "kernel_avg_ms": round(kern_ms, 4),
+                "frac_of_bidir_ring_roofline": round(busbw / BIDIR_RING_GBPS, 4)}
+        workload = "in-place allreduce(sum) of a %d MiB %s buffer per GPU, %s schedule" % (S >> 20, args.dtype,
+                                                                                        algo_name)
+        par = "dp%d (one process per GPU, xGMI P2P)" % world
+    out = {
+        "metric": "allreduce GB/s (device-resident fp32) at 1/2/4/8 GPUs; % xGMI roofline",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": {"float32": "f32", "float16": "f16", "bfloat16": "bf16", "float64": "f64"}[args.dtype],
+        "data": "synthetic (splitmix64 device generator, seed 0x5EED0000)",
+        "config": {"workload": workload, "bytes_per_gpu": S, "parallelism": par},
+        "algbw_GBps": round(algbw, 2),
+        "roofline": roof,
+        "cpu_baseline": cpu_baseline(S, args.cpu_seconds) if world == 1 else None,
+    }
+    if world > 1:
+        out["busbw_GBps"] = round(algbw * 2 * (world - 1) / world, 2)
+    if check is not None:
+        out["oracle_check"] = check
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        rdc_amd.finalize()
+
+
+if __name__ == "__main__":
+    main()

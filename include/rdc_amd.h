@@ -1,0 +1,120 @@
+/*
+ * rdc_amd.h — C ABI of the MI355X-native rdc allreduce path (librdc_amd.so).
+ *
+ * The reference ships NO C ABI: its Python package calls `_LIB.Rdc*` symbols
+ * that exist nowhere in src/ (SURVEY.md §0 finding 3).  The entry points below
+ * are exactly the ones those callers bind, with the signatures the call sites
+ * imply, plus device-resident extensions for the MI355X path.
+ * Plain pointers and sizes only; no torch types.
+ *
+ * Conventions
+ *   - every function returns 0 on success and a non-zero code on failure
+ *     (RdcGetLastError() then describes it), except the getters
+ *     RdcGetRank/RdcGetWorldSize/RdcIsDistributed/RdcCommRank/RdcCommSize;
+ *     the reference aborts via CHECK_F instead — the C++ header include/rdc.h
+ *     restores that behaviour on top of these codes.
+ *   - dtype: mpi::DataType (include/core/mpi.h:19-30) = rdc/core.py:160-169:
+ *       0 int8, 1 uint8, 2 int32, 3 uint32, 4 int64, 5 uint64, 6 float32,
+ *       7 float64, 8 long long, 9 unsigned long long
+ *     MI355X additions: 10 float16 (IEEE binary16), 11 bfloat16.
+ *   - op: mpi::OpType (include/core/mpi.h:12-17) = rdc/core.py:16-20:
+ *       0 MAX, 1 MIN, 2 SUM, 3 BITOR (integer dtypes only)
+ *   - results are bit-identical to the reference's CPU ring allreduce
+ *     (src/comm/communicator_collective.cc:115-203) on the same inputs.
+ */
+#ifndef RDC_AMD_H_
+#define RDC_AMD_H_
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ */
+/* Reference-bound entry points (the names rdc/core.py & rdc/comm.py call) */
+/* ------------------------------------------------------------------ */
+
+/* rdc::Init (include/rdc.h:58-61, include/core/rdc-inl.h:21-23;
+ * rdc/core.py:29-49 calls RdcInit(len(args), arr)).  argv entries of the form
+ * key=val override environment variables (communicator_manager.cc:87-104).
+ * Keys: RDC_RANK, RDC_WORLD_SIZE|rdc_world_size, RDC_TRACKER_URI,
+ * RDC_TRACKER_PORT, rdc_reduce_ring_mincount, RDC_DEVICE, RDC_SCRATCH_BYTES,
+ * RDC_ALGO (mesh|ring), RDC_NBLOCKS, RDC_TILE_BYTES, RDC_TIMEOUT.
+ * Falls back to torchrun's RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT
+ * (tracker port = MASTER_PORT+1).  Does not touch the GPU. */
+int RdcInit(int argc, char** argv);
+/* rdc::Finalize (include/rdc.h:75; rdc/core.py:52-57) */
+int RdcFinalize(void);
+/* rdc::GetRank / GetWorldSize / IsDistributed (include/rdc.h:76-80;
+ * rdc/core.py:66-87) */
+int RdcGetRank(void);
+int RdcGetWorldSize(void);
+int RdcIsDistributed(void);
+/* rdc::TrackerPrint (include/api.h:9; rdc/core.py:90-103) */
+int RdcTrackerPrint(const char* msg);
+/* rdc/core.py:106-118 */
+int RdcGetProcessorName(char* buf, unsigned long* out_len, unsigned long max_len);
+/* rdc::Barrier (include/api.h:14) */
+int RdcBarrier(void);
+
+/* rdc::Allreduce<OP,DType> (include/api.h:62-64, include/core/rdc-inl.h:125-135)
+ * on the "main" communicator; rdc/core.py:204-216 calls
+ * RdcAllreduce(ptr, size, dtype_enum, int(op), prepare_fun|NULL, NULL).
+ * sendrecv may be host or device memory (detected); synchronous, in place.
+ * prepare_fun(prepare_arg), when given, runs before the reduction. */
+int RdcAllreduce(void* sendrecv, size_t count, int dtype, int op, void (*prepare_fun)(void*),
+                 void* prepare_arg);
+/* rdc::Broadcast(void*, size, root) (include/api.h:23-24, rdc-inl.h:71-75;
+ * rdc/core.py:143-154).  Host or device memory; synchronous. */
+int RdcBroadcast(void* sendrecv, unsigned long size, int root);
+
+/* rdc::NewCommunicator / GetCommunicator (include/rdc.h:62-71;
+ * rdc/comm.py:398-427 calls RdcNewCommunicator(byref(handle), name)).
+ * NewCommunicator is collective over all ranks. */
+int RdcNewCommunicator(void** out, const char* name);
+int RdcGetCommunicator(void** out, const char* name);
+
+/* ------------------------------------------------------------------ */
+/* MI355X device-resident extensions                                    */
+/* ------------------------------------------------------------------ */
+
+/* In-place allreduce of device memory on `comm`, enqueued on `stream`
+ * (hipStream_t; NULL = default stream).  Asynchronous: errors raised inside
+ * the kernels (a peer that never joins) surface at RdcCommCheck. */
+int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op, void* stream);
+/* algo: 0 auto, 1 ring (the reference schedule), 2 mesh (all links) */
+int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream);
+int RdcCommBroadcast(void* comm, void* dev_buf, size_t bytes, int root, void* stream);
+/* synchronise `stream` and report any device-side collective failure */
+int RdcCommCheck(void* comm, void* stream);
+int RdcCommRank(void* comm);
+int RdcCommSize(void* comm);
+int RdcCommDevice(void* comm);
+/* 0 uncached, 1 fine-grained, 2 coarse-grained scratch */
+int RdcCommAllocKind(void* comm);
+
+/* Single process driving n ranks (devices[i] = HIP device of rank i; devices
+ * may repeat).  comms[i] receives rank i's handle.  scratch_bytes 0 = default. */
+int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes);
+/* Destroy a communicator (collective for communicators made by
+ * RdcNewCommunicator; local for RdcCommInitAll groups). */
+int RdcCommDestroy(void* comm);
+
+/* op::Reducer<OP,DType>(src, dst, count) (include/core/mpi.h:113-120) on
+ * device memory: dst[i] = OP::Reduce(dst[i], src[i]).  Stream-ordered. */
+int RdcReduce(void* dst, const void* src, size_t count, int dtype, int op, void* stream);
+/* Synthetic inputs: u = splitmix64(seed ^ (rank<<40) ^ i) mapped per dtype
+ * (identical to the CPU oracle's generator).  Stream-ordered. */
+int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, void* stream);
+
+/* Set a parameter (same keys as RdcInit argv). */
+int RdcSetParam(const char* name, const char* value);
+/* Description of the last failure on this thread ("" if none). */
+const char* RdcGetLastError(void);
+const char* RdcVersion(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RDC_AMD_H_ */

@@ -1,0 +1,75 @@
+"""Loader of the native library librdc_amd.so (built in-tree for gfx950).
+
+There is no CPU fallback: if the library is missing, importing the package
+fails loudly.  Build it with ``make -C rdc_amd/csrc`` (or
+``__graft_entry__.build()``).
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librdc_amd.so")
+
+
+def build(jobs=4):
+    """Compile librdc_amd.so with hipcc --offload-arch=gfx950."""
+    subprocess.check_call(["make", "-s", "-j%d" % jobs, "-C", os.path.join(HERE, "csrc")])
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "rdc_amd: native library %s is missing; build it with `make -C rdc_amd/csrc` "
+            "(the MI355X path has no CPU fallback)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    pvp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "RdcInit": (i, [i, ctypes.POINTER(ctypes.c_char_p)]),
+        "RdcFinalize": (i, []),
+        "RdcGetRank": (i, []),
+        "RdcGetWorldSize": (i, []),
+        "RdcIsDistributed": (i, []),
+        "RdcTrackerPrint": (i, [ctypes.c_char_p]),
+        "RdcGetProcessorName": (i, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_ulong), ctypes.c_ulong]),
+        "RdcBarrier": (i, []),
+        "RdcAllreduce": (i, [vp, sz, i, i, vp, vp]),
+        "RdcBroadcast": (i, [vp, ctypes.c_ulong, i]),
+        "RdcNewCommunicator": (i, [pvp, ctypes.c_char_p]),
+        "RdcGetCommunicator": (i, [pvp, ctypes.c_char_p]),
+        "RdcCommAllreduce": (i, [vp, vp, sz, i, i, vp]),
+        "RdcCommAllreduceEx": (i, [vp, vp, sz, i, i, i, vp]),
+        "RdcCommBroadcast": (i, [vp, vp, sz, i, vp]),
+        "RdcCommCheck": (i, [vp, vp]),
+        "RdcCommRank": (i, [vp]),
+        "RdcCommSize": (i, [vp]),
+        "RdcCommDevice": (i, [vp]),
+        "RdcCommAllocKind": (i, [vp]),
+        "RdcCommInitAll": (i, [pvp, i, ctypes.POINTER(ctypes.c_int), sz]),
+        "RdcCommDestroy": (i, [vp]),
+        "RdcReduce": (i, [vp, vp, sz, i, i, vp]),
+        "RdcFill": (i, [vp, sz, i, u64, i, vp]),
+        "RdcSetParam": (i, [ctypes.c_char_p, ctypes.c_char_p]),
+        "RdcGetLastError": (ctypes.c_char_p, []),
+        "RdcVersion": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+_LIB = _load()
+
+
+class RdcError(RuntimeError):
+    pass
+
+
+def check_call(rc):
+    """Raise RdcError with the library's message when rc != 0."""
+    if rc != 0:
+        raise RdcError(_LIB.RdcGetLastError().decode("utf-8", "replace"))
+    return rc

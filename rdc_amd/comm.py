@@ -1,0 +1,100 @@
+"""Communicator handles — rdc/comm.py's ``new_comm`` / ``get_comm`` / ``Comm``
+(rdc/comm.py:351-427) over the MI355X device path, plus single-process
+multi-rank groups (``init_group``) for driving several GPUs from one process.
+"""
+import ctypes
+
+from ._lib import _LIB, check_call
+from . import device as _dev
+
+ALGO_AUTO, ALGO_RING, ALGO_MESH = 0, 1, 2
+_ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "mesh": ALGO_MESH}
+
+
+class Comm(object):
+    """A communicator handle.  Collectives are in place on device memory and
+    stream-ordered (torch's current stream unless ``stream`` is given)."""
+    __slots__ = ("handle", "own_handle")
+
+    def __init__(self, handle=None, own_handle=False):
+        self.handle = ctypes.c_void_p(handle) if isinstance(handle, int) else (handle or ctypes.c_void_p())
+        self.own_handle = own_handle
+
+    @property
+    def rank(self):
+        return _LIB.RdcCommRank(self.handle)
+
+    @property
+    def world_size(self):
+        return _LIB.RdcCommSize(self.handle)
+
+    @property
+    def device(self):
+        return _LIB.RdcCommDevice(self.handle)
+
+    @property
+    def alloc_kind(self):
+        return _LIB.RdcCommAllocKind(self.handle)
+
+    def allreduce(self, tensor, op, algo="auto", stream=None):
+        """In-place allreduce of a contiguous ROCm tensor; returns it."""
+        _dev._check_tensor(tensor)
+        s = stream if stream is not None else _dev.current_stream_ptr(tensor.device)
+        check_call(_LIB.RdcCommAllreduceEx(self.handle, ctypes.c_void_p(tensor.data_ptr()), tensor.numel(),
+                                           _dev.dtype_enum(tensor.dtype), int(op), _ALGOS[algo], s))
+        return tensor
+
+    def allreduce_ptr(self, ptr, count, dtype, op, algo=ALGO_AUTO, stream=None):
+        check_call(_LIB.RdcCommAllreduceEx(self.handle, ctypes.c_void_p(ptr), count, dtype, int(op), algo,
+                                           stream))
+
+    def broadcast(self, tensor, root, stream=None):
+        _dev._check_tensor(tensor)
+        s = stream if stream is not None else _dev.current_stream_ptr(tensor.device)
+        check_call(_LIB.RdcCommBroadcast(self.handle, ctypes.c_void_p(tensor.data_ptr()),
+                                         tensor.numel() * tensor.element_size(), root, s))
+        return tensor
+
+    def check(self, stream=None):
+        """Synchronise the stream and raise if a device-side wait failed."""
+        if stream is None:
+            import torch
+            stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        check_call(_LIB.RdcCommCheck(self.handle, stream))
+
+    def destroy(self):
+        if self.handle:
+            check_call(_LIB.RdcCommDestroy(self.handle))
+            self.handle = ctypes.c_void_p()
+
+
+def new_comm(name):
+    """Create (collectively) the communicator ``name``."""
+    comm = Comm()
+    if isinstance(name, str):
+        name = name.encode("utf-8")
+    elif not isinstance(name, bytes):
+        raise TypeError("name must be a string or bytearray")
+    check_call(_LIB.RdcNewCommunicator(ctypes.byref(comm.handle), name))
+    return comm
+
+
+def get_comm(name="main"):
+    """Existing communicator ``name`` ("main" is created on first use)."""
+    comm = Comm()
+    if isinstance(name, str):
+        name = name.encode("utf-8")
+    elif not isinstance(name, bytes):
+        raise TypeError("name must be a string or bytearray")
+    check_call(_LIB.RdcGetCommunicator(ctypes.byref(comm.handle), name))
+    return comm
+
+
+def init_group(devices, scratch_bytes=0):
+    """Single-process group: one communicator per entry of ``devices``
+    (device ids may repeat).  Returns the list of Comm, rank i = devices[i]."""
+    n = len(devices)
+    handles = (ctypes.c_void_p * n)()
+    devs = (ctypes.c_int * n)(*devices)
+    check_call(_LIB.RdcCommInitAll(handles, n, devs, scratch_bytes))
+    return [Comm(ctypes.c_void_p(handles[i]), own_handle=True) for i in range(n)]

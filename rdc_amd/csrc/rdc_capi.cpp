@@ -1,0 +1,415 @@
+// C ABI of librdc_amd.so (include/rdc_amd.h) and the process-wide manager —
+// the counterpart of comm::CommunicatorManager (src/comm/communicator_manager.cc)
+// for the device path: parameters from env + argv (:87-115, :140-162), the
+// communicator registry (:164-193), and the host-memory entry points the
+// reference's Python package binds (rdc/core.py).
+#include <hip/hip_runtime_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/rdc_amd.h"
+#include "rdc_bootstrap.h"
+#include "rdc_comm.h"
+
+using namespace rdc_amd;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct Manager {
+    std::recursive_mutex mu;
+    bool inited = false;
+    int rank = 0, world = 1, device = -1;
+    std::string tracker_uri = "127.0.0.1";
+    int tracker_port = 29571;
+    size_t ring_mincount = 1;  // rdc_reduce_ring_mincount (communicator_manager.cc:46)
+    double bootstrap_timeout_s = 300.0;
+    CommConfig cfg;
+    std::unique_ptr<Bootstrap> bs;
+    std::map<std::string, std::unique_ptr<Communicator>> comms;
+    std::map<Communicator*, std::unique_ptr<Communicator>> groups;  // RdcCommInitAll handles
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
+    hipStream_t stream = nullptr;
+};
+
+Manager& M() {
+    static Manager* m = new Manager();  // never destroyed: may outlive HIP teardown
+    return *m;
+}
+
+// ParseUnit (src/comm/communicator_manager.cc:14-42): {integer}{B,K,M,G}
+size_t parse_unit(const char* v) {
+    char unit = 0;
+    unsigned long amt = 0;
+    int k = sscanf(v, "%lu%c", &amt, &unit);
+    if (k == 2) {
+        switch (unit) {
+            case 'B': return amt;
+            case 'K': return (size_t)amt << 10;
+            case 'M': return (size_t)amt << 20;
+            case 'G': return (size_t)amt << 30;
+            default: throw std::invalid_argument(std::string("rdc: bad size ") + v);
+        }
+    }
+    if (k == 1) return amt;
+    throw std::invalid_argument(std::string("rdc: bad size ") + v);
+}
+
+void set_param(Manager& m, const char* name, const char* val) {
+    std::string k(name);
+    if (k == "RDC_TRACKER_URI") m.tracker_uri = val;
+    else if (k == "RDC_TRACKER_PORT") m.tracker_port = atoi(val);
+    else if (k == "rdc_world_size" || k == "RDC_WORLD_SIZE") m.world = atoi(val);
+    else if (k == "RDC_RANK" || k == "rdc_rank") m.rank = atoi(val);
+    else if (k == "rdc_reduce_ring_mincount") m.ring_mincount = parse_unit(val);
+    else if (k == "RDC_DEVICE") m.device = atoi(val);
+    else if (k == "RDC_SCRATCH_BYTES" || k == "rdc_reduce_buffer") m.cfg.scratch_bytes = parse_unit(val);
+    else if (k == "RDC_ALGO") {
+        std::string v(val);
+        m.cfg.algo = v == "ring" ? RDC_ALGO_RING : v == "mesh" ? RDC_ALGO_MESH : RDC_ALGO_AUTO;
+    } else if (k == "RDC_NBLOCKS") m.cfg.max_blocks = atoi(val);
+    else if (k == "RDC_TILE_BYTES") m.cfg.tile_bytes = parse_unit(val);
+    else if (k == "RDC_TIMEOUT") m.cfg.timeout_s = atof(val);
+    else if (k == "RDC_BOOTSTRAP_TIMEOUT") m.bootstrap_timeout_s = atof(val);
+    // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
+    // to subsystems outside the device path and are accepted silently
+}
+
+void env_param(Manager& m, const char* name) {
+    const char* v = getenv(name);
+    if (v && *v) set_param(m, name, v);
+}
+
+template <typename F>
+int guard(F&& f) {
+    try {
+        f();
+        g_last_error.clear();
+        return 0;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+    } catch (...) {
+        g_last_error = "rdc: unknown error";
+    }
+    return 1;
+}
+
+void require_init(Manager& m) {
+    if (!m.inited) throw std::runtime_error("rdc: RdcInit has not been called");
+}
+
+int pick_device(Manager& m) {
+    if (m.device >= 0) return m.device;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        throw std::runtime_error("rdc: no HIP device visible (the MI355X path has no CPU fallback)");
+    const char* lr = getenv("LOCAL_RANK");
+    int d = lr ? atoi(lr) : m.rank;
+    m.device = d % ndev;
+    return m.device;
+}
+
+Communicator* get_comm(Manager& m, const std::string& name, bool create) {
+    auto it = m.comms.find(name);
+    if (it != m.comms.end()) return it->second.get();
+    if (!create) throw std::runtime_error("rdc: communicator '" + name + "' does not exist");
+    require_init(m);
+    Communicator* c = Communicator::Create(name, m.bs.get(), pick_device(m), m.cfg);
+    m.comms[name].reset(c);
+    return c;
+}
+
+Communicator* as_comm(void* h) {
+    if (!h) throw std::invalid_argument("rdc: null communicator handle");
+    return static_cast<Communicator*>(h);
+}
+
+bool is_device_pointer(const void* p) {
+    hipPointerAttribute_t attr;
+    memset(&attr, 0, sizeof(attr));
+    hipError_t e = hipPointerGetAttributes(&attr, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+hipStream_t manager_stream(Manager& m, int device) {
+    if (!m.stream) {
+        if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking) != hipSuccess)
+            throw std::runtime_error("rdc: cannot create stream");
+    }
+    return m.stream;
+}
+
+void* staging(Manager& m, size_t bytes, int device) {
+    if (bytes > m.stage_bytes) {
+        if (m.stage) (void)hipFree(m.stage);
+        m.stage = nullptr;
+        m.stage_bytes = 0;
+        (void)hipSetDevice(device);
+        if (hipMalloc(&m.stage, bytes) != hipSuccess) throw std::runtime_error("rdc: cannot allocate staging buffer");
+        m.stage_bytes = bytes;
+    }
+    return m.stage;
+}
+
+void hcheck(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("rdc: ") + what + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+extern "C" {
+
+int RdcInit(int argc, char** argv) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    if (m.inited) return 0;
+    return guard([&] {
+        // torchrun-style fallbacks first, rdc names override, argv overrides all
+        if (const char* v = getenv("RANK")) m.rank = atoi(v);
+        if (const char* v = getenv("WORLD_SIZE")) m.world = atoi(v);
+        if (const char* v = getenv("MASTER_ADDR")) m.tracker_uri = v;
+        if (const char* v = getenv("MASTER_PORT")) m.tracker_port = atoi(v) + 1;
+        static const char* keys[] = {"RDC_TRACKER_URI", "RDC_TRACKER_PORT", "RDC_WORLD_SIZE", "rdc_world_size",
+                                     "RDC_RANK", "rdc_reduce_ring_mincount", "RDC_DEVICE", "RDC_SCRATCH_BYTES",
+                                     "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
+                                     "RDC_BOOTSTRAP_TIMEOUT"};
+        for (const char* k : keys) env_param(m, k);
+        for (int i = 0; i < argc; ++i) {
+            if (!argv || !argv[i]) continue;
+            char name[256], val[256];
+            if (sscanf(argv[i], "%255[^=]=%255s", name, val) == 2) set_param(m, name, val);
+        }
+        if (m.world < 1 || m.rank < 0 || m.rank >= m.world)
+            throw std::invalid_argument("rdc: bad rank " + std::to_string(m.rank) + " / world " +
+                                        std::to_string(m.world));
+        if (m.world > RDC_MAX_RANKS) throw std::invalid_argument("rdc: world size exceeds 16");
+        m.bs.reset(new TcpBootstrap(m.rank, m.world, m.tracker_uri, m.tracker_port, m.bootstrap_timeout_s));
+        m.inited = true;
+    });
+}
+
+int RdcFinalize(void) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    if (!m.inited) return 0;
+    return guard([&] {
+        m.comms.clear();  // collective destroys (barriers) in name order on every rank
+        if (m.stage) (void)hipFree(m.stage);
+        m.stage = nullptr;
+        m.stage_bytes = 0;
+        if (m.stream) (void)hipStreamDestroy(m.stream);
+        m.stream = nullptr;
+        if (m.bs) m.bs->barrier();
+        m.bs.reset();
+        m.inited = false;
+        m.rank = 0;
+        m.world = 1;
+    });
+}
+
+int RdcGetRank(void) { return M().rank; }
+int RdcGetWorldSize(void) { return M().world; }
+int RdcIsDistributed(void) { return M().world > 1 ? 1 : 0; }
+
+int RdcTrackerPrint(const char* msg) {
+    fprintf(stderr, "[rdc rank %d] %s\n", M().rank, msg ? msg : "");
+    fflush(stderr);
+    return 0;
+}
+
+int RdcGetProcessorName(char* buf, unsigned long* out_len, unsigned long max_len) {
+    return guard([&] {
+        if (!buf || max_len == 0) throw std::invalid_argument("rdc: bad buffer");
+        char host[256] = {0};
+        gethostname(host, sizeof(host) - 1);
+        size_t n = strnlen(host, sizeof(host));
+        if (n >= max_len) n = max_len - 1;
+        memcpy(buf, host, n);
+        buf[n] = 0;
+        if (out_len) *out_len = n;
+    });
+}
+
+int RdcBarrier(void) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        require_init(m);
+        m.bs->barrier();
+    });
+}
+
+int RdcNewCommunicator(void** out, const char* name) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        if (!out || !name) throw std::invalid_argument("rdc: null argument");
+        *out = get_comm(m, name, true);
+    });
+}
+
+int RdcGetCommunicator(void** out, const char* name) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        if (!out) throw std::invalid_argument("rdc: null argument");
+        // the reference aborts on a missing name (communicator_manager.cc:190-193);
+        // "main" is created on first use instead
+        std::string n = name ? name : "main";
+        *out = get_comm(m, n, n == "main");
+    });
+}
+
+int RdcAllreduce(void* sendrecv, size_t count, int dtype, int op, void (*prepare_fun)(void*), void* prepare_arg) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        require_init(m);
+        if (prepare_fun) prepare_fun(prepare_arg);
+        const size_t esz = rdc_dtype_size(dtype);
+        if (esz == 0) throw std::invalid_argument("rdc: bad dtype " + std::to_string(dtype));
+        if (op < 0 || op >= RDC_OP_COUNT) throw std::invalid_argument("rdc: bad op " + std::to_string(op));
+        if (op == RDC_OP_BITOR && rdc_dtype_is_float(dtype))
+            throw std::invalid_argument("rdc: BITOR needs an integer dtype");
+        // world size 1: Communicator::Allreduce returns at once (communicator_base.h:133-138)
+        if (m.world == 1 || count == 0) return;
+        Communicator* c = get_comm(m, "main", true);
+        hipStream_t s = manager_stream(m, c->device());
+        if (is_device_pointer(sendrecv)) {
+            c->Allreduce(sendrecv, count, dtype, op, s);
+            c->Check(s);
+            return;
+        }
+        // host-resident buffer: H2D, device allreduce, D2H
+        const size_t bytes = count * esz;
+        void* d = staging(m, bytes, c->device());
+        hcheck(hipMemcpyAsync(d, sendrecv, bytes, hipMemcpyHostToDevice, s), "H2D");
+        c->Allreduce(d, count, dtype, op, s);
+        hcheck(hipMemcpyAsync(sendrecv, d, bytes, hipMemcpyDeviceToHost, s), "D2H");
+        c->Check(s);
+    });
+}
+
+int RdcBroadcast(void* sendrecv, unsigned long size, int root) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        require_init(m);
+        if (root < 0 || root >= m.world) throw std::invalid_argument("rdc: broadcast root out of range");
+        if (m.world == 1 || size == 0) return;
+        Communicator* c = get_comm(m, "main", true);
+        hipStream_t s = manager_stream(m, c->device());
+        if (is_device_pointer(sendrecv)) {
+            c->Broadcast(sendrecv, size, root, s);
+            c->Check(s);
+            return;
+        }
+        void* d = staging(m, size, c->device());
+        if (c->rank() == root) hcheck(hipMemcpyAsync(d, sendrecv, size, hipMemcpyHostToDevice, s), "H2D");
+        c->Broadcast(d, size, root, s);
+        if (c->rank() != root) hcheck(hipMemcpyAsync(sendrecv, d, size, hipMemcpyDeviceToHost, s), "D2H");
+        c->Check(s);
+    });
+}
+
+int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op, void* stream) {
+    return RdcCommAllreduceEx(comm, dev_buf, count, dtype, op, RDC_ALGO_AUTO, stream);
+}
+
+int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream) {
+    return guard([&] {
+        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_MESH) throw std::invalid_argument("rdc: bad algo");
+        as_comm(comm)->Allreduce(dev_buf, count, dtype, op, static_cast<hipStream_t>(stream), algo);
+    });
+}
+
+int RdcCommBroadcast(void* comm, void* dev_buf, size_t bytes, int root, void* stream) {
+    return guard([&] { as_comm(comm)->Broadcast(dev_buf, bytes, root, static_cast<hipStream_t>(stream)); });
+}
+
+int RdcCommCheck(void* comm, void* stream) {
+    return guard([&] { as_comm(comm)->Check(static_cast<hipStream_t>(stream)); });
+}
+
+int RdcCommRank(void* comm) { return comm ? static_cast<Communicator*>(comm)->rank() : -1; }
+int RdcCommSize(void* comm) { return comm ? static_cast<Communicator*>(comm)->size() : -1; }
+int RdcCommDevice(void* comm) { return comm ? static_cast<Communicator*>(comm)->device() : -1; }
+int RdcCommAllocKind(void* comm) { return comm ? static_cast<Communicator*>(comm)->alloc_kind() : -1; }
+
+int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        if (!comms || !devices) throw std::invalid_argument("rdc: null argument");
+        // parameters from the environment even without RdcInit
+        static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
+                                     "RDC_TIMEOUT"};
+        if (!m.inited)
+            for (const char* k : keys) env_param(m, k);
+        CommConfig cfg = m.cfg;
+        if (scratch_bytes) cfg.scratch_bytes = scratch_bytes;
+        std::vector<Communicator*> out;
+        Communicator::CreateGroup("group", n, devices, cfg, &out);
+        for (int i = 0; i < n; ++i) {
+            m.groups[out[(size_t)i]].reset(out[(size_t)i]);
+            comms[i] = out[(size_t)i];
+        }
+    });
+}
+
+int RdcCommDestroy(void* comm) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        Communicator* c = as_comm(comm);
+        auto g = m.groups.find(c);
+        if (g != m.groups.end()) {
+            m.groups.erase(g);
+            return;
+        }
+        for (auto it = m.comms.begin(); it != m.comms.end(); ++it) {
+            if (it->second.get() == c) {
+                m.comms.erase(it);
+                return;
+            }
+        }
+        throw std::invalid_argument("rdc: unknown communicator handle");
+    });
+}
+
+int RdcReduce(void* dst, const void* src, size_t count, int dtype, int op, void* stream) {
+    return guard([&] { DeviceReduce(dst, src, count, dtype, op, static_cast<hipStream_t>(stream)); });
+}
+
+int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, void* stream) {
+    return guard([&] { DeviceFill(dev_buf, count, dtype, seed, rank, static_cast<hipStream_t>(stream)); });
+}
+
+int RdcSetParam(const char* name, const char* value) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        if (!name || !value) throw std::invalid_argument("rdc: null argument");
+        set_param(m, name, value);
+    });
+}
+
+const char* RdcGetLastError(void) { return g_last_error.c_str(); }
+
+const char* RdcVersion(void) { return "rdc_amd 0.1 (gfx950)"; }
+
+}  // extern "C"

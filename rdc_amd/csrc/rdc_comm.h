@@ -1,0 +1,89 @@
+// Device communicator of the MI355X rdc path — the counterpart of the
+// reference's comm::Communicator (include/comm/communicator_base.h:37-283)
+// with its TCP link mesh replaced by IPC-mapped HBM scratch on every peer GPU.
+//
+// HBM layout per rank (one uncached allocation, IPC-exported):
+//   [ RS region : n slots x slot_bytes ][ AG region : n slots x slot_bytes ]
+// and a flag array (uncached, IPC-exported): uint32 [2][n][max_tiles].
+//   mesh : RS slot p  <- rank p's copy of my chunk;   AG slot c <- owner c's result
+//   ring : RS slot j  <- reduce-scatter step j;       AG slot j <- allgather step j
+//   bcast: the whole AG region holds the root's piece
+// Every launch carries seq (same on all ranks, +1 per launch); a flag word
+// equal to seq means "this tile of this launch has landed".
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "rdc_bootstrap.h"
+#include "rdc_common.h"
+
+namespace rdc_amd {
+
+struct CommConfig {
+    size_t scratch_bytes = (size_t)2 << 30;  // RS + AG regions, per rank
+    int algo = RDC_ALGO_AUTO;
+    int max_blocks = 0;                      // 0 = auto
+    size_t tile_bytes = 0;                   // 0 = auto
+    double timeout_s = 60.0;                 // device-side wait limit
+};
+
+class Communicator {
+public:
+    // Multi-process: one communicator per process, peers found through `bs`
+    // (collective over bs).
+    static Communicator* Create(const std::string& name, Bootstrap* bs, int device, const CommConfig& cfg);
+    // Single process driving n ranks (devices may repeat, e.g. n ranks on one GPU).
+    static void CreateGroup(const std::string& name, int n, const int* devices, const CommConfig& cfg,
+                            std::vector<Communicator*>* out);
+    ~Communicator();
+
+    // in-place device allreduce, stream-ordered; returns hipError_t-style code
+    void Allreduce(void* buf, size_t count, int dtype, int op, hipStream_t stream, int algo = RDC_ALGO_AUTO);
+    void Broadcast(void* buf, size_t bytes, int root, hipStream_t stream);
+    // waits for `stream`, then reads the device error word; throws on error
+    void Check(hipStream_t stream);
+
+    int rank() const { return rank_; }
+    int size() const { return n_; }
+    int device() const { return device_; }
+    const std::string& name() const { return name_; }
+    int alloc_kind() const { return alloc_kind_; }  // 0 uncached, 1 fine-grained, 2 coarse
+    size_t slot_bytes() const { return slot_bytes_; }
+    uint32_t seq() const { return seq_; }
+    const CommConfig& config() const { return cfg_; }
+    // plan introspection for tests: tile bytes and grid the next allreduce of
+    // `piece_chunk_bytes` per chunk would use
+    void Plan(size_t chunk_bytes, int algo, size_t* tile, int* nb_s, int* nb_r, int* nb_g) const;
+
+private:
+    Communicator() {}
+    void AllocLocal();
+    void FillArgsCommon(CollArgs* a) const;
+    int PickAlgo(int algo) const;
+
+    std::string name_;
+    int rank_ = 0, n_ = 1, device_ = 0;
+    CommConfig cfg_;
+    Bootstrap* bs_ = nullptr;       // not owned
+    bool owns_peers_ipc_ = false;   // peers opened through IPC
+    char* scratch_ = nullptr;
+    uint32_t* flags_ = nullptr;
+    uint32_t* err_ = nullptr;
+    size_t slot_bytes_ = 0, region_bytes_ = 0, flag_bytes_ = 0;
+    uint32_t max_tiles_ = 0;
+    uint32_t seq_ = 0;
+    int alloc_kind_ = 0;
+    int num_cus_ = 256;
+    int wall_khz_ = 100000;         // wall_clock64() rate
+    char* peer_scratch_[RDC_MAX_RANKS] = {};
+    uint32_t* peer_flags_[RDC_MAX_RANKS] = {};
+};
+
+// op::Reducer<OP,DType> on device: dst = OP(dst, src) element-wise
+void DeviceReduce(void* dst, const void* src, size_t count, int dtype, int op, hipStream_t stream, int grid = 0);
+void DeviceFill(void* buf, size_t count, int dtype, uint64_t seed, int rank, hipStream_t stream);
+
+}  // namespace rdc_amd

@@ -1,0 +1,82 @@
+// Shared host/device definitions for the MI355X rdc allreduce path.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+// mpi::DataType (include/core/mpi.h:19-30) + MI355X-build additions
+enum {
+    RDC_DT_INT8 = 0,
+    RDC_DT_UINT8 = 1,
+    RDC_DT_INT32 = 2,
+    RDC_DT_UINT32 = 3,
+    RDC_DT_INT64 = 4,
+    RDC_DT_UINT64 = 5,
+    RDC_DT_FLOAT32 = 6,
+    RDC_DT_FLOAT64 = 7,
+    RDC_DT_LONGLONG = 8,
+    RDC_DT_ULONGLONG = 9,
+    RDC_DT_FLOAT16 = 10,
+    RDC_DT_BFLOAT16 = 11,
+    RDC_DT_COUNT = 12
+};
+// mpi::OpType (include/core/mpi.h:12-17)
+enum { RDC_OP_MAX = 0, RDC_OP_MIN = 1, RDC_OP_SUM = 2, RDC_OP_BITOR = 3, RDC_OP_COUNT = 4 };
+
+// allreduce data-movement schedules
+enum {
+    RDC_ALGO_AUTO = 0,
+    RDC_ALGO_RING = 1,  // the reference's ring: n-1 reduce-scatter + n-1 allgather steps
+    RDC_ALGO_MESH = 2   // direct all-links exchange, same per-chunk accumulation order
+};
+
+#define RDC_MAX_RANKS 16
+#define RDC_SLOT_ALIGN 256         // scratch images keep the user buffer's address mod 256
+#define RDC_MIN_TILE (16u << 10)   // smallest tile, bytes
+
+// device error codes written to the communicator's error word
+enum {
+    RDC_KERR_NONE = 0,
+    RDC_KERR_TIMEOUT_RS = 1,
+    RDC_KERR_TIMEOUT_AG = 2,
+    RDC_KERR_TIMEOUT_BCAST = 3,
+    RDC_KERR_TIMEOUT_RING = 4
+};
+
+static inline size_t rdc_dtype_size(int dtype) {
+    switch (dtype) {
+        case RDC_DT_INT8: case RDC_DT_UINT8: return 1;
+        case RDC_DT_INT32: case RDC_DT_UINT32: case RDC_DT_FLOAT32: return 4;
+        case RDC_DT_INT64: case RDC_DT_UINT64: case RDC_DT_FLOAT64:
+        case RDC_DT_LONGLONG: case RDC_DT_ULONGLONG: return 8;
+        case RDC_DT_FLOAT16: case RDC_DT_BFLOAT16: return 2;
+        default: return 0;
+    }
+}
+static inline int rdc_dtype_is_float(int dtype) {
+    return dtype == RDC_DT_FLOAT32 || dtype == RDC_DT_FLOAT64 || dtype == RDC_DT_FLOAT16 ||
+           dtype == RDC_DT_BFLOAT16;
+}
+
+// Everything one collective launch needs.  Passed by value as the kernel
+// argument (< 1.5 KiB).  Peer pointers are IPC-mapped (multi-process) or
+// direct (single-process); index [rank] is the local one.
+struct CollArgs {
+    char* user;                          // local in-place buffer (byte 0 of the whole buffer)
+    int n;                               // ranks
+    int rank;
+    uint32_t seq;                        // launch sequence number, same on every rank
+    int root;                            // broadcast root
+    uint64_t tile_bytes;                 // multiple of RDC_SLOT_ALIGN
+    int tiles[RDC_MAX_RANKS];            // tiles in chunk c for this launch
+    uint64_t off[RDC_MAX_RANKS];         // byte offset of chunk c's piece in `user`
+    uint64_t len[RDC_MAX_RANKS];         // byte length of chunk c's piece
+    uint32_t mis[RDC_MAX_RANKS];         // (user + off[c]) % RDC_SLOT_ALIGN
+    uint64_t slot_bytes;                 // scratch slot stride
+    uint32_t max_tiles;                  // flag array row stride
+    char* rs[RDC_MAX_RANKS];             // rank p's reduce-scatter scratch region
+    char* ag[RDC_MAX_RANKS];             // rank p's allgather scratch region
+    uint32_t* flags[RDC_MAX_RANKS];      // rank p's flag region: [2][n][max_tiles]
+    int nb_scatter, nb_reduce, nb_gather;  // mesh block roles
+    uint32_t* err;                       // local device error word
+    uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up
+};

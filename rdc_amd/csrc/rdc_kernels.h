@@ -1,0 +1,20 @@
+// Host-visible launchers of the gfx950 kernels (rdc_kernels.hip).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include "rdc_common.h"
+
+namespace rdc_amd {
+
+struct KernelSet {
+    hipError_t (*reduce)(char* dst, const char* src, uint64_t nbytes, int grid, hipStream_t s);
+    hipError_t (*mesh)(const CollArgs& a, int grid, hipStream_t s);
+    hipError_t (*ring)(const CollArgs& a, int grid, hipStream_t s);
+};
+
+// false if (dtype, op) is not a valid reference combination
+bool get_kernels(int dtype, int op, KernelSet* ks);
+hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s);
+hipError_t launch_fill(void* buf, uint64_t count, int dtype, uint64_t seed, int rank, hipStream_t s);
+
+}  // namespace rdc_amd

@@ -1,0 +1,69 @@
+"""One rank of a multi-process GPU parity run (spawned by tests/test_gpu_allreduce.py).
+
+argv: rank world port outdir cases_json.  Every case: device-side synthetic
+input (RdcFill, seed/rank) -> collective on the given communicator ->
+bytes saved to outdir/case<i>_rank<r>.npy for the parent to check against
+the CPU oracle.  All ranks share GPU 0 (RDC_DEVICE=0) on the 1-GPU box.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    rank, world, port, outdir, cases = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
+    cases = json.loads(open(cases).read())
+    import torch
+    import rdc_amd
+    from rdc_amd._lib import _LIB, check_call
+    rdc_amd.init(["RDC_RANK=%d" % rank, "RDC_WORLD_SIZE=%d" % world, "RDC_TRACKER_PORT=%d" % port,
+                  "RDC_TRACKER_URI=127.0.0.1", "RDC_DEVICE=%s" % os.environ.get("RDC_DEVICE", "0")])
+    torch.cuda.set_device(int(os.environ.get("RDC_DEVICE", "0")))
+    comms = {}
+    esz = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 4, 7: 8, 8: 8, 9: 8, 10: 2, 11: 2}
+    stream = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    for i, c in enumerate(cases):
+        name = c.get("comm", "main")
+        if name not in comms:
+            comms[name] = rdc_amd.new_comm(name) if name != "main" else rdc_amd.get_comm("main")
+        comm = comms[name]
+        kind = c.get("kind", "allreduce")
+        count, dtype = c["count"], c["dtype"]
+        pad = c.get("pad", 0)
+        nbytes = count * esz[dtype]
+        buf = torch.zeros(nbytes + pad + 64, dtype=torch.uint8, device="cuda")
+        p = buf.data_ptr() + pad
+        check_call(_LIB.RdcFill(ctypes.c_void_p(p), count, dtype, c.get("seed", 0x5EED0000), rank, sp))
+        reps = c.get("reps", 1)
+        for _ in range(reps):
+            if kind == "allreduce":
+                check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(p), count, dtype, c["op"],
+                                                   c.get("algo", 0), sp))
+            elif kind == "broadcast":
+                check_call(_LIB.RdcCommBroadcast(comm.handle, ctypes.c_void_p(p), nbytes, c["root"], sp))
+            elif kind == "host_allreduce":
+                host = buf[pad: pad + nbytes].cpu().numpy().copy()
+                check_call(_LIB.RdcAllreduce(host.ctypes.data_as(ctypes.c_void_p), count, dtype, c["op"], None,
+                                             None))
+                buf[pad: pad + nbytes] = torch.from_numpy(host).cuda()
+        comm.check(sp)
+        out = buf[pad: pad + nbytes].cpu().numpy()
+        if c.get("digest"):
+            import hashlib
+            open(os.path.join(outdir, "case%d_rank%d.sha" % (i, rank)), "w").write(
+                hashlib.sha256(out.tobytes()).hexdigest())
+        else:
+            np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
+        print("rank %d case %d ok" % (rank, i), flush=True)
+    rdc_amd.finalize()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,184 @@
+"""GPU parity of the device allreduce / broadcast against the CPU oracle
+(the reference's ring, bit-exact), through the C ABI.
+
+* single-process groups: n communicators on GPU 0, one stream each;
+* multi-process: n processes on GPU 0 exchanging HIP IPC handles over the
+  TCP bootstrap — the same code path as one process per GPU on an 8-GPU node.
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.conftest import ROOT, free_port
+from tests.gpu_util import VALID, from_dev, ptr, rand_input, same_bits, to_dev
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def group3():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import rdc_amd
+    comms = rdc_amd.init_group([0, 0, 0], scratch_bytes=24 << 20)
+    yield comms
+    for c in comms:
+        c.destroy()
+
+
+@pytest.fixture(scope="module")
+def group2():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import rdc_amd
+    comms = rdc_amd.init_group([0, 0], scratch_bytes=16 << 20)
+    yield comms
+    for c in comms:
+        c.destroy()
+
+
+def run_group(comms, inputs, dtype, op, algo, pads=None):
+    """Launch every rank's allreduce on its own stream, then collect."""
+    from rdc_amd._lib import _LIB
+    import ctypes
+    n = len(comms)
+    count = inputs[0].size
+    pads = pads or [0] * n
+    esz = np.dtype(O.NP_DTYPE[dtype]).itemsize
+    bufs = [to_dev(x, p * esz) for x, p in zip(inputs, pads)]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    torch.cuda.synchronize()
+    for r in range(n):
+        rc = _LIB.RdcCommAllreduceEx(comms[r].handle, ptr(bufs[r], pads[r] * esz), count, dtype, op, algo,
+                                     ctypes.c_void_p(streams[r].cuda_stream))
+        assert rc == 0, _LIB.RdcGetLastError()
+    for r in range(n):
+        comms[r].check(ctypes.c_void_p(streams[r].cuda_stream))
+    return [from_dev(bufs[r], pads[r] * esz, count, dtype) for r in range(n)]
+
+
+@pytest.mark.parametrize("algo", [1, 2])
+@pytest.mark.parametrize("dtype,op", VALID)
+def test_group3_all_types(group3, dtype, op, algo):
+    rng = np.random.default_rng(77 + dtype * 8 + op)
+    for count in (1, 2, 5, 1001, 4099):
+        inputs = [rand_input(rng, count, dtype) for _ in range(3)]
+        want = O.expected_allreduce(inputs, dtype, op)
+        got = run_group(group3, inputs, dtype, op, algo, pads=[1, 0, 3])
+        for r in range(3):
+            assert same_bits(got[r], want, dtype), (dtype, op, algo, count, r)
+
+
+@pytest.mark.parametrize("algo", [1, 2])
+def test_group_multi_piece(group2, algo):
+    """Buffers larger than the scratch go through several launches (pieces)."""
+    rng = np.random.default_rng(5)
+    count = (6 << 20) // 4 * 3 + 7   # 18 MiB fp32 > 2 x 4 MiB slots
+    inputs = [rng.standard_normal(count).astype(np.float32) for _ in range(2)]
+    want = O.expected_allreduce(inputs, O.DT_FLOAT32, O.OP_SUM)
+    got = run_group(group2, inputs, O.DT_FLOAT32, O.OP_SUM, algo, pads=[0, 5])
+    for r in range(2):
+        assert same_bits(got[r], want, O.DT_FLOAT32)
+
+
+def test_group_repeated_calls(group3):
+    """seq-numbered flags: many back-to-back launches on the same communicator."""
+    rng = np.random.default_rng(9)
+    for it in range(20):
+        count = int(rng.integers(1, 70000))
+        algo = 1 + it % 2
+        inputs = [rng.standard_normal(count).astype(np.float32) for _ in range(3)]
+        want = O.expected_allreduce(inputs, O.DT_FLOAT32, O.OP_SUM)
+        got = run_group(group3, inputs, O.DT_FLOAT32, O.OP_SUM, algo)
+        for r in range(3):
+            assert same_bits(got[r], want, O.DT_FLOAT32), (it, count, algo)
+
+
+def test_group_broadcast(group3):
+    import ctypes
+    from rdc_amd._lib import _LIB
+    rng = np.random.default_rng(3)
+    for root in range(3):
+        for nbytes in (1, 100, 1 << 20 | 3):
+            data = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(3)]
+            bufs = [to_dev(d, 1) for d in data]
+            streams = [torch.cuda.Stream() for _ in range(3)]
+            torch.cuda.synchronize()
+            for r in range(3):
+                assert _LIB.RdcCommBroadcast(group3[r].handle, ptr(bufs[r], 1), nbytes, root,
+                                             ctypes.c_void_p(streams[r].cuda_stream)) == 0
+            for r in range(3):
+                group3[r].check(ctypes.c_void_p(streams[r].cuda_stream))
+                assert from_dev(bufs[r], 1, nbytes, O.DT_UINT8).tobytes() == data[root].tobytes()
+
+
+# --------------------------------------------------------------- multi-process
+def run_mp(world, cases, timeout=240, env_extra=None):
+    tmp = tempfile.mkdtemp(prefix="rdc_mp_")
+    cf = os.path.join(tmp, "cases.json")
+    with open(cf, "w") as f:
+        json.dump(cases, f)
+    port = free_port()
+    env = dict(os.environ)
+    env.update({"RDC_DEVICE": "0", "RDC_NBLOCKS": env.get("RDC_NBLOCKS", "32"), "RDC_SCRATCH_BYTES": "64M"})
+    env.update(env_extra or {})
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), str(r), str(world),
+                               str(port), tmp, cf], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out.decode(errors="replace"))
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r][-3000:])
+    return tmp
+
+
+def expected_for(case, world):
+    dt = case["dtype"]
+    inputs = [O.fill(case["count"], dt, case.get("seed", 0x5EED0000), r) for r in range(world)]
+    kind = case.get("kind", "allreduce")
+    if kind == "broadcast":
+        return [inputs[case["root"]]] * world
+    bufs = [x.copy() for x in inputs]
+    for _ in range(case.get("reps", 1)):
+        O.allreduce_ring(bufs, dt, case["op"])
+    return bufs
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_mp_allreduce(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [
+        {"count": 1, "dtype": 6, "op": 2},
+        {"count": 1001, "dtype": 6, "op": 2, "algo": 2, "pad": 4},
+        {"count": 1001, "dtype": 6, "op": 2, "algo": 1, "pad": 8},
+        {"count": 4099, "dtype": 2, "op": 0},
+        {"count": 1 << 20, "dtype": 10, "op": 2},
+        {"count": 3 << 20, "dtype": 7, "op": 1, "algo": 1},
+        {"count": 5 << 20, "dtype": 6, "op": 2, "algo": 2},     # 20 MiB > scratch: 2 pieces
+        {"count": 77777, "dtype": 1, "op": 3, "comm": "second"},
+        {"count": 70000, "dtype": 11, "op": 2, "reps": 3},
+        {"count": 123457, "dtype": 0, "kind": "broadcast", "root": world - 1},
+        {"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"},
+    ]
+    tmp = run_mp(world, cases)
+    for i, c in enumerate(cases):
+        want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            exp = np.frombuffer(want[r].tobytes(), dtype=np.uint8)
+            assert got.tobytes() == exp.tobytes(), (i, c, r)
