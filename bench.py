@@ -103,7 +103,7 @@ def main():
     dt_enum, esz = DTYPES[args.dtype]
     count = args.bytes // esz
     S = count * esz
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % torch.cuda.device_count())
     tdtype = getattr(torch, args.dtype)
     stream = torch.cuda.current_stream()
     sp = ctypes.c_void_p(stream.cuda_stream)

@@ -18,6 +18,14 @@ def build(jobs=4):
 
 
 def _load():
+    # torch wheels bundle their own libamdhip64 (soname libamdhip64.so.7, but
+    # linked by the name libamdhip64.so).  Import torch first so this library
+    # binds to the runtime torch already loaded; loading ours first would put
+    # two HIP runtimes in one process.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             "rdc_amd: native library %s is missing; build it with `make -C rdc_amd/csrc` "

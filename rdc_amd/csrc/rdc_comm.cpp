@@ -1,6 +1,8 @@
 // Device communicator (see rdc_comm.h).
 #include "rdc_comm.h"
 
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -60,8 +62,17 @@ void* alloc_shared(size_t bytes, int* kind) {
     return p;
 }
 
+void dbg(const char* fmt, int rank, const char* what) {
+    static const bool on = getenv("RDC_DEBUG") != nullptr;
+    if (on) {
+        fprintf(stderr, fmt, rank, what);
+        fflush(stderr);
+    }
+}
+
 struct PeerInfo {
     hipIpcMemHandle_t scratch;
+    hipIpcMemHandle_t ag;
     hipIpcMemHandle_t flags;
     int32_t device;
     int32_t pid;
@@ -76,16 +87,21 @@ struct PeerInfo {
 
 void Communicator::AllocLocal() {
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    size_t slot = round_down(cfg_.scratch_bytes / (2 * (size_t)n_), 4096);
+    // RS and AG regions are separate allocations, each below 2 GiB: on ROCm
+    // 7.2 (dmabuf IPC) hipIpcOpenMemHandle of an allocation >= 2 GiB never
+    // returns (measured: 2044 MiB opens, 2048 MiB hangs).
+    size_t region = std::min<size_t>(cfg_.scratch_bytes / 2, kMaxRegionBytes);
+    size_t slot = round_down(region / (size_t)n_, 4096);
     if (slot < 64 * 1024 || n_ == 1) slot = 64 * 1024;  // world size 1 never moves data
     slot_bytes_ = slot;
     region_bytes_ = slot * (size_t)n_;
     max_tiles_ = (uint32_t)(region_bytes_ / RDC_MIN_TILE + 2);
     flag_bytes_ = round_up((size_t)2 * n_ * max_tiles_ * sizeof(uint32_t), 4096);
-    int k1 = 0, k2 = 0;
-    scratch_ = static_cast<char*>(alloc_shared(2 * region_bytes_, &k1));
+    int k1 = 0, k2 = 0, k3 = 0;
+    scratch_ = static_cast<char*>(alloc_shared(region_bytes_, &k1));
+    scratch_ag_ = static_cast<char*>(alloc_shared(region_bytes_, &k3));
     flags_ = static_cast<uint32_t*>(alloc_shared(flag_bytes_, &k2));
-    alloc_kind_ = std::max(k1, k2);
+    alloc_kind_ = std::max(std::max(k1, k2), k3);
     hip_check(hipMalloc(&err_, 64), "hipMalloc err");
     hip_check(hipMemset(flags_, 0, flag_bytes_), "memset flags");
     hip_check(hipMemset(err_, 0, 64), "memset err");
@@ -98,6 +114,7 @@ void Communicator::AllocLocal() {
         wclk = 100000;
     wall_khz_ = wclk;
     peer_scratch_[rank_] = scratch_;
+    peer_ag_[rank_] = scratch_ag_;
     peer_flags_[rank_] = flags_;
 }
 
@@ -110,11 +127,14 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     c->cfg_ = cfg;
     c->bs_ = bs;
     if (c->n_ > RDC_MAX_RANKS) throw std::runtime_error("rdc: world size exceeds RDC_MAX_RANKS");
+    dbg("[rdc %d] %s\n", c->rank_, "alloc");
     c->AllocLocal();
+    dbg("[rdc %d] %s\n", c->rank_, "alloc done");
 
     PeerInfo mine;
     memset(&mine, 0, sizeof(mine));
     hip_check(hipIpcGetMemHandle(&mine.scratch, c->scratch_), "hipIpcGetMemHandle(scratch)");
+    hip_check(hipIpcGetMemHandle(&mine.ag, c->scratch_ag_), "hipIpcGetMemHandle(ag)");
     hip_check(hipIpcGetMemHandle(&mine.flags, c->flags_), "hipIpcGetMemHandle(flags)");
     mine.device = device;
     mine.pid = (int32_t)getpid();
@@ -123,7 +143,9 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     mine.max_tiles = c->max_tiles_;
     gethostname(mine.host, sizeof(mine.host) - 1);
     std::vector<PeerInfo> all((size_t)c->n_);
+    dbg("[rdc %d] %s\n", c->rank_, "handles exported");
     bs->allgather(&mine, sizeof(mine), all.data());
+    dbg("[rdc %d] %s\n", c->rank_, "handles exchanged");
     for (int p = 0; p < c->n_; ++p) {
         if (all[(size_t)p].slot_bytes != mine.slot_bytes || all[(size_t)p].max_tiles != mine.max_tiles)
             throw std::runtime_error("rdc: ranks disagree on scratch size (set RDC_SCRATCH_BYTES identically)");
@@ -146,14 +168,19 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     for (int p = 0; p < c->n_; ++p) {
         if (p == c->rank_) continue;
         void* ps = nullptr;
+        void* pa = nullptr;
         void* pf = nullptr;
         hip_check(hipIpcOpenMemHandle(&ps, all[(size_t)p].scratch, hipIpcMemLazyEnablePeerAccess),
                   "hipIpcOpenMemHandle(scratch)");
+        hip_check(hipIpcOpenMemHandle(&pa, all[(size_t)p].ag, hipIpcMemLazyEnablePeerAccess),
+                  "hipIpcOpenMemHandle(ag)");
+        c->peer_ag_[p] = static_cast<char*>(pa);
         hip_check(hipIpcOpenMemHandle(&pf, all[(size_t)p].flags, hipIpcMemLazyEnablePeerAccess),
                   "hipIpcOpenMemHandle(flags)");
         c->peer_scratch_[p] = static_cast<char*>(ps);
         c->peer_flags_[p] = static_cast<uint32_t*>(pf);
     }
+    dbg("[rdc %d] %s\n", c->rank_, "peers mapped");
     c->owns_peers_ipc_ = true;
     bs->barrier();
     return c.release();
@@ -176,6 +203,7 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
     for (int i = 0; i < n; ++i) {
         for (int j = 0; j < n; ++j) {
             cs[(size_t)i]->peer_scratch_[j] = cs[(size_t)j]->scratch_;
+            cs[(size_t)i]->peer_ag_[j] = cs[(size_t)j]->scratch_ag_;
             cs[(size_t)i]->peer_flags_[j] = cs[(size_t)j]->flags_;
             if (devices[i] != devices[j]) {
                 int can = 0;
@@ -201,6 +229,7 @@ Communicator::~Communicator() {
         for (int p = 0; p < n_; ++p)
             if (p != rank_) {
                 if (peer_scratch_[p]) (void)hipIpcCloseMemHandle(peer_scratch_[p]);
+                if (peer_ag_[p]) (void)hipIpcCloseMemHandle(peer_ag_[p]);
                 if (peer_flags_[p]) (void)hipIpcCloseMemHandle(peer_flags_[p]);
             }
         try {
@@ -209,6 +238,7 @@ Communicator::~Communicator() {
         }
     }
     if (scratch_) (void)hipFree(scratch_);
+    if (scratch_ag_) (void)hipFree(scratch_ag_);
     if (flags_) (void)hipFree(flags_);
     if (err_) (void)hipFree(err_);
 }
@@ -227,7 +257,7 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     a->max_tiles = max_tiles_;
     for (int p = 0; p < n_; ++p) {
         a->rs[p] = peer_scratch_[p];
-        a->ag[p] = peer_scratch_[p] + region_bytes_;
+        a->ag[p] = peer_ag_[p];
         a->flags[p] = peer_flags_[p];
     }
     a->err = err_;
@@ -294,7 +324,8 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
                 a.off[c] = 0;
                 a.len[c] = 0;
             }
-            a.mis[c] = (uint32_t)(((uintptr_t)user + a.off[c]) % RDC_SLOT_ALIGN);
+            // buffer-relative: every rank places chunk c's bytes identically
+            a.mis[c] = (uint32_t)(a.off[c] % 16);
             chunk_max = std::max<size_t>(chunk_max, a.len[c]);
         }
         size_t tile;
@@ -329,7 +360,7 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
         a.root = root;
         a.off[0] = off;
         a.len[0] = std::min(cap, bytes - off);
-        a.mis[0] = (uint32_t)(((uintptr_t)user + off) % RDC_SLOT_ALIGN);
+        a.mis[0] = (uint32_t)(off % 16);
         size_t tile = cfg_.tile_bytes ? cfg_.tile_bytes
                                       : std::min<size_t>(std::max<size_t>(a.len[0] / (size_t)G, RDC_MIN_TILE),
                                                          (size_t)1 << 20);
@@ -365,9 +396,9 @@ void DeviceReduce(void* dst, const void* src, size_t count, int dtype, int op, h
         throw std::invalid_argument("rdc: buffer not aligned to its element size");
     if (count == 0) return;
     const uint64_t nbytes = (uint64_t)count * esz;
-    if (grid <= 0) {
-        const uint64_t want = (nbytes / 16 + 256 * 4 - 1) / (256 * 4);
-        grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, 2048));
+    if (grid <= 0) {  // >= 4 KiB per block, at most 4096 blocks (16 per CU)
+        const uint64_t want = (nbytes + 4095) / 4096;
+        grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, 4096));
     }
     hip_check(ks.reduce(static_cast<char*>(dst), static_cast<const char*>(src), nbytes, grid, stream),
               "launch reduce");

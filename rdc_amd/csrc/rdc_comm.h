@@ -2,8 +2,8 @@
 // reference's comm::Communicator (include/comm/communicator_base.h:37-283)
 // with its TCP link mesh replaced by IPC-mapped HBM scratch on every peer GPU.
 //
-// HBM layout per rank (one uncached allocation, IPC-exported):
-//   [ RS region : n slots x slot_bytes ][ AG region : n slots x slot_bytes ]
+// HBM layout per rank (uncached allocations, IPC-exported, each < 2 GiB):
+//   RS region : n slots x slot_bytes      AG region : n slots x slot_bytes
 // and a flag array (uncached, IPC-exported): uint32 [2][n][max_tiles].
 //   mesh : RS slot p  <- rank p's copy of my chunk;   AG slot c <- owner c's result
 //   ring : RS slot j  <- reduce-scatter step j;       AG slot j <- allgather step j
@@ -23,7 +23,7 @@
 namespace rdc_amd {
 
 struct CommConfig {
-    size_t scratch_bytes = (size_t)2 << 30;  // RS + AG regions, per rank
+    size_t scratch_bytes = (size_t)4080 << 20;  // RS + AG regions (2 x 2040 MiB), per rank
     int algo = RDC_ALGO_AUTO;
     int max_blocks = 0;                      // 0 = auto
     size_t tile_bytes = 0;                   // 0 = auto
@@ -69,7 +69,9 @@ private:
     CommConfig cfg_;
     Bootstrap* bs_ = nullptr;       // not owned
     bool owns_peers_ipc_ = false;   // peers opened through IPC
-    char* scratch_ = nullptr;
+    static constexpr size_t kMaxRegionBytes = (size_t)2040 << 20;
+    char* scratch_ = nullptr;       // RS region
+    char* scratch_ag_ = nullptr;    // AG region
     uint32_t* flags_ = nullptr;
     uint32_t* err_ = nullptr;
     size_t slot_bytes_ = 0, region_bytes_ = 0, flag_bytes_ = 0;
@@ -79,6 +81,7 @@ private:
     int num_cus_ = 256;
     int wall_khz_ = 100000;         // wall_clock64() rate
     char* peer_scratch_[RDC_MAX_RANKS] = {};
+    char* peer_ag_[RDC_MAX_RANKS] = {};
     uint32_t* peer_flags_[RDC_MAX_RANKS] = {};
 };
 

@@ -70,7 +70,7 @@ struct CollArgs {
     int tiles[RDC_MAX_RANKS];            // tiles in chunk c for this launch
     uint64_t off[RDC_MAX_RANKS];         // byte offset of chunk c's piece in `user`
     uint64_t len[RDC_MAX_RANKS];         // byte length of chunk c's piece
-    uint32_t mis[RDC_MAX_RANKS];         // (user + off[c]) % RDC_SLOT_ALIGN
+    uint32_t mis[RDC_MAX_RANKS];         // off[c] % 16: scratch image alignment (rank-independent)
     uint64_t slot_bytes;                 // scratch slot stride
     uint32_t max_tiles;                  // flag array row stride
     char* rs[RDC_MAX_RANKS];             // rank p's reduce-scatter scratch region

@@ -179,14 +179,16 @@ __device__ __forceinline__ bool block_wait(uint32_t* const* flags, int nflags, u
 }
 
 // ------------------------------------------------------ block-wide moves ----
-// All three helpers take byte ranges [0,len) whose base addresses are
-// congruent mod 16 (the library places every scratch image at the user
-// buffer's alignment), so the middle runs as 16-byte lanes and only the
-// <16-byte head/tail is handled element-wise.
+// Byte ranges [0,len).  Scratch images sit at the buffer-relative alignment
+// (offset % 16), so they are congruent with the user buffer whenever the
+// user pointer is 16-B aligned: then the middle runs as 16-byte lanes and
+// only the <16-byte head/tail goes element-wise.  A rank whose pointer is
+// not 16-B aligned takes the narrow path (units of the widest common
+// alignment), still exact.
 
-// dst[i] = src[i]
-__device__ __forceinline__ void block_copy(char* __restrict__ dst, const char* __restrict__ src,
-                                           uint64_t len) {
+// dst[i] = src[i], dst and src congruent mod 16
+__device__ __forceinline__ void block_copy_vec(char* __restrict__ dst, const char* __restrict__ src,
+                                               uint64_t len) {
     const uint64_t mis = (uint64_t)(uintptr_t)src & 15;
     uint64_t head = mis ? (16 - mis) : 0;
     if (head > len) head = len;
@@ -208,6 +210,30 @@ __device__ __forceinline__ void block_copy(char* __restrict__ dst, const char* _
         for (int u = 0; u < U; ++u) st16_nt(d + i + u * step, v[u]);
     }
     for (; i < nvec; i += step) st16_nt(d + i, ld16_nt(s + i));
+}
+
+template <typename W>
+__device__ __forceinline__ void block_copy_words(char* dst, const char* src, uint64_t len) {
+    const uint64_t mis = (uint64_t)(uintptr_t)src & (sizeof(W) - 1);
+    uint64_t head = mis ? sizeof(W) - mis : 0;
+    if (head > len) head = len;
+    const uint64_t nw = (len - head) / sizeof(W);
+    const uint64_t tail_start = head + nw * sizeof(W);
+    const unsigned tid = threadIdx.x;
+    if (tid < head) dst[tid] = src[tid];
+    if (tid < len - tail_start) dst[tail_start + tid] = src[tail_start + tid];
+    const W* s = reinterpret_cast<const W*>(src + head);
+    W* d = reinterpret_cast<W*>(dst + head);
+    for (uint64_t i = tid; i < nw; i += blockDim.x) d[i] = s[i];
+}
+
+__device__ __forceinline__ void block_copy(char* __restrict__ dst, const char* __restrict__ src, uint64_t len) {
+    const uintptr_t x = ((uintptr_t)dst ^ (uintptr_t)src) & 15;
+    if (x == 0) block_copy_vec(dst, src, len);
+    else if ((x & 7) == 0) block_copy_words<uint64_t>(dst, src, len);
+    else if ((x & 3) == 0) block_copy_words<uint32_t>(dst, src, len);
+    else if ((x & 1) == 0) block_copy_words<uint16_t>(dst, src, len);
+    else block_copy_words<uint8_t>(dst, src, len);
 }
 
 }  // namespace rdc_amd

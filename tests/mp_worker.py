@@ -16,6 +16,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def log(*a):
+    if os.environ.get("RDC_DEBUG"):
+        import time
+        print("[%.3f]" % time.time(), *a, flush=True)
+
+
 def main():
     rank, world, port, outdir, cases = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
     cases = json.loads(open(cases).read())
@@ -25,6 +31,7 @@ def main():
     rdc_amd.init(["RDC_RANK=%d" % rank, "RDC_WORLD_SIZE=%d" % world, "RDC_TRACKER_PORT=%d" % port,
                   "RDC_TRACKER_URI=127.0.0.1", "RDC_DEVICE=%s" % os.environ.get("RDC_DEVICE", "0")])
     torch.cuda.set_device(int(os.environ.get("RDC_DEVICE", "0")))
+    log("rank", rank, "init done")
     comms = {}
     esz = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 4, 7: 8, 8: 8, 9: 8, 10: 2, 11: 2}
     stream = torch.cuda.current_stream()
@@ -33,14 +40,16 @@ def main():
         name = c.get("comm", "main")
         if name not in comms:
             comms[name] = rdc_amd.new_comm(name) if name != "main" else rdc_amd.get_comm("main")
+            log("rank", rank, "comm", name, "ready")
         comm = comms[name]
         kind = c.get("kind", "allreduce")
         count, dtype = c["count"], c["dtype"]
-        pad = c.get("pad", 0)
+        pad = c.get("pad", 0) + rank * c.get("pad_per_rank", 0)
         nbytes = count * esz[dtype]
         buf = torch.zeros(nbytes + pad + 64, dtype=torch.uint8, device="cuda")
         p = buf.data_ptr() + pad
         check_call(_LIB.RdcFill(ctypes.c_void_p(p), count, dtype, c.get("seed", 0x5EED0000), rank, sp))
+        log("rank", rank, "case", i, "filled")
         reps = c.get("reps", 1)
         for _ in range(reps):
             if kind == "allreduce":
@@ -53,7 +62,9 @@ def main():
                 check_call(_LIB.RdcAllreduce(host.ctypes.data_as(ctypes.c_void_p), count, dtype, c["op"], None,
                                              None))
                 buf[pad: pad + nbytes] = torch.from_numpy(host).cuda()
+        log("rank", rank, "case", i, "launched")
         comm.check(sp)
+        log("rank", rank, "case", i, "done")
         out = buf[pad: pad + nbytes].cpu().numpy()
         if c.get("digest"):
             import hashlib

@@ -22,25 +22,37 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(scope="module")
-def group3():
+# Ranks of a single-process group that share one GPU must run concurrently:
+# each gets ONE stream for the whole module, created up front, so every rank
+# sits on its own hardware queue (conftest sets GPU_MAX_HW_QUEUES=16).
+# Creating fresh streams per call would eventually put two ranks on one
+# queue, serialising a waiting kernel in front of the one it waits for.
+class Group(list):
+    streams = None
+
+
+def make_group(n, scratch):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import rdc_amd
-    comms = rdc_amd.init_group([0, 0, 0], scratch_bytes=24 << 20)
-    yield comms
-    for c in comms:
+    g = Group(rdc_amd.init_group([0] * n, scratch_bytes=scratch))
+    g.streams = [torch.cuda.Stream() for _ in range(n)]
+    return g
+
+
+@pytest.fixture(scope="module")
+def group3():
+    g = make_group(3, 24 << 20)
+    yield g
+    for c in g:
         c.destroy()
 
 
 @pytest.fixture(scope="module")
 def group2():
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    import rdc_amd
-    comms = rdc_amd.init_group([0, 0], scratch_bytes=16 << 20)
-    yield comms
-    for c in comms:
+    g = make_group(2, 16 << 20)
+    yield g
+    for c in g:
         c.destroy()
 
 
@@ -53,7 +65,7 @@ def run_group(comms, inputs, dtype, op, algo, pads=None):
     pads = pads or [0] * n
     esz = np.dtype(O.NP_DTYPE[dtype]).itemsize
     bufs = [to_dev(x, p * esz) for x, p in zip(inputs, pads)]
-    streams = [torch.cuda.Stream() for _ in range(n)]
+    streams = comms.streams
     torch.cuda.synchronize()
     for r in range(n):
         rc = _LIB.RdcCommAllreduceEx(comms[r].handle, ptr(bufs[r], pads[r] * esz), count, dtype, op, algo,
@@ -108,15 +120,15 @@ def test_group_broadcast(group3):
     for root in range(3):
         for nbytes in (1, 100, 1 << 20 | 3):
             data = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(3)]
-            bufs = [to_dev(d, 1) for d in data]
-            streams = [torch.cuda.Stream() for _ in range(3)]
+            bufs = [to_dev(d, 1 + r) for r, d in enumerate(data)]
+            streams = group3.streams
             torch.cuda.synchronize()
             for r in range(3):
-                assert _LIB.RdcCommBroadcast(group3[r].handle, ptr(bufs[r], 1), nbytes, root,
+                assert _LIB.RdcCommBroadcast(group3[r].handle, ptr(bufs[r], 1 + r), nbytes, root,
                                              ctypes.c_void_p(streams[r].cuda_stream)) == 0
             for r in range(3):
                 group3[r].check(ctypes.c_void_p(streams[r].cuda_stream))
-                assert from_dev(bufs[r], 1, nbytes, O.DT_UINT8).tobytes() == data[root].tobytes()
+                assert from_dev(bufs[r], 1 + r, nbytes, O.DT_UINT8).tobytes() == data[root].tobytes()
 
 
 # --------------------------------------------------------------- multi-process
@@ -174,6 +186,8 @@ def test_mp_allreduce(world):
         {"count": 70000, "dtype": 11, "op": 2, "reps": 3},
         {"count": 123457, "dtype": 0, "kind": "broadcast", "root": world - 1},
         {"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"},
+        {"count": 100003, "dtype": 6, "op": 2, "algo": 2, "pad_per_rank": 4},   # ranks' buffers differ mod 16
+        {"count": 100003, "dtype": 10, "op": 0, "algo": 1, "pad_per_rank": 2},
     ]
     tmp = run_mp(world, cases)
     for i, c in enumerate(cases):
@@ -182,3 +196,34 @@ def test_mp_allreduce(world):
             got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
             exp = np.frombuffer(want[r].tobytes(), dtype=np.uint8)
             assert got.tobytes() == exp.tobytes(), (i, c, r)
+
+
+def test_mp_full_size_cfg2():
+    """BASELINE cfg2 at full size: fp32 256 MiB allreduce over 2 ranks, both
+    schedules, checked bit-exact (sha256) against the oracle's ring."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import hashlib
+    count = (256 << 20) // 4
+    cases = [{"count": count, "dtype": 6, "op": 2, "algo": 2, "digest": True},
+             {"count": count, "dtype": 6, "op": 2, "algo": 1, "digest": True}]
+    tmp = run_mp(2, cases, timeout=400, env_extra={"RDC_SCRATCH_BYTES": "4080M", "RDC_NBLOCKS": "64"})
+    want = expected_for(cases[0], 2)
+    h = hashlib.sha256(np.frombuffer(want[0].tobytes(), dtype=np.uint8).tobytes()).hexdigest()
+    for i in range(2):
+        for r in range(2):
+            assert open(os.path.join(tmp, "case%d_rank%d.sha" % (i, r))).read() == h, (i, r)
+
+
+def test_mp_many_small_buckets_cfg5_shape():
+    """test/mallreduce.cc shape: back-to-back 1 MiB fp32 allreduces on one buffer."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [{"count": 1 << 18, "dtype": 6, "op": 2, "reps": 64},
+             {"count": 1 << 18, "dtype": 2, "op": 0, "reps": 64, "algo": 1}]
+    tmp = run_mp(4, cases)
+    for i, c in enumerate(cases):
+        want = expected_for(c, 4)
+        for r in range(4):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)

@@ -1,0 +1,133 @@
+// Variant sweep for the 1-GPU reduce kernel (dst += src, fp32, 1 GiB):
+// load/store cache policy, unroll depth, grid size, grid-stride vs
+// block-contiguous walk.  Prints one line per variant: ms and GB/s (3*S).
+//   hipcc --offload-arch=gfx950 -O3 -I rdc_amd/csrc tools/bench_reduce.hip -o /tmp/bench_reduce
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
+#include "rdc_device.h"
+
+using namespace rdc_amd;
+
+template <bool NTL, bool NTS>
+__device__ __forceinline__ v4u LD(const v4u* p) {
+    if (NTL) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <bool NTS>
+__device__ __forceinline__ void ST(v4u* p, v4u v) {
+    if (NTS) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// grid-stride, U independent 16-B positions per lane per iteration
+template <int U, bool NTL, bool NTS, int B>
+__global__ __launch_bounds__(B) void k_gs(v4u* __restrict__ d, const v4u* __restrict__ s, uint64_t nvec) {
+    const uint64_t stride = (uint64_t)gridDim.x * B;
+    uint64_t i = (uint64_t)blockIdx.x * B + threadIdx.x;
+    for (; i + (U - 1) * stride < nvec; i += U * stride) {
+        v4u a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = LD<NTL, NTS>(d + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) b[u] = LD<NTL, NTS>(s + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) ST<NTS>(d + i + u * stride, reduce16<RDC_OP_SUM, float>(a[u], b[u]));
+    }
+    for (; i < nvec; i += stride) ST<NTS>(d + i, reduce16<RDC_OP_SUM, float>(LD<NTL, NTS>(d + i), LD<NTL, NTS>(s + i)));
+}
+
+// block-contiguous: block b owns [b*per, (b+1)*per), walks it U*B vectors at a time
+template <int U, bool NTL, bool NTS, int B>
+__global__ __launch_bounds__(B) void k_bc(v4u* __restrict__ d, const v4u* __restrict__ s, uint64_t nvec) {
+    const uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per;
+    uint64_t hi = lo + per;
+    if (hi > nvec) hi = nvec;
+    uint64_t i = lo + threadIdx.x;
+    for (; i + (U - 1) * B < hi; i += U * B) {
+        v4u a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = LD<NTL, NTS>(d + i + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) b[u] = LD<NTL, NTS>(s + i + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) ST<NTS>(d + i + u * B, reduce16<RDC_OP_SUM, float>(a[u], b[u]));
+    }
+    for (; i < hi; i += B) ST<NTS>(d + i, reduce16<RDC_OP_SUM, float>(LD<NTL, NTS>(d + i), LD<NTL, NTS>(s + i)));
+}
+
+#define CK(x)                                                                  \
+    do {                                                                       \
+        hipError_t e = (x);                                                    \
+        if (e != hipSuccess) {                                                 \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            exit(1);                                                           \
+        }                                                                      \
+    } while (0)
+
+typedef void (*KFn)(v4u*, const v4u*, uint64_t);
+
+struct Variant {
+    const char* name;
+    KFn fn;
+    int block;
+};
+
+int main(int argc, char** argv) {
+    const size_t S = argc > 1 ? strtoull(argv[1], 0, 0) : (1ull << 30);
+    const uint64_t nvec = S / 16;
+    v4u *d, *s;
+    CK(hipMalloc(&d, S));
+    CK(hipMalloc(&s, S));
+    CK(hipMemset(d, 0, S));
+    CK(hipMemset(s, 0, S));
+    std::vector<Variant> vs = {
+        {"gs U4 nt/nt B256", (KFn)k_gs<4, true, true, 256>, 256},
+        {"gs U4 plain B256", (KFn)k_gs<4, false, false, 256>, 256},
+        {"gs U4 ntL/plainS B256", (KFn)k_gs<4, true, false, 256>, 256},
+        {"gs U4 plainL/ntS B256", (KFn)k_gs<4, false, true, 256>, 256},
+        {"gs U8 nt/nt B256", (KFn)k_gs<8, true, true, 256>, 256},
+        {"gs U8 plain B256", (KFn)k_gs<8, false, false, 256>, 256},
+        {"gs U2 nt/nt B256", (KFn)k_gs<2, true, true, 256>, 256},
+        {"gs U4 nt/nt B512", (KFn)k_gs<4, true, true, 512>, 512},
+        {"gs U4 plain B512", (KFn)k_gs<4, false, false, 512>, 512},
+        {"bc U4 nt/nt B256", (KFn)k_bc<4, true, true, 256>, 256},
+        {"bc U4 plain B256", (KFn)k_bc<4, false, false, 256>, 256},
+        {"bc U8 plain B256", (KFn)k_bc<8, false, false, 256>, 256},
+        {"bc U8 nt/nt B256", (KFn)k_bc<8, true, true, 256>, 256},
+    };
+    const int grids[] = {512, 1024, 2048, 4096, 8192, 16384};
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (auto& v : vs) {
+        for (int g : grids) {
+            for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(v.fn, dim3(g), dim3(v.block), 0, 0, d, s, nvec);
+            CK(hipDeviceSynchronize());
+            const int it = 20;
+            CK(hipEventRecord(e0));
+            for (int k = 0; k < it; ++k) hipLaunchKernelGGL(v.fn, dim3(g), dim3(v.block), 0, 0, d, s, nvec);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= it;
+            printf("%-24s grid %6d : %.4f ms  %.1f GB/s (3S)\n", v.name, g, ms, 3.0 * S / (ms * 1e-3) / 1e9);
+        }
+    }
+    // copy reference: hipMemcpy D2D (2S traffic)
+    for (int w = 0; w < 3; ++w) CK(hipMemcpy(d, s, S, hipMemcpyDeviceToDevice));
+    CK(hipEventRecord(e0));
+    for (int k = 0; k < 20; ++k) CK(hipMemcpyAsync(d, s, S, hipMemcpyDeviceToDevice, 0));
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= 20;
+    printf("%-24s          : %.4f ms  %.1f GB/s (2S)\n", "hipMemcpy D2D", ms, 2.0 * S / (ms * 1e-3) / 1e9);
+    return 0;
+}
