@@ -1,0 +1,174 @@
+/*!
+ * rdc.h — the reference's C++ interface (include/rdc.h, include/api.h,
+ * include/core/rdc-inl.h, include/core/mpi.h of akkaze/rdc) over the
+ * MI355X device path in librdc_amd.so.
+ *
+ * Drop-in for the allreduce/broadcast surface: same namespaces, names,
+ * template parameters and argument meaning.  Differences, all deliberate:
+ *   - the collectives work on host OR device (hipMalloc'd) pointers and are
+ *     bit-identical to the reference's CPU ring allreduce;
+ *   - comm::ICommunicator's collectives are real virtual calls (the
+ *     reference's are non-virtual no-ops, include/comm/communicator.h:92-108);
+ *   - failures abort with a message, like the reference's CHECK_F.
+ * Link with -lrdc_amd.  Header-only otherwise.
+ */
+#pragma once
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <string>
+#include <vector>
+
+#include "rdc_amd.h"
+
+namespace rdc {
+
+/*! \brief name of the default communicator (include/comm/communicator.h:21) */
+static const std::string kMainCommName = "main";
+
+namespace mpi {
+/*! \brief reduction operators (include/core/mpi.h:12-17) */
+enum OpType { kMax = 0, kMin = 1, kSum = 2, kBitwiseOR = 3 };
+/*! \brief element types (include/core/mpi.h:19-30) */
+enum DataType {
+    kChar = 0,
+    kUChar = 1,
+    kInt = 2,
+    kUInt = 3,
+    kLong = 4,
+    kULong = 5,
+    kFloat = 6,
+    kDouble = 7,
+    kLongLong = 8,
+    kULongLong = 9
+};
+template <typename DType>
+inline DataType GetType(void);
+template <> inline DataType GetType<char>(void) { return kChar; }
+template <> inline DataType GetType<signed char>(void) { return kChar; }
+template <> inline DataType GetType<unsigned char>(void) { return kUChar; }
+template <> inline DataType GetType<int>(void) { return kInt; }
+template <> inline DataType GetType<unsigned int>(void) { return kUInt; }
+template <> inline DataType GetType<long>(void) { return kLong; }                       // NOLINT
+template <> inline DataType GetType<unsigned long>(void) { return kULong; }             // NOLINT
+template <> inline DataType GetType<float>(void) { return kFloat; }
+template <> inline DataType GetType<double>(void) { return kDouble; }
+template <> inline DataType GetType<long long>(void) { return kLongLong; }              // NOLINT
+template <> inline DataType GetType<unsigned long long>(void) { return kULongLong; }    // NOLINT
+}  // namespace mpi
+
+/*! \brief reduction operators (include/core/mpi.h:84-112) */
+namespace op {
+struct Max { static const mpi::OpType kType = mpi::kMax; };
+struct Min { static const mpi::OpType kType = mpi::kMin; };
+struct Sum { static const mpi::OpType kType = mpi::kSum; };
+struct BitOR { static const mpi::OpType kType = mpi::kBitwiseOR; };
+}  // namespace op
+
+namespace detail {
+inline void Check(int rc, const char* what) {
+    if (rc != 0) {
+        fprintf(stderr, "rdc: %s failed: %s\n", what, RdcGetLastError());
+        abort();
+    }
+}
+}  // namespace detail
+
+namespace comm {
+/*! \brief a named communicator (include/comm/communicator.h:41-146) */
+class ICommunicator {
+public:
+    ICommunicator(void* handle, const std::string& name) : handle_(handle), name_(name) {}
+    virtual ~ICommunicator() {}
+    /*! \brief in-place allreduce of count elements (host or device memory) */
+    virtual void Allreduce(void* sendrecvbuf, uint64_t count, mpi::DataType dtype, mpi::OpType op) {
+        detail::Check(RdcAllreduceOn(handle_, sendrecvbuf, count, (int)dtype, (int)op), "Allreduce");
+    }
+    /*! \brief broadcast size bytes from root (host or device memory) */
+    virtual void Broadcast(void* sendrecvaddr, uint64_t size, int root) {
+        detail::Check(RdcBroadcastOn(handle_, sendrecvaddr, size, root), "Broadcast");
+    }
+    int GetRank() const { return RdcCommRank(handle_); }
+    int GetWorldSize() const { return RdcCommSize(handle_); }
+    std::string name() const { return name_; }
+    void* handle() const { return handle_; }
+
+private:
+    void* handle_;
+    std::string name_;
+};
+
+inline std::vector<ICommunicator*>& Registry() {
+    static std::vector<ICommunicator*> r;
+    return r;
+}
+}  // namespace comm
+
+/*! \brief initialise rdc; argv key=val pairs are parameters (rdc-inl.h:21-23) */
+inline void Init(int argc, char** argv) { detail::Check(RdcInit(argc, argv), "Init"); }
+inline void Init() { Init(0, nullptr); }
+
+inline comm::ICommunicator* Lookup(const std::string& name) {
+    for (comm::ICommunicator* c : comm::Registry())
+        if (c->name() == name) return c;
+    return nullptr;
+}
+/*! \brief create (collectively) a communicator (rdc-inl.h:25-27) */
+inline comm::ICommunicator* NewCommunicator(const std::string& name) {
+    if (comm::ICommunicator* c = Lookup(name)) return c;
+    void* h = nullptr;
+    detail::Check(RdcNewCommunicator(&h, name.c_str()), "NewCommunicator");
+    comm::ICommunicator* c = new comm::ICommunicator(h, name);
+    comm::Registry().push_back(c);
+    return c;
+}
+/*! \brief an existing communicator; "main" is created on first use (rdc-inl.h:29-31) */
+inline comm::ICommunicator* GetCommunicator(const std::string& name = kMainCommName) {
+    if (comm::ICommunicator* c = Lookup(name)) return c;
+    void* h = nullptr;
+    detail::Check(RdcGetCommunicator(&h, name.c_str()), "GetCommunicator");
+    comm::ICommunicator* c = new comm::ICommunicator(h, name);
+    comm::Registry().push_back(c);
+    return c;
+}
+inline void Finalize() {
+    for (comm::ICommunicator* c : comm::Registry()) delete c;
+    comm::Registry().clear();
+    detail::Check(RdcFinalize(), "Finalize");
+}
+inline int GetRank() { return RdcGetRank(); }
+inline int GetWorldSize() { return RdcGetWorldSize(); }
+inline bool IsDistributed() { return RdcIsDistributed() != 0; }
+inline void TrackerPrint(const std::string& msg) { RdcTrackerPrint(msg.c_str()); }
+inline void Barrier() { detail::Check(RdcBarrier(), "Barrier"); }
+
+/*! \brief in-place allreduce (include/api.h:62-64, rdc-inl.h:125-135) */
+template <typename OP, typename DType>
+inline void Allreduce(DType* sendrecvbuf, uint64_t count, const std::string& comm_name = kMainCommName) {
+    if (GetWorldSize() == 1 || count == 0) return;  // communicator_base.h:133-138
+    GetCommunicator(comm_name)->Allreduce(sendrecvbuf, count, mpi::GetType<DType>(), OP::kType);
+}
+
+/*! \brief broadcast a memory region from root (include/api.h:23-24) */
+inline void Broadcast(void* sendrecv_data, uint64_t size, int root, const std::string& comm_name = kMainCommName) {
+    if (GetWorldSize() == 1 || size == 0) return;
+    GetCommunicator(comm_name)->Broadcast(sendrecv_data, size, root);
+}
+/*! \brief broadcast a vector, resizing receivers (rdc-inl.h:76-88) */
+template <typename DType>
+inline void Broadcast(std::vector<DType>& sendrecv_data, int root, const std::string& comm_name = kMainCommName) {
+    uint64_t size = sendrecv_data.size();
+    Broadcast(&size, sizeof(size), root, comm_name);
+    if (sendrecv_data.size() != size) sendrecv_data.resize(size);
+    if (size != 0) Broadcast(sendrecv_data.data(), size * sizeof(DType), root, comm_name);
+}
+/*! \brief broadcast a string, resizing receivers (rdc-inl.h:89-100) */
+inline void Broadcast(std::string& sendrecv_data, int root, const std::string& comm_name = kMainCommName) {
+    uint64_t size = sendrecv_data.length();
+    Broadcast(&size, sizeof(size), root, comm_name);
+    if (sendrecv_data.length() != size) sendrecv_data.resize(size);
+    if (size != 0) Broadcast(&sendrecv_data[0], size, root, comm_name);
+}
+
+}  // namespace rdc

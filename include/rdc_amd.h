@@ -69,6 +69,12 @@ int RdcAllreduce(void* sendrecv, size_t count, int dtype, int op, void (*prepare
  * rdc/core.py:143-154).  Host or device memory; synchronous. */
 int RdcBroadcast(void* sendrecv, unsigned long size, int root);
 
+/* The same two calls on a named communicator (rdc::Allreduce<OP,DType>(buf,
+ * count, comm_name), include/api.h:62-64; rdc::Broadcast(..., comm_name),
+ * include/api.h:23-26).  Host or device memory; synchronous. */
+int RdcAllreduceOn(void* comm, void* sendrecv, size_t count, int dtype, int op);
+int RdcBroadcastOn(void* comm, void* sendrecv, size_t size, int root);
+
 /* rdc::NewCommunicator / GetCommunicator (include/rdc.h:62-71;
  * rdc/comm.py:398-427 calls RdcNewCommunicator(byref(handle), name)).
  * NewCommunicator is collective over all ranks. */
@@ -107,6 +113,18 @@ int RdcReduce(void* dst, const void* src, size_t count, int dtype, int op, void*
 /* Synthetic inputs: u = splitmix64(seed ^ (rank<<40) ^ i) mapped per dtype
  * (identical to the CPU oracle's generator).  Stream-ordered. */
 int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, void* stream);
+
+/* Host-side planning, no GPU needed (what the launches of a collective will
+ * be; used by the CPU tests).  RdcPlanLayout: out = {slot_bytes,
+ * region_bytes, max_tiles, flag_bytes} of a communicator of n ranks.
+ * RdcPlanAllreduce: one record of RDC_PLAN_WORDS uint64 per launch:
+ *   [tile_bytes, nb_scatter, nb_reduce, nb_gather,
+ *    off[16], len[16], mis[16], tiles[16]]   (per chunk c < n)
+ * *out_pieces = number of launches (records written: min(that, max_pieces)). */
+#define RDC_PLAN_WORDS 68
+int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4);
+int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int algo, size_t tile_bytes,
+                     int max_blocks, uint64_t* out, int max_pieces, int* out_pieces);
 
 /* Set a parameter (same keys as RdcInit argv). */
 int RdcSetParam(const char* name, const char* value);

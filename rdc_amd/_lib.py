@@ -44,6 +44,8 @@ def _load():
         "RdcBarrier": (i, []),
         "RdcAllreduce": (i, [vp, sz, i, i, vp, vp]),
         "RdcBroadcast": (i, [vp, ctypes.c_ulong, i]),
+        "RdcAllreduceOn": (i, [vp, vp, sz, i, i]),
+        "RdcBroadcastOn": (i, [vp, vp, sz, i]),
         "RdcNewCommunicator": (i, [pvp, ctypes.c_char_p]),
         "RdcGetCommunicator": (i, [pvp, ctypes.c_char_p]),
         "RdcCommAllreduce": (i, [vp, vp, sz, i, i, vp]),
@@ -58,6 +60,8 @@ def _load():
         "RdcCommDestroy": (i, [vp]),
         "RdcReduce": (i, [vp, vp, sz, i, i, vp]),
         "RdcFill": (i, [vp, sz, i, u64, i, vp]),
+        "RdcPlanLayout": (i, [i, sz, ctypes.POINTER(u64)]),
+        "RdcPlanAllreduce": (i, [i, sz, i, sz, i, sz, i, ctypes.POINTER(u64), i, ctypes.POINTER(ctypes.c_int)]),
         "RdcSetParam": (i, [ctypes.c_char_p, ctypes.c_char_p]),
         "RdcGetLastError": (ctypes.c_char_p, []),
         "RdcVersion": (ctypes.c_char_p, []),

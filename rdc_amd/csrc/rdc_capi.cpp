@@ -9,6 +9,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -124,7 +125,8 @@ Communicator* get_comm(Manager& m, const std::string& name, bool create) {
     if (it != m.comms.end()) return it->second.get();
     if (!create) throw std::runtime_error("rdc: communicator '" + name + "' does not exist");
     require_init(m);
-    Communicator* c = Communicator::Create(name, m.bs.get(), pick_device(m), m.cfg);
+    Communicator* c = Communicator::Create(name, m.bs.get(), m.world == 1 ? std::max(m.device, 0) : pick_device(m),
+                                           m.cfg);
     m.comms[name].reset(c);
     return c;
 }
@@ -274,33 +276,62 @@ int RdcGetCommunicator(void** out, const char* name) {
     });
 }
 
+namespace {
+
+void check_dtype_op(int dtype, int op) {
+    if (rdc_dtype_size(dtype) == 0) throw std::invalid_argument("rdc: bad dtype " + std::to_string(dtype));
+    if (op < 0 || op >= RDC_OP_COUNT) throw std::invalid_argument("rdc: bad op " + std::to_string(op));
+    if (op == RDC_OP_BITOR && rdc_dtype_is_float(dtype))
+        throw std::invalid_argument("rdc: BITOR needs an integer dtype");
+}
+
+// synchronous allreduce of host or device memory on communicator c
+void allreduce_sync(Manager& m, Communicator* c, void* sendrecv, size_t count, int dtype, int op) {
+    check_dtype_op(dtype, op);
+    if (c->size() == 1 || count == 0) return;
+    hipStream_t s = manager_stream(m, c->device());
+    if (is_device_pointer(sendrecv)) {
+        c->Allreduce(sendrecv, count, dtype, op, s);
+        c->Check(s);
+        return;
+    }
+    // host-resident buffer: H2D, device allreduce, D2H (host path)
+    const size_t bytes = count * rdc_dtype_size(dtype);
+    void* d = staging(m, bytes, c->device());
+    hcheck(hipMemcpyAsync(d, sendrecv, bytes, hipMemcpyHostToDevice, s), "H2D");
+    c->Allreduce(d, count, dtype, op, s);
+    hcheck(hipMemcpyAsync(sendrecv, d, bytes, hipMemcpyDeviceToHost, s), "D2H");
+    c->Check(s);
+}
+
+void broadcast_sync(Manager& m, Communicator* c, void* sendrecv, size_t size, int root) {
+    if (root < 0 || root >= c->size()) throw std::invalid_argument("rdc: broadcast root out of range");
+    if (c->size() == 1 || size == 0) return;
+    hipStream_t s = manager_stream(m, c->device());
+    if (is_device_pointer(sendrecv)) {
+        c->Broadcast(sendrecv, size, root, s);
+        c->Check(s);
+        return;
+    }
+    void* d = staging(m, size, c->device());
+    if (c->rank() == root) hcheck(hipMemcpyAsync(d, sendrecv, size, hipMemcpyHostToDevice, s), "H2D");
+    c->Broadcast(d, size, root, s);
+    if (c->rank() != root) hcheck(hipMemcpyAsync(sendrecv, d, size, hipMemcpyDeviceToHost, s), "D2H");
+    c->Check(s);
+}
+
+}  // namespace
+
 int RdcAllreduce(void* sendrecv, size_t count, int dtype, int op, void (*prepare_fun)(void*), void* prepare_arg) {
     Manager& m = M();
     std::lock_guard<std::recursive_mutex> lk(m.mu);
     return guard([&] {
         require_init(m);
         if (prepare_fun) prepare_fun(prepare_arg);
-        const size_t esz = rdc_dtype_size(dtype);
-        if (esz == 0) throw std::invalid_argument("rdc: bad dtype " + std::to_string(dtype));
-        if (op < 0 || op >= RDC_OP_COUNT) throw std::invalid_argument("rdc: bad op " + std::to_string(op));
-        if (op == RDC_OP_BITOR && rdc_dtype_is_float(dtype))
-            throw std::invalid_argument("rdc: BITOR needs an integer dtype");
+        check_dtype_op(dtype, op);
         // world size 1: Communicator::Allreduce returns at once (communicator_base.h:133-138)
         if (m.world == 1 || count == 0) return;
-        Communicator* c = get_comm(m, "main", true);
-        hipStream_t s = manager_stream(m, c->device());
-        if (is_device_pointer(sendrecv)) {
-            c->Allreduce(sendrecv, count, dtype, op, s);
-            c->Check(s);
-            return;
-        }
-        // host-resident buffer: H2D, device allreduce, D2H
-        const size_t bytes = count * esz;
-        void* d = staging(m, bytes, c->device());
-        hcheck(hipMemcpyAsync(d, sendrecv, bytes, hipMemcpyHostToDevice, s), "H2D");
-        c->Allreduce(d, count, dtype, op, s);
-        hcheck(hipMemcpyAsync(sendrecv, d, bytes, hipMemcpyDeviceToHost, s), "D2H");
-        c->Check(s);
+        allreduce_sync(m, get_comm(m, "main", true), sendrecv, count, dtype, op);
     });
 }
 
@@ -311,19 +342,20 @@ int RdcBroadcast(void* sendrecv, unsigned long size, int root) {
         require_init(m);
         if (root < 0 || root >= m.world) throw std::invalid_argument("rdc: broadcast root out of range");
         if (m.world == 1 || size == 0) return;
-        Communicator* c = get_comm(m, "main", true);
-        hipStream_t s = manager_stream(m, c->device());
-        if (is_device_pointer(sendrecv)) {
-            c->Broadcast(sendrecv, size, root, s);
-            c->Check(s);
-            return;
-        }
-        void* d = staging(m, size, c->device());
-        if (c->rank() == root) hcheck(hipMemcpyAsync(d, sendrecv, size, hipMemcpyHostToDevice, s), "H2D");
-        c->Broadcast(d, size, root, s);
-        if (c->rank() != root) hcheck(hipMemcpyAsync(sendrecv, d, size, hipMemcpyDeviceToHost, s), "D2H");
-        c->Check(s);
+        broadcast_sync(m, get_comm(m, "main", true), sendrecv, size, root);
     });
+}
+
+int RdcAllreduceOn(void* comm, void* sendrecv, size_t count, int dtype, int op) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] { allreduce_sync(m, as_comm(comm), sendrecv, count, dtype, op); });
+}
+
+int RdcBroadcastOn(void* comm, void* sendrecv, size_t size, int root) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] { broadcast_sync(m, as_comm(comm), sendrecv, size, root); });
 }
 
 int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op, void* stream) {
@@ -397,6 +429,43 @@ int RdcReduce(void* dst, const void* src, size_t count, int dtype, int op, void*
 
 int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, void* stream) {
     return guard([&] { DeviceFill(dev_buf, count, dtype, seed, rank, static_cast<hipStream_t>(stream)); });
+}
+
+int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4) {
+    return guard([&] {
+        if (n < 1 || n > RDC_MAX_RANKS || !out4) throw std::invalid_argument("rdc: bad argument");
+        const Layout L = MakeLayout(n, scratch_bytes ? scratch_bytes : CommConfig().scratch_bytes);
+        out4[0] = L.slot_bytes;
+        out4[1] = L.region_bytes;
+        out4[2] = L.max_tiles;
+        out4[3] = L.flag_bytes;
+    });
+}
+
+int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int algo, size_t tile_bytes,
+                     int max_blocks, uint64_t* out, int max_pieces, int* out_pieces) {
+    return guard([&] {
+        const size_t esz = rdc_dtype_size(dtype);
+        if (n < 1 || n > RDC_MAX_RANKS || esz == 0 || !out_pieces) throw std::invalid_argument("rdc: bad argument");
+        if (algo == RDC_ALGO_AUTO) algo = RDC_ALGO_MESH;
+        const Layout L = MakeLayout(n, scratch_bytes ? scratch_bytes : CommConfig().scratch_bytes);
+        const std::vector<Piece> plan = PlanAllreduce(n, count, esz, L, algo, tile_bytes, max_blocks > 0 ? max_blocks : 256);
+        *out_pieces = (int)plan.size();
+        for (int k = 0; k < (int)plan.size() && k < max_pieces && out; ++k) {
+            uint64_t* o = out + (size_t)k * RDC_PLAN_WORDS;
+            const Piece& p = plan[(size_t)k];
+            o[0] = p.tile_bytes;
+            o[1] = (uint64_t)p.nb_scatter;
+            o[2] = (uint64_t)p.nb_reduce;
+            o[3] = (uint64_t)p.nb_gather;
+            for (int c = 0; c < RDC_MAX_RANKS; ++c) {
+                o[4 + c] = p.off[c];
+                o[20 + c] = p.len[c];
+                o[36 + c] = p.mis[c];
+                o[52 + c] = (uint64_t)p.tiles[c];
+            }
+        }
+    });
 }
 
 int RdcSetParam(const char* name, const char* value) {

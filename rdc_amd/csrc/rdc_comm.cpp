@@ -11,6 +11,7 @@
 #include <string>
 
 #include "rdc_kernels.h"
+#include "rdc_plan.h"
 
 namespace rdc_amd {
 
@@ -18,19 +19,6 @@ namespace {
 
 void hip_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string("rdc: ") + what + ": " + hipGetErrorString(e));
-}
-
-size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-size_t round_down(size_t x, size_t a) { return x / a * a; }
-
-// utils::Split (include/utils/utils.h:59-70) in 64-bit: same ranges for every
-// count the reference's int version can represent.
-void split(int64_t count, int n, int64_t* b, int64_t* e) {
-    const int64_t k = count / n, m = count % n;
-    for (int i = 0; i < n; ++i) {
-        b[i] = (int64_t)i * k + std::min<int64_t>(i, m);
-        e[i] = (int64_t)(i + 1) * k + std::min<int64_t>(i + 1, m);
-    }
 }
 
 int env_alloc_kind() {
@@ -87,16 +75,11 @@ struct PeerInfo {
 
 void Communicator::AllocLocal() {
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    // RS and AG regions are separate allocations, each below 2 GiB: on ROCm
-    // 7.2 (dmabuf IPC) hipIpcOpenMemHandle of an allocation >= 2 GiB never
-    // returns (measured: 2044 MiB opens, 2048 MiB hangs).
-    size_t region = std::min<size_t>(cfg_.scratch_bytes / 2, kMaxRegionBytes);
-    size_t slot = round_down(region / (size_t)n_, 4096);
-    if (slot < 64 * 1024 || n_ == 1) slot = 64 * 1024;  // world size 1 never moves data
-    slot_bytes_ = slot;
-    region_bytes_ = slot * (size_t)n_;
-    max_tiles_ = (uint32_t)(region_bytes_ / RDC_MIN_TILE + 2);
-    flag_bytes_ = round_up((size_t)2 * n_ * max_tiles_ * sizeof(uint32_t), 4096);
+    const Layout L = MakeLayout(n_, cfg_.scratch_bytes);
+    slot_bytes_ = L.slot_bytes;
+    region_bytes_ = L.region_bytes;
+    max_tiles_ = L.max_tiles;
+    flag_bytes_ = L.flag_bytes;
     int k1 = 0, k2 = 0, k3 = 0;
     scratch_ = static_cast<char*>(alloc_shared(region_bytes_, &k1));
     scratch_ag_ = static_cast<char*>(alloc_shared(region_bytes_, &k3));
@@ -127,6 +110,9 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     c->cfg_ = cfg;
     c->bs_ = bs;
     if (c->n_ > RDC_MAX_RANKS) throw std::runtime_error("rdc: world size exceeds RDC_MAX_RANKS");
+    // world size 1 moves no data (Communicator::Allreduce returns at once,
+    // communicator_base.h:133-138): no device resources, no GPU needed
+    if (c->n_ == 1) return c.release();
     dbg("[rdc %d] %s\n", c->rank_, "alloc");
     c->AllocLocal();
     dbg("[rdc %d] %s\n", c->rank_, "alloc done");
@@ -219,6 +205,7 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
 }
 
 Communicator::~Communicator() {
+    if (n_ == 1 && scratch_ == nullptr) return;  // trivial communicator
     (void)hipSetDevice(device_);
     (void)hipDeviceSynchronize();
     if (owns_peers_ipc_ && bs_) {
@@ -264,32 +251,16 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     a->timeout_ticks = (uint64_t)(cfg_.timeout_s * (double)wall_khz_ * 1000.0);
 }
 
-void Communicator::Plan(size_t chunk_bytes, int algo, size_t* tile, int* nb_s, int* nb_r, int* nb_g) const {
-    algo = PickAlgo(algo);
-    size_t t = cfg_.tile_bytes;
-    if (t == 0) {
-        // mesh: ~64 tiles per chunk keeps every reduce block busy; ring: each
-        // block walks 2(n-1) hand-offs per tile, so aim for one tile per block.
-        const size_t want = algo == RDC_ALGO_RING ? chunk_bytes / (size_t)num_cus_ : chunk_bytes / 64;
-        t = std::min<size_t>(std::max<size_t>(want, RDC_MIN_TILE), (size_t)1 << 20);
-    }
-    t = std::max<size_t>(round_up(t, RDC_SLOT_ALIGN), RDC_MIN_TILE);
-    *tile = t;
-    const int T = (int)((chunk_bytes + t - 1) / t);
-    const int G = cfg_.max_blocks > 0 ? cfg_.max_blocks : num_cus_;
-    if (algo == RDC_ALGO_RING) {
-        *nb_s = std::max(1, std::min(T, G));
-        *nb_r = *nb_g = 0;
-        return;
-    }
-    const int items_s = (n_ - 1) * T;
-    int s = std::max(1, std::min(items_s, G * 3 / 8));
-    int r = std::max(1, std::min(T, G * 3 / 8));
-    int g = std::max(1, std::min(items_s, G - s - r));
-    *nb_s = s;
-    *nb_r = r;
-    *nb_g = g;
+Layout Communicator::layout() const {
+    Layout L;
+    L.slot_bytes = slot_bytes_;
+    L.region_bytes = region_bytes_;
+    L.max_tiles = max_tiles_;
+    L.flag_bytes = flag_bytes_;
+    return L;
 }
+
+int Communicator::max_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_blocks : num_cus_; }
 
 void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStream_t stream, int algo) {
     KernelSet ks;
@@ -303,44 +274,24 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
     if (buf == nullptr) throw std::invalid_argument("rdc: null buffer");
     algo = PickAlgo(algo);
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
-    split((int64_t)count, n_, cb, ce);
-    const int64_t maxlen = ce[0] - cb[0];  // first chunk is never shorter
-    const int64_t pe = (int64_t)(round_down(slot_bytes_ - RDC_SLOT_ALIGN, RDC_SLOT_ALIGN) / esz);
-    const int64_t npieces = (maxlen + pe - 1) / pe;
-    char* user = static_cast<char*>(buf);
-    for (int64_t k = 0; k < npieces; ++k) {
+    const std::vector<Piece> plan = PlanAllreduce(n_, count, esz, layout(), algo, cfg_.tile_bytes, max_blocks());
+    for (const Piece& p : plan) {
         CollArgs a;
         FillArgsCommon(&a);
-        a.user = user;
-        size_t chunk_max = 0;
-        for (int c = 0; c < n_; ++c) {
-            const int64_t b0 = cb[c] + k * pe;
-            const int64_t e0 = std::min(ce[c], b0 + pe);
-            if (e0 > b0) {
-                a.off[c] = (uint64_t)b0 * esz;
-                a.len[c] = (uint64_t)(e0 - b0) * esz;
-            } else {
-                a.off[c] = 0;
-                a.len[c] = 0;
-            }
-            // buffer-relative: every rank places chunk c's bytes identically
-            a.mis[c] = (uint32_t)(a.off[c] % 16);
-            chunk_max = std::max<size_t>(chunk_max, a.len[c]);
-        }
-        size_t tile;
-        int nb_s, nb_r, nb_g;
-        Plan(chunk_max, algo, &tile, &nb_s, &nb_r, &nb_g);
-        a.tile_bytes = tile;
-        for (int c = 0; c < n_; ++c) a.tiles[c] = (int)((a.len[c] + tile - 1) / tile);
+        a.user = static_cast<char*>(buf);
+        memcpy(a.off, p.off, sizeof(a.off));
+        memcpy(a.len, p.len, sizeof(a.len));
+        memcpy(a.mis, p.mis, sizeof(a.mis));
+        memcpy(a.tiles, p.tiles, sizeof(a.tiles));
+        a.tile_bytes = p.tile_bytes;
         a.seq = ++seq_;
         if (algo == RDC_ALGO_RING) {
-            hip_check(ks.ring(a, nb_s, stream), "launch ring allreduce");
+            hip_check(ks.ring(a, p.nb_scatter, stream), "launch ring allreduce");
         } else {
-            a.nb_scatter = nb_s;
-            a.nb_reduce = nb_r;
-            a.nb_gather = nb_g;
-            hip_check(ks.mesh(a, nb_s + nb_r + nb_g, stream), "launch mesh allreduce");
+            a.nb_scatter = p.nb_scatter;
+            a.nb_reduce = p.nb_reduce;
+            a.nb_gather = p.nb_gather;
+            hip_check(ks.mesh(a, p.nb_scatter + p.nb_reduce + p.nb_gather, stream), "launch mesh allreduce");
         }
     }
 }
@@ -350,29 +301,23 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
     if (n_ == 1 || bytes == 0) return;
     if (buf == nullptr) throw std::invalid_argument("rdc: null buffer");
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    const size_t cap = round_down(region_bytes_ - RDC_SLOT_ALIGN, RDC_SLOT_ALIGN);
-    char* user = static_cast<char*>(buf);
-    const int G = cfg_.max_blocks > 0 ? cfg_.max_blocks : num_cus_;
-    for (size_t off = 0; off < bytes; off += cap) {
+    for (const Piece& p : PlanBroadcast(bytes, layout(), cfg_.tile_bytes, max_blocks())) {
         CollArgs a;
         FillArgsCommon(&a);
-        a.user = user;
+        a.user = static_cast<char*>(buf);
         a.root = root;
-        a.off[0] = off;
-        a.len[0] = std::min(cap, bytes - off);
-        a.mis[0] = (uint32_t)(off % 16);
-        size_t tile = cfg_.tile_bytes ? cfg_.tile_bytes
-                                      : std::min<size_t>(std::max<size_t>(a.len[0] / (size_t)G, RDC_MIN_TILE),
-                                                         (size_t)1 << 20);
-        tile = std::max<size_t>(round_up(tile, RDC_SLOT_ALIGN), RDC_MIN_TILE);
-        a.tile_bytes = tile;
-        a.tiles[0] = (int)((a.len[0] + tile - 1) / tile);
+        a.off[0] = p.off[0];
+        a.len[0] = p.len[0];
+        a.mis[0] = p.mis[0];
+        a.tiles[0] = p.tiles[0];
+        a.tile_bytes = p.tile_bytes;
         a.seq = ++seq_;
-        hip_check(launch_bcast(a, std::max(1, std::min(a.tiles[0], G)), stream), "launch broadcast");
+        hip_check(launch_bcast(a, p.nb_scatter, stream), "launch broadcast");
     }
 }
 
 void Communicator::Check(hipStream_t stream) {
+    if (err_ == nullptr) return;  // world size 1: nothing was ever launched
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamSynchronize(stream), "stream sync");
     uint32_t e = 0;

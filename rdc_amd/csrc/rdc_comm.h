@@ -19,6 +19,7 @@
 
 #include "rdc_bootstrap.h"
 #include "rdc_common.h"
+#include "rdc_plan.h"
 
 namespace rdc_amd {
 
@@ -54,9 +55,8 @@ public:
     size_t slot_bytes() const { return slot_bytes_; }
     uint32_t seq() const { return seq_; }
     const CommConfig& config() const { return cfg_; }
-    // plan introspection for tests: tile bytes and grid the next allreduce of
-    // `piece_chunk_bytes` per chunk would use
-    void Plan(size_t chunk_bytes, int algo, size_t* tile, int* nb_s, int* nb_r, int* nb_g) const;
+    Layout layout() const;
+    int max_blocks() const;
 
 private:
     Communicator() {}
@@ -69,7 +69,6 @@ private:
     CommConfig cfg_;
     Bootstrap* bs_ = nullptr;       // not owned
     bool owns_peers_ipc_ = false;   // peers opened through IPC
-    static constexpr size_t kMaxRegionBytes = (size_t)2040 << 20;
     char* scratch_ = nullptr;       // RS region
     char* scratch_ag_ = nullptr;    // AG region
     uint32_t* flags_ = nullptr;

@@ -1,0 +1,114 @@
+// Host-side planning (see rdc_plan.h).
+#include "rdc_plan.h"
+
+#include <string.h>
+
+#include <algorithm>
+
+namespace rdc_amd {
+
+namespace {
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+size_t round_down(size_t x, size_t a) { return x / a * a; }
+}  // namespace
+
+Layout MakeLayout(int n, size_t scratch_bytes) {
+    Layout L;
+    const size_t region = std::min<size_t>(scratch_bytes / 2, kMaxRegionBytes);
+    size_t slot = round_down(region / (size_t)n, 4096);
+    if (slot < 64 * 1024 || n == 1) slot = 64 * 1024;  // world size 1 never moves data
+    L.slot_bytes = slot;
+    L.region_bytes = slot * (size_t)n;
+    L.max_tiles = (uint32_t)(L.region_bytes / RDC_MIN_TILE + 2);
+    L.flag_bytes = round_up((size_t)2 * n * L.max_tiles * sizeof(uint32_t), 4096);
+    return L;
+}
+
+void SplitRanges(int64_t count, int n, int64_t* b, int64_t* e) {
+    const int64_t k = count / n, m = count % n;
+    for (int i = 0; i < n; ++i) {
+        b[i] = (int64_t)i * k + std::min<int64_t>(i, m);
+        e[i] = (int64_t)(i + 1) * k + std::min<int64_t>(i + 1, m);
+    }
+}
+
+void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blocks, Piece* p) {
+    size_t t = cfg_tile;
+    if (t == 0) {
+        // mesh: ~64 tiles per chunk keeps every reduce block busy; ring: each
+        // block walks 2(n-1) hand-offs per tile, so aim for one tile per block.
+        const size_t want = algo == RDC_ALGO_RING ? chunk_bytes / (size_t)std::max(1, max_blocks) : chunk_bytes / 64;
+        t = std::min<size_t>(std::max<size_t>(want, RDC_MIN_TILE), (size_t)1 << 20);
+    }
+    t = std::max<size_t>(round_up(t, RDC_SLOT_ALIGN), RDC_MIN_TILE);
+    p->tile_bytes = t;
+    const int T = (int)((chunk_bytes + t - 1) / t);
+    const int G = std::max(1, max_blocks);
+    if (algo == RDC_ALGO_RING) {
+        p->nb_scatter = std::max(1, std::min(T, G));
+        p->nb_reduce = p->nb_gather = 0;
+        return;
+    }
+    const int items_s = (n - 1) * T;
+    const int s = std::max(1, std::min(items_s, G * 3 / 8));
+    const int r = std::max(1, std::min(T, G * 3 / 8));
+    const int g = std::max(1, std::min(items_s, G - s - r));
+    p->nb_scatter = s;
+    p->nb_reduce = r;
+    p->nb_gather = g;
+}
+
+std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout& L, int algo, size_t cfg_tile,
+                                 int max_blocks) {
+    std::vector<Piece> out;
+    if (n <= 1 || count == 0 || esz == 0) return out;
+    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+    SplitRanges((int64_t)count, n, cb, ce);
+    const int64_t maxlen = ce[0] - cb[0];  // the first chunk is never shorter
+    // a piece occupies at most slot - 256 bytes (+ < 16 bytes of alignment slack)
+    const int64_t pe = (int64_t)(round_down(L.slot_bytes - RDC_SLOT_ALIGN, RDC_SLOT_ALIGN) / esz);
+    const int64_t npieces = (maxlen + pe - 1) / pe;
+    for (int64_t k = 0; k < npieces; ++k) {
+        Piece p;
+        memset(&p, 0, sizeof(p));
+        size_t chunk_max = 0;
+        for (int c = 0; c < n; ++c) {
+            const int64_t b0 = cb[c] + k * pe;
+            const int64_t e0 = std::min(ce[c], b0 + pe);
+            if (e0 > b0) {
+                p.off[c] = (uint64_t)b0 * esz;
+                p.len[c] = (uint64_t)(e0 - b0) * esz;
+            }
+            // buffer-relative: every rank places chunk c's bytes identically
+            p.mis[c] = (uint32_t)(p.off[c] % 16);
+            chunk_max = std::max<size_t>(chunk_max, p.len[c]);
+        }
+        PlanTiles(chunk_max, n, algo, cfg_tile, max_blocks, &p);
+        for (int c = 0; c < n; ++c) p.tiles[c] = (int)((p.len[c] + p.tile_bytes - 1) / p.tile_bytes);
+        out.push_back(p);
+    }
+    return out;
+}
+
+std::vector<Piece> PlanBroadcast(uint64_t bytes, const Layout& L, size_t cfg_tile, int max_blocks) {
+    std::vector<Piece> out;
+    const size_t cap = round_down(L.region_bytes - RDC_SLOT_ALIGN, RDC_SLOT_ALIGN);
+    const int G = std::max(1, max_blocks);
+    for (uint64_t off = 0; off < bytes; off += cap) {
+        Piece p;
+        memset(&p, 0, sizeof(p));
+        p.off[0] = off;
+        p.len[0] = std::min<uint64_t>(cap, bytes - off);
+        p.mis[0] = (uint32_t)(off % 16);
+        size_t t = cfg_tile ? cfg_tile
+                            : std::min<size_t>(std::max<size_t>(p.len[0] / (size_t)G, RDC_MIN_TILE), (size_t)1 << 20);
+        t = std::max<size_t>(round_up(t, RDC_SLOT_ALIGN), RDC_MIN_TILE);
+        p.tile_bytes = t;
+        p.tiles[0] = (int)((p.len[0] + t - 1) / t);
+        p.nb_scatter = std::max(1, std::min(p.tiles[0], G));
+        out.push_back(p);
+    }
+    return out;
+}
+
+}  // namespace rdc_amd

@@ -1,0 +1,51 @@
+// Host-side planning of one device collective: chunk map, pieces, tiles and
+// block roles.  Pure functions (no HIP calls), so the CPU tests exercise the
+// exact logic the launches use (exported as RdcPlanAllreduce/RdcPlanLayout).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "rdc_common.h"
+
+namespace rdc_amd {
+
+// scratch geometry of one communicator (identical on every rank)
+struct Layout {
+    size_t slot_bytes = 0;    // one slot = one chunk piece (+ alignment slack)
+    size_t region_bytes = 0;  // n slots; RS and AG regions are separate allocations
+    uint32_t max_tiles = 0;   // flag-row length
+    size_t flag_bytes = 0;    // [2][n][max_tiles] uint32, rounded to 4 KiB
+};
+// RS / AG regions are capped below 2 GiB: on ROCm 7.2 (dmabuf IPC)
+// hipIpcOpenMemHandle of an allocation >= 2 GiB never returns
+// (measured on MI355X: 2044 MiB opens, 2048 MiB hangs).
+constexpr size_t kMaxRegionBytes = (size_t)2040 << 20;
+Layout MakeLayout(int n, size_t scratch_bytes);
+
+// utils::Split (include/utils/utils.h:59-70) in 64-bit arithmetic: the first
+// count % n chunks get one extra element; same ranges as the reference for
+// every count its int version can represent.
+void SplitRanges(int64_t count, int n, int64_t* begin, int64_t* end);
+
+struct Piece {
+    uint64_t off[RDC_MAX_RANKS];  // byte offset of chunk c's piece in the user buffer
+    uint64_t len[RDC_MAX_RANKS];  // byte length (0 = chunk c has nothing in this piece)
+    uint32_t mis[RDC_MAX_RANKS];  // off % 16: where the piece sits inside its scratch slot
+    int tiles[RDC_MAX_RANKS];     // ceil(len / tile_bytes)
+    uint64_t tile_bytes;
+    int nb_scatter, nb_reduce, nb_gather;  // mesh roles; ring uses nb_scatter as its grid
+};
+
+// tile size and grid for a piece whose largest chunk is chunk_bytes
+void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blocks, Piece* p);
+
+// Every launch of an allreduce of `count` elements of `esz` bytes.
+std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout& L, int algo, size_t cfg_tile,
+                                 int max_blocks);
+
+// Broadcast pieces of `bytes` (use off/len/mis/tiles [0]).
+std::vector<Piece> PlanBroadcast(uint64_t bytes, const Layout& L, size_t cfg_tile, int max_blocks);
+
+}  // namespace rdc_amd

@@ -1,0 +1,48 @@
+// Known-answer program over include/rdc.h, following the checks of the
+// reference's test/allreduce.cc:17-55 and test/broadcast.cc: every rank holds
+// a[i] = rank + N + i; Allreduce<Max> must give (W-1)+N+i and Allreduce<Sum>
+// sum_j (j+N+i); a broadcast string from rank 0 must arrive intact.
+// Buffers live in host memory (the reference's own setting): the library
+// stages them through HBM and runs the device allreduce.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "rdc.h"
+
+static int fail(const char* what, int i, long got, long want) {
+    fprintf(stderr, "rank %d: %s mismatch at %d: %ld != %ld\n", rdc::GetRank(), what, i, got, want);
+    return 1;
+}
+
+int main(int argc, char* argv[]) {
+    rdc::Init(argc, argv);
+    rdc::NewCommunicator(rdc::kMainCommName);
+    const int N = argc >= 2 ? atoi(argv[1]) : 3;
+    const int W = rdc::GetWorldSize(), R = rdc::GetRank();
+    std::vector<int> a(N);
+    for (int i = 0; i < N; ++i) a[i] = R + N + i;
+    rdc::Allreduce<rdc::op::Max>(&a[0], N);
+    for (int i = 0; i < N; ++i)
+        if (a[i] != (W - 1) + N + i) return fail("max", i, a[i], (W - 1) + N + i);
+    for (int i = 0; i < N; ++i) a[i] = R + N + i;
+    rdc::Allreduce<rdc::op::Sum>(&a[0], N);
+    for (int i = 0; i < N; ++i) {
+        long want = 0;
+        for (int j = 0; j < W; ++j) want += j + N + i;
+        if (a[i] != want) return fail("sum", i, a[i], want);
+    }
+    std::string s = R == 0 ? "hello world" : "";
+    rdc::Broadcast(s, 0);
+    if (s != "hello world") return fail("broadcast", 0, (long)s.size(), 11);
+    std::vector<double> v;
+    if (R == W - 1) v = {1.5, -2.25, 3.0};
+    rdc::Broadcast(v, W - 1);
+    if (v.size() != 3 || v[1] != -2.25) return fail("broadcast vector", 0, (long)v.size(), 3);
+    printf("rank %d: known-answer OK (world %d, N %d)\n", R, W, N);
+    rdc::Finalize();
+    return 0;
+}

@@ -1,0 +1,59 @@
+"""GPU: the reference-shaped entry points end to end.
+
+* the C++ header (include/rdc.h) known-answer program — test/allreduce.cc's
+  checks — as 2 and 3 processes on GPU 0, host buffers staged through HBM;
+* bench.py launched exactly as the driver launches it for N > 1
+  (torch.distributed.run, one process per rank; here all ranks share GPU 0).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tests.conftest import ROOT, free_port
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def known_answer_exe(tmp_path_factory):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    exe = str(tmp_path_factory.mktemp("cpp") / "known_answer")
+    subprocess.check_call(["g++", "-std=c++11", "-O1", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "known_answer.cc"), "-o", exe,
+                           "-L", os.path.join(ROOT, "rdc_amd"), "-lrdc_amd",
+                           "-Wl,-rpath," + os.path.join(ROOT, "rdc_amd")])
+    return exe
+
+
+@pytest.mark.parametrize("world,N", [(2, 3), (3, 1024), (3, 100003)])
+def test_cpp_known_answer(known_answer_exe, world, N):
+    port = free_port()
+    env = dict(os.environ, RDC_DEVICE="0", RDC_SCRATCH_BYTES="64M", RDC_NBLOCKS="32")
+    procs = [subprocess.Popen([known_answer_exe, str(N), "RDC_RANK=%d" % r, "rdc_world_size=%d" % world,
+                               "RDC_TRACKER_URI=127.0.0.1", "RDC_TRACKER_PORT=%d" % port],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(world)]
+    outs = [p.communicate(timeout=180)[0] for p in procs]
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, o[-2000:]
+        assert "rank %d: known-answer OK" % r in o
+
+
+def test_bench_torchrun_two_ranks():
+    port = free_port()
+    env = dict(os.environ, RDC_NBLOCKS="32")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--bytes", str(64 << 20)]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["roofline"]["bound"] == "xgmi"
+    assert out["config"]["bytes_per_gpu"] == 64 << 20

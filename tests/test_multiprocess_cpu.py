@@ -1,0 +1,139 @@
+"""CPU, world size > 1.
+
+* the native TCP bootstrap (tracker replacement, rdc_amd/csrc/rdc_bootstrap.cpp):
+  rank/world from env or argv key=val, barrier, connect timeout;
+* the mesh decomposition under torch.distributed gloo (world size 2 and 3):
+  each rank folds ONLY its own Split chunk in the reference ring's order from
+  all ranks' inputs, then the owners' chunks are gathered — exactly the work
+  split k_mesh performs — and must equal the oracle's ring allreduce
+  bit-for-bit on every rank.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.conftest import ROOT, free_port
+
+
+def clean_env():
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    return e
+
+
+BOOT = r'''
+import sys, rdc_amd as r
+r.init(sys.argv[1:])
+for _ in range(5):
+    r.barrier()
+print("rank %d/%d ok" % (r.get_rank(), r.get_world_size()), flush=True)
+r.finalize()
+'''
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_tcp_bootstrap(world):
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, "-c", BOOT, "RDC_RANK=%d" % r, "rdc_world_size=%d" % world,
+                               "RDC_TRACKER_URI=127.0.0.1", "RDC_TRACKER_PORT=%d" % port],
+                              cwd=ROOT, env=clean_env(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(world)]
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, o
+        assert "rank %d/%d ok" % (r, world) in o
+
+
+def test_torchrun_env_fallback():
+    """RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT (+1 = tracker port) as under torchrun."""
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = clean_env()
+        env.update(RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port - 1))
+        procs.append(subprocess.Popen([sys.executable, "-c", BOOT], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+
+
+def test_bootstrap_timeout_is_an_error():
+    code = r'''
+import rdc_amd as r
+from rdc_amd._lib import RdcError
+try:
+    r.init(["RDC_RANK=1", "RDC_WORLD_SIZE=2", "RDC_TRACKER_PORT=%d", "RDC_BOOTSTRAP_TIMEOUT=1"])
+except RdcError as e:
+    assert "connect" in str(e); print("OK")
+''' % free_port()
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=clean_env(), capture_output=True, text=True,
+                       timeout=60)
+    assert "OK" in p.stdout, p.stdout + p.stderr
+
+
+def fold_chunk(parts, c, dtype, op):
+    """Chunk c's ring order: s = x[c-1]; s = OP(x[c-2], s); ...; s = OP(x[c], s)
+    (OP(dst, src) = op::Reducer with dst the rank's own value)."""
+    n = len(parts)
+    acc = parts[(c - 1) % n].copy()
+    for k in range(2, n + 1):
+        dst = parts[(c - k) % n].copy()
+        O.reducer(acc, dst, dtype, op)
+        acc = dst
+    return acc
+
+
+def _gloo_worker(rank, world, port, count, dtype, op, q):
+    try:
+        _gloo_body(rank, world, port, count, dtype, op, q)
+    except Exception as e:  # report instead of leaving the parent waiting
+        q.put((rank, repr(e)))
+
+
+def _gloo_body(rank, world, port, count, dtype, op, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = O.fill(count, dtype, 0x5EED0000, rank)
+    # exchange inputs (stand-in for the scatter stage's pushes)
+    xs = [torch.empty(count, dtype=torch.from_numpy(x).dtype) for _ in range(world)]
+    dist.all_gather(xs, torch.from_numpy(x))
+    inputs = [t.numpy() for t in xs]
+    # owner computes its chunk in ring order (k_mesh's reduce role)
+    b, e = O.split(count, world)[rank]
+    part = [np.ascontiguousarray(v[b:e]) for v in inputs]
+    mine = fold_chunk(part, rank, dtype, op)
+    # gather the owners' results (k_mesh's allgather role); gloo wants equal
+    # sizes, so pad every chunk to the first (longest) one and trim after
+    sizes = [e2 - b2 for b2, e2 in O.split(count, world)]
+    padded = np.zeros(sizes[0], dtype=x.dtype)
+    padded[: mine.size] = mine
+    outs = [torch.empty(sizes[0], dtype=torch.from_numpy(x).dtype) for _ in sizes]
+    dist.all_gather(outs, torch.from_numpy(padded))
+    got = np.concatenate([t.numpy()[:s] for t, s in zip(outs, sizes)])
+    want = O.expected_allreduce(inputs, dtype, op)
+    q.put((rank, got.tobytes() == want.tobytes()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("count,dtype,op", [(1001, O.DT_FLOAT32, O.OP_SUM), (4099, O.DT_FLOAT64, O.OP_MAX),
+                                            (7, O.DT_INT32, O.OP_SUM)])
+def test_gloo_owner_computes_matches_ring(world, count, dtype, op):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, world, port, count, dtype, op, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(res[r] is True for r in range(world)), res

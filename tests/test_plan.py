@@ -1,0 +1,95 @@
+"""CPU: host-side planning of device collectives (rdc_amd/csrc/rdc_plan.cpp via
+RdcPlanAllreduce / RdcPlanLayout) — the exact logic the launches use.
+
+Checks that for every (n, count, dtype, scratch) the launches cover each
+Split chunk (include/utils/utils.h:59-70) exactly once, in order, that every
+piece fits its scratch slot, tiles and flag indices stay in range, and the
+scratch placement is rank-independent (off % 16)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+WORDS = 68
+
+
+def plan(n, count, dtype, scratch, algo=2, tile=0, max_blocks=256):
+    from rdc_amd._lib import _LIB
+    npieces = ctypes.c_int()
+    rc = _LIB.RdcPlanAllreduce(n, count, dtype, scratch, algo, tile, max_blocks, None, 0, ctypes.byref(npieces))
+    assert rc == 0, _LIB.RdcGetLastError()
+    k = npieces.value
+    buf = (ctypes.c_uint64 * (WORDS * max(1, k)))()
+    assert _LIB.RdcPlanAllreduce(n, count, dtype, scratch, algo, tile, max_blocks, buf, k, ctypes.byref(npieces)) == 0
+    arr = np.frombuffer(buf, dtype=np.uint64).reshape(max(1, k), WORDS)[:k]
+    out = []
+    for row in arr:
+        out.append(dict(tile=int(row[0]), nb=(int(row[1]), int(row[2]), int(row[3])),
+                        off=[int(x) for x in row[4:4 + n]], len=[int(x) for x in row[20:20 + n]],
+                        mis=[int(x) for x in row[36:36 + n]], tiles=[int(x) for x in row[52:52 + n]]))
+    return out
+
+
+def layout(n, scratch):
+    from rdc_amd._lib import _LIB
+    out = (ctypes.c_uint64 * 4)()
+    assert _LIB.RdcPlanLayout(n, scratch, out) == 0
+    return dict(slot=out[0], region=out[1], max_tiles=out[2], flag_bytes=out[3])
+
+
+CASES = [(n, count, dt, scratch)
+         for n in (2, 3, 5, 8, 16)
+         for count in (1, 2, 15, 1001, 4099, 1 << 20, (3 << 22) + 7)
+         for dt in (O.DT_INT8, O.DT_FLOAT16, O.DT_FLOAT32, O.DT_FLOAT64)
+         for scratch in (1 << 20, 24 << 20, 0)]
+
+
+@pytest.mark.parametrize("n,count,dt,scratch", CASES[::3])
+@pytest.mark.parametrize("algo", [1, 2])
+def test_plan_covers_chunks(n, count, dt, scratch, algo):
+    esz = np.dtype(O.NP_DTYPE[dt]).itemsize
+    L = layout(n, scratch)
+    pieces = plan(n, count, dt, scratch, algo)
+    ranges = O.split(count, n)
+    nxt = [b * esz for b, _ in ranges]
+    for p in pieces:
+        t = p["tile"]
+        assert t % 256 == 0 and t >= 16 << 10
+        nb_s, nb_r, nb_g = p["nb"]
+        if algo == 2:
+            assert min(nb_s, nb_r, nb_g) >= 1 and nb_s + nb_r + nb_g <= 256
+        else:
+            assert nb_s >= 1
+        for c in range(n):
+            ln = p["len"][c]
+            assert p["mis"][c] == (p["off"][c] % 16)
+            assert p["mis"][c] + ln <= L["slot"]           # fits its scratch slot
+            assert p["tiles"][c] == -(-ln // t)
+            assert p["tiles"][c] <= L["max_tiles"]         # flag index in range
+            if ln:
+                assert p["off"][c] == nxt[c]               # contiguous, in order
+                nxt[c] += ln
+    for c in range(n):
+        assert nxt[c] == ranges[c][1] * esz                # each chunk covered exactly once
+
+
+def test_layout_regions_below_2gib():
+    for n in (1, 2, 8, 16):
+        for scratch in (1 << 20, 4080 << 20, 16 << 30):
+            L = layout(n, scratch)
+            assert L["region"] < (2 << 30)                   # hipIpcOpenMemHandle limit
+            assert L["slot"] * n == L["region"]
+            assert L["flag_bytes"] >= 2 * n * L["max_tiles"] * 4
+
+
+def test_default_scratch_fits_cfg3_in_one_launch():
+    """1 GiB fp32 over 8 ranks: one launch per allreduce with the default scratch."""
+    assert len(plan(8, (1 << 30) // 4, O.DT_FLOAT32, 0)) == 1
+    assert len(plan(2, (256 << 20) // 4, O.DT_FLOAT32, 0)) == 1
+
+
+def test_empty_and_world1():
+    assert plan(4, 0, O.DT_FLOAT32, 0) == []
+    assert plan(1, 100, O.DT_FLOAT32, 0) == []
