@@ -39,9 +39,10 @@ def test_cpp_known_answer(known_answer_exe, world, N):
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
              for r in range(world)]
     outs = [p.communicate(timeout=180)[0] for p in procs]
+    report = "\n".join("--- rank %d rc=%s\n%s" % (r, p.returncode, o[-1500:]) for r, (p, o) in enumerate(zip(procs, outs)))
     for r, (p, o) in enumerate(zip(procs, outs)):
-        assert p.returncode == 0, o[-2000:]
-        assert "rank %d: known-answer OK" % r in o
+        assert p.returncode == 0, report
+        assert "rank %d: known-answer OK" % r in o, report
 
 
 def test_bench_torchrun_two_ranks():

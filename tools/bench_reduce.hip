@@ -60,6 +60,63 @@ __global__ __launch_bounds__(B) void k_bc(v4u* __restrict__ d, const v4u* __rest
     for (; i < hi; i += B) ST<NTS>(d + i, reduce16<RDC_OP_SUM, float>(LD<NTL, NTS>(d + i), LD<NTL, NTS>(s + i)));
 }
 
+// block-contiguous, software pipelined: next iteration's loads issued before
+// this iteration's stores
+template <int U, int B>
+__global__ __launch_bounds__(B) void k_bcp(v4u* __restrict__ d, const v4u* __restrict__ s, uint64_t nvec) {
+    const uint64_t per = ((nvec + gridDim.x - 1) / gridDim.x + U * B - 1) / (U * B) * (U * B);
+    const uint64_t lo = (uint64_t)blockIdx.x * per;
+    uint64_t hi = lo + per;
+    if (hi > nvec) hi = nvec;
+    if (lo >= hi) return;
+    uint64_t i = lo + threadIdx.x;
+    v4u a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t j = i + u * B;
+        if (j < hi) { a[u] = LD<true, true>(d + j); b[u] = LD<true, true>(s + j); }
+    }
+    for (; i < hi; i += U * B) {
+        v4u na[U], nb[U];
+        const uint64_t ni = i + U * B;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = ni + u * B;
+            if (j < hi) { na[u] = LD<true, true>(d + j); nb[u] = LD<true, true>(s + j); }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = i + u * B;
+            if (j < hi) ST<true>(d + j, reduce16<RDC_OP_SUM, float>(a[u], b[u]));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) { a[u] = na[u]; b[u] = nb[u]; }
+    }
+}
+
+// wave-contiguous: each wave owns a contiguous span, U x 1 KiB per step
+template <int U, int B>
+__global__ __launch_bounds__(B) void k_wc(v4u* __restrict__ d, const v4u* __restrict__ s, uint64_t nvec) {
+    const int waves = gridDim.x * (B / 64);
+    const int w = blockIdx.x * (B / 64) + threadIdx.x / 64;
+    const int lane = threadIdx.x & 63;
+    const uint64_t per = (nvec + waves - 1) / waves;
+    const uint64_t lo = (uint64_t)w * per;
+    uint64_t hi = lo + per;
+    if (hi > nvec) hi = nvec;
+    uint64_t i = lo + lane;
+    for (; i + (U - 1) * 64 < hi; i += U * 64) {
+        v4u a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = LD<true, true>(d + i + u * 64);
+#pragma unroll
+        for (int u = 0; u < U; ++u) b[u] = LD<true, true>(s + i + u * 64);
+#pragma unroll
+        for (int u = 0; u < U; ++u) ST<true>(d + i + u * 64, reduce16<RDC_OP_SUM, float>(a[u], b[u]));
+    }
+    for (; i < hi; i += 64) ST<true>(d + i, reduce16<RDC_OP_SUM, float>(LD<true, true>(d + i), LD<true, true>(s + i)));
+}
+
 #define CK(x)                                                                  \
     do {                                                                       \
         hipError_t e = (x);                                                    \
@@ -86,21 +143,22 @@ int main(int argc, char** argv) {
     CK(hipMemset(d, 0, S));
     CK(hipMemset(s, 0, S));
     std::vector<Variant> vs = {
-        {"gs U4 nt/nt B256", (KFn)k_gs<4, true, true, 256>, 256},
-        {"gs U4 plain B256", (KFn)k_gs<4, false, false, 256>, 256},
-        {"gs U4 ntL/plainS B256", (KFn)k_gs<4, true, false, 256>, 256},
-        {"gs U4 plainL/ntS B256", (KFn)k_gs<4, false, true, 256>, 256},
-        {"gs U8 nt/nt B256", (KFn)k_gs<8, true, true, 256>, 256},
-        {"gs U8 plain B256", (KFn)k_gs<8, false, false, 256>, 256},
-        {"gs U2 nt/nt B256", (KFn)k_gs<2, true, true, 256>, 256},
-        {"gs U4 nt/nt B512", (KFn)k_gs<4, true, true, 512>, 512},
-        {"gs U4 plain B512", (KFn)k_gs<4, false, false, 512>, 512},
         {"bc U4 nt/nt B256", (KFn)k_bc<4, true, true, 256>, 256},
-        {"bc U4 plain B256", (KFn)k_bc<4, false, false, 256>, 256},
-        {"bc U8 plain B256", (KFn)k_bc<8, false, false, 256>, 256},
-        {"bc U8 nt/nt B256", (KFn)k_bc<8, true, true, 256>, 256},
+        {"bc U2 nt/nt B256", (KFn)k_bc<2, true, true, 256>, 256},
+        {"bc U4 nt/nt B512", (KFn)k_bc<4, true, true, 512>, 512},
+        {"bc U2 nt/nt B512", (KFn)k_bc<2, true, true, 512>, 512},
+        {"bc U4 nt/nt B1024", (KFn)k_bc<4, true, true, 1024>, 1024},
+        {"bc U8 nt/nt B128", (KFn)k_bc<8, true, true, 128>, 128},
+        {"bc U4 ntL/plainS B256", (KFn)k_bc<4, true, false, 256>, 256},
+        {"bcp U2 B256", (KFn)k_bcp<2, 256>, 256},
+        {"bcp U4 B256", (KFn)k_bcp<4, 256>, 256},
+        {"bcp U2 B512", (KFn)k_bcp<2, 512>, 512},
+        {"wc U4 B256", (KFn)k_wc<4, 256>, 256},
+        {"wc U8 B256", (KFn)k_wc<8, 256>, 256},
+        {"wc U4 B512", (KFn)k_wc<4, 512>, 512},
+        {"gs U2 nt/nt B256", (KFn)k_gs<2, true, true, 256>, 256},
     };
-    const int grids[] = {512, 1024, 2048, 4096, 8192, 16384};
+    const int grids[] = {256, 512, 1024, 2048, 4096, 8192};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -108,7 +166,7 @@ int main(int argc, char** argv) {
         for (int g : grids) {
             for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(v.fn, dim3(g), dim3(v.block), 0, 0, d, s, nvec);
             CK(hipDeviceSynchronize());
-            const int it = 20;
+            const int it = 30;
             CK(hipEventRecord(e0));
             for (int k = 0; k < it; ++k) hipLaunchKernelGGL(v.fn, dim3(g), dim3(v.block), 0, 0, d, s, nvec);
             CK(hipEventRecord(e1));

@@ -1,0 +1,55 @@
+"""Summarise rocprofv3 PMC passes into HBM bytes per launch.
+
+    python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> \
+        <kernel-substring> <key> [profiles/traffic.json]
+
+Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KB;
+on gfx950 FETCH_SIZE reports exactly half the bytes of a wide (16 B/lane)
+coalesced streaming read, so it is doubled; WRITE_SIZE is exact for
+16-B-per-lane streaming stores.  FETCH_SIZE and WRITE_SIZE were collected in
+separate passes (they do not fit one pass of TCC counters).
+"""
+import csv
+import json
+import os
+import statistics
+import sys
+
+
+def per_launch(path, counter, kern):
+    vals = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] == counter and kern in row["Kernel_Name"]:
+                vals.append(float(row["Counter_Value"]))
+    if not vals:
+        raise SystemExit("no %s rows for %s in %s" % (counter, kern, path))
+    return statistics.median(vals), len(vals)
+
+
+def main():
+    fetch_csv, write_csv, kern, key = sys.argv[1:5]
+    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles",
+                                                            "traffic.json")
+    f_kb, nf = per_launch(fetch_csv, "FETCH_SIZE", kern)
+    w_kb, nw = per_launch(write_csv, "WRITE_SIZE", kern)
+    read_b = 2 * f_kb * 1024      # gfx950: FETCH_SIZE = half the streamed bytes
+    write_b = w_kb * 1024
+    try:
+        data = json.load(open(out))
+    except (OSError, ValueError):
+        data = {}
+    data[key] = int(read_b + write_b)
+    data.setdefault("_detail", {})[key] = {
+        "kernel": kern, "FETCH_SIZE_KB_median": f_kb, "WRITE_SIZE_KB_median": w_kb, "launches": [nf, nw],
+        "read_bytes_corrected": int(read_b), "write_bytes": int(write_b),
+        "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count for 16-B streaming reads); "
+                      "write = WRITE_SIZE x 1024",
+    }
+    with open(out, "w") as fh:
+        json.dump(data, fh, indent=1, sort_keys=True)
+    print(json.dumps({key: data[key]}))
+
+
+if __name__ == "__main__":
+    main()
