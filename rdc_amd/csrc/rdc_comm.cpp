@@ -85,7 +85,7 @@ void Communicator::AllocLocal() {
     scratch_ag_ = static_cast<char*>(alloc_shared(region_bytes_, &k3));
     flags_ = static_cast<uint32_t*>(alloc_shared(flag_bytes_, &k2));
     alloc_kind_ = std::max(std::max(k1, k2), k3);
-    hip_check(hipMalloc(&err_, 64), "hipMalloc err");
+    hip_check(hipMalloc(&err_, 64), "hipMalloc err");  // [0] error word, [16] launch arrival counter
     hip_check(hipMemset(flags_, 0, flag_bytes_), "memset flags");
     hip_check(hipMemset(err_, 0, 64), "memset err");
     hip_check(hipDeviceSynchronize(), "sync after alloc");
@@ -248,6 +248,7 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
         a->flags[p] = peer_flags_[p];
     }
     a->err = err_;
+    a->done_ctr = err_ + 16;
     a->timeout_ticks = (uint64_t)(cfg_.timeout_s * (double)wall_khz_ * 1000.0);
 }
 

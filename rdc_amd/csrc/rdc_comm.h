@@ -4,7 +4,7 @@
 //
 // HBM layout per rank (uncached allocations, IPC-exported, each < 2 GiB):
 //   RS region : n slots x slot_bytes      AG region : n slots x slot_bytes
-// and a flag array (uncached, IPC-exported): uint32 [2][n][max_tiles].
+// and a flag array (uncached, IPC-exported): uint32 [2n][max_tiles] + done[n].
 //   mesh : RS slot p  <- rank p's copy of my chunk;   AG slot c <- owner c's result
 //   ring : RS slot j  <- reduce-scatter step j;       AG slot j <- allgather step j
 //   bcast: the whole AG region holds the root's piece

@@ -75,8 +75,9 @@ struct CollArgs {
     uint32_t max_tiles;                  // flag array row stride
     char* rs[RDC_MAX_RANKS];             // rank p's reduce-scatter scratch region
     char* ag[RDC_MAX_RANKS];             // rank p's allgather scratch region
-    uint32_t* flags[RDC_MAX_RANKS];      // rank p's flag region: [2][n][max_tiles]
+    uint32_t* flags[RDC_MAX_RANKS];      // rank p's flag region: [2n][max_tiles] + done[n]
     int nb_scatter, nb_reduce, nb_gather;  // mesh block roles
     uint32_t* err;                       // local device error word
+    uint32_t* done_ctr;                  // local per-launch block arrival counter (self-resetting)
     uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up
 };

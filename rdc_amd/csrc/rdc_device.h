@@ -199,7 +199,7 @@ __device__ __forceinline__ void block_copy_vec(char* __restrict__ dst, const cha
     if (tid < len - tail_start) dst[tail_start + tid] = src[tail_start + tid];
     const v4u* s = reinterpret_cast<const v4u*>(src + head);
     v4u* d = reinterpret_cast<v4u*>(dst + head);
-    constexpr int U = 4;
+    constexpr int U = 8;  // 32 KiB in flight per 256-thread block
     const uint64_t step = (uint64_t)blockDim.x;
     uint64_t i = tid;
     for (; i + (U - 1) * step < nvec; i += U * step) {

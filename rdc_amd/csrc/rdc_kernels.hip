@@ -26,6 +26,11 @@ namespace rdc_amd {
 
 constexpr int kBlock = 256;
 
+// rank `owner`'s flag word that rank `writer` sets when it finished a launch
+__device__ __forceinline__ uint32_t* done_word(const CollArgs& a, int owner, int writer) {
+    return a.flags[owner] + (uint64_t)(2 * a.n) * a.max_tiles + writer;
+}
+
 // =============================================================== reduce ===
 template <int OP, typename T>
 __device__ __forceinline__ void reduce_elems(char* dst, const char* src, uint64_t nelem, uint64_t first,
@@ -99,7 +104,7 @@ __device__ __forceinline__ void mesh_fold_elem(const CollArgs& a, char* own, con
 
 // Fold one tile of chunk r: out = ring-order reduction of the n ranks'
 // tile, written to the local user buffer and to every peer's allgather slot.
-template <int OP, typename T>
+template <int OP, typename T, int NMAX>
 __device__ void mesh_reduce_tile(const CollArgs& a, int t, uint64_t tlen) {
     const int n = a.n, r = a.rank;
     const uint64_t toff = (uint64_t)t * a.tile_bytes;
@@ -123,41 +128,42 @@ __device__ void mesh_reduce_tile(const CollArgs& a, int t, uint64_t tlen) {
         if (tid < nh) mesh_fold_elem<OP, T>(a, own, slot0, soff, tid * sizeof(T));
         else if (tid >= 64 && tid - 64 < nt) mesh_fold_elem<OP, T>(a, own, slot0, soff, tail + (tid - 64) * sizeof(T));
     }
-    constexpr int U = 2;
+    // All n contributions of U positions are loaded before folding (NMAX x U
+    // 16-B loads in flight per lane); folding one rank at a time inside a
+    // runtime loop would leave the lane latency-bound at n = 8.
+    constexpr int U = NMAX <= 8 ? 2 : 1;
     const uint64_t stride = kBlock;
-    uint64_t i = tid;
-    for (; i < nvec; i += U * stride) {
-        v4u acc[U];
+    for (uint64_t i = tid; i < nvec; i += U * stride) {
+        v4u v[U][NMAX];
         bool live[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) live[u] = i + u * stride < nvec;
-        int q = (r - 1 + n) % n;
-        {
+#pragma unroll
+        for (int k = 1; k <= NMAX; ++k) {
+            if (k > n) break;
+            const int q = (r - k + n) % n;  // k-th value in ring order: x[r-1], x[r-2], ..., x[r]
             const char* src = (q == r ? (const char*)own : slot0 + q * a.slot_bytes) + head;
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (live[u]) acc[u] = ld16_nt(src + (i + u * stride) * 16);
-        }
-        for (int k = 2; k <= n; ++k) {
-            q = (r - k + n) % n;
-            const char* src = (q == r ? (const char*)own : slot0 + q * a.slot_bytes) + head;
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (live[u]) acc[u] = reduce16<OP, T>(ld16_nt(src + (i + u * stride) * 16), acc[u]);
+                if (live[u]) v[u][k - 1] = ld16_nt(src + (i + u * stride) * 16);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (!live[u]) continue;
+            v4u acc = v[u][0];
+#pragma unroll
+            for (int k = 2; k <= NMAX; ++k)
+                if (k <= n) acc = reduce16<OP, T>(v[u][k - 1], acc);
             const uint64_t b = head + (i + u * stride) * 16;
-            st16(own + b, acc[u]);
+            st16(own + b, acc);
             for (int p = 0; p < n; ++p)
-                if (p != r) st16_nt(a.ag[p] + soff + b, acc[u]);
+                if (p != r) st16_nt(a.ag[p] + soff + b, acc);
         }
     }
 }
 
-template <int OP, typename T>
-__global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
+template <int OP, typename T, int NMAX>
+__device__ void mesh_body(const CollArgs& a) {
     const int n = a.n, r = a.rank;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     int b = blockIdx.x;
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
             const uint64_t toff = (uint64_t)t * a.tile_bytes;
             uint64_t tlen = a.len[r] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-            mesh_reduce_tile<OP, T>(a, t, tlen);
+            mesh_reduce_tile<OP, T, NMAX>(a, t, tlen);
             if (threadIdx.x < (unsigned)(n - 1)) {
                 const int p = (r + 1 + threadIdx.x) % n;
                 s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
@@ -260,7 +266,7 @@ __device__ void block_reduce_into(char* own, const char* recv, uint64_t len) {
 }
 
 template <int OP, typename T>
-__global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
+__device__ void ring_body(const CollArgs& a) {
     const int n = a.n, r = a.rank;
     const int prev = (r - 1 + n) % n;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
@@ -320,10 +326,21 @@ __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
 
 // ============================================================ broadcast ===
 // piece = [off[0], off[0]+len[0]) of the user buffer; tiles[0] tiles.
-__global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
+__device__ void bcast_body(const CollArgs& a) {
     const int n = a.n, r = a.rank, root = a.root;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
+    if (r == root && blockIdx.x < a.tiles[0]) {
+        // A broadcast's receivers never report back, so before overwriting a
+        // peer's allgather region the root waits until that peer finished
+        // its previous launch (done word >= seq-1).  Allreduce launches need
+        // no such gate: their peer writes depend on data the target only
+        // sends once it has entered the same launch.
+        if (threadIdx.x < (unsigned)(n - 1))
+            s_flags[threadIdx.x] = done_word(a, r, (root + 1 + threadIdx.x) % n);
+        __syncthreads();
+        if (!block_wait(s_flags, n - 1, a.seq - 1, ab, RDC_KERR_TIMEOUT_BCAST)) return;
+    }
     for (int t = blockIdx.x; t < a.tiles[0]; t += gridDim.x) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[0] - toff;
@@ -345,6 +362,43 @@ __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
             __syncthreads();
         }
     }
+}
+
+// ======================================================= launch epilogue ===
+// Every block of every collective launch ends here exactly once (also after
+// a timeout).  The last block to arrive resets the local arrival counter and
+// publishes done = seq into every peer's flag array (row 2n, column = this
+// rank): "this rank finished reading its scratch for launch seq".
+__device__ __forceinline__ void launch_done(const CollArgs& a) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t prev = atomicAdd(a.done_ctr, 1u);
+        if (prev == gridDim.x - 1) {
+            __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int p = 0; p < a.n; ++p)
+                if (p != a.rank) flag_store(done_word(a, p, a.rank), a.seq);
+        }
+    }
+}
+
+template <int OP, typename T, int NMAX>
+__global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
+    mesh_body<OP, T, NMAX>(a);
+    launch_done(a);
+}
+
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
+    ring_body<OP, T>(a);
+    launch_done(a);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
+    bcast_body(a);
+    launch_done(a);
 }
 
 // ================================================================= fill ===
@@ -391,7 +445,10 @@ struct Kernels {
         return hipGetLastError();
     }
     static hipError_t mesh(const CollArgs& a, int grid, hipStream_t s) {
-        hipLaunchKernelGGL((k_mesh<OP, T>), dim3(grid), dim3(kBlock), 0, s, a);
+        if (a.n <= 8)
+            hipLaunchKernelGGL((k_mesh<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_mesh<OP, T, 16>), dim3(grid), dim3(kBlock), 0, s, a);
         return hipGetLastError();
     }
     static hipError_t ring(const CollArgs& a, int grid, hipStream_t s) {

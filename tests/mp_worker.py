@@ -50,6 +50,20 @@ def main():
         p = buf.data_ptr() + pad
         check_call(_LIB.RdcFill(ctypes.c_void_p(p), count, dtype, c.get("seed", 0x5EED0000), rank, sp))
         log("rank", rank, "case", i, "filled")
+        if kind == "bcast_chain":
+            # stream-ordered chain without host syncs: refill, broadcast from a
+            # rotating root, accumulate — exposes a root overwriting a peer's
+            # scratch before the peer consumed the previous broadcast
+            acc = torch.zeros(count, dtype=torch.int32, device="cuda")
+            for k in range(c["steps"]):
+                root = (k * 3 + 1) % world
+                check_call(_LIB.RdcFill(ctypes.c_void_p(p), count, 2, c.get("seed", 0x5EED0000) + k, rank, sp))
+                check_call(_LIB.RdcCommBroadcast(comm.handle, ctypes.c_void_p(p), count * 4, root, sp))
+                check_call(_LIB.RdcReduce(ctypes.c_void_p(acc.data_ptr()), ctypes.c_void_p(p), count, 2, 2, sp))
+            comm.check(sp)
+            np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), acc.cpu().numpy().view(np.uint8))
+            print("rank %d case %d ok" % (rank, i), flush=True)
+            continue
         reps = c.get("reps", 1)
         for _ in range(reps):
             if kind == "allreduce":

@@ -160,6 +160,13 @@ def run_mp(world, cases, timeout=240, env_extra=None):
 
 def expected_for(case, world):
     dt = case["dtype"]
+    if case.get("kind") == "bcast_chain":
+        acc = np.zeros(case["count"], dtype=np.int32)
+        for k in range(case["steps"]):
+            root = (k * 3 + 1) % world
+            O.reducer(O.fill(case["count"], O.DT_INT32, case.get("seed", 0x5EED0000) + k, root), acc, O.DT_INT32,
+                      O.OP_SUM)
+        return [acc] * world
     inputs = [O.fill(case["count"], dt, case.get("seed", 0x5EED0000), r) for r in range(world)]
     kind = case.get("kind", "allreduce")
     if kind == "broadcast":
@@ -170,7 +177,7 @@ def expected_for(case, world):
     return bufs
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_mp_allreduce(world):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -188,6 +195,8 @@ def test_mp_allreduce(world):
         {"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"},
         {"count": 100003, "dtype": 6, "op": 2, "algo": 2, "pad_per_rank": 4},   # ranks' buffers differ mod 16
         {"count": 100003, "dtype": 10, "op": 0, "algo": 1, "pad_per_rank": 2},
+        {"count": 2, "dtype": 2, "kind": "bcast_chain", "steps": 40},
+        {"count": 300001, "dtype": 2, "kind": "bcast_chain", "steps": 12},
     ]
     tmp = run_mp(world, cases)
     for i, c in enumerate(cases):

@@ -1,0 +1,71 @@
+"""PCIe-inclusive rate of the host-resident allreduce (rdc's native setting:
+buffers begin and end in host memory).  Each call: H2D copy, device
+allreduce, D2H copy, synchronise (RdcAllreduce on a numpy buffer).
+
+    python -m torch.distributed.run --nproc-per-node N tools/host_path.py [bytes] [iters]
+    python tools/host_path.py [bytes] [iters]          # N = 1: H2D + reduce + D2H
+
+Prints one JSON line (rank 0) with GB/s = S / t per call (max over ranks).
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    S = int(float(sys.argv[1])) if len(sys.argv) > 1 else (256 << 20)
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    import numpy as np
+    import torch
+    import rdc_amd
+    from rdc_amd._lib import _LIB, check_call
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+    count = S // 4
+    host = np.random.default_rng(rank).standard_normal(count).astype(np.float32)
+    p = host.ctypes.data_as(ctypes.c_void_p)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        rdc_amd.init([])
+
+        def call():
+            check_call(_LIB.RdcAllreduce(p, count, 6, 2, None, None))
+    else:
+        d = torch.empty(count, dtype=torch.float32, device="cuda")
+        s = torch.empty(count, dtype=torch.float32, device="cuda")
+        src = np.ones(count, dtype=np.float32)
+
+        def call():  # the 1-GPU data point with host buffers: H2D x2, reduce, D2H
+            d.copy_(torch.from_numpy(host))
+            s.copy_(torch.from_numpy(src))
+            rdc_amd.reduce_(d, s, rdc_amd.Op.SUM)
+            host[:] = d.cpu().numpy()
+    call()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        call()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+    if rank == 0:
+        print(json.dumps({"host_path": True, "n": world, "bytes": S, "ms_per_call": round(dt * 1e3, 3),
+                          "GBps": round(S / dt / 1e9, 3), "memory": "pageable numpy"}), flush=True)
+    if world > 1:
+        dist.barrier()
+        rdc_amd.finalize()
+
+
+if __name__ == "__main__":
+    main()
