@@ -1,400 +1,10 @@
-// MI355X (gfx950) kernels of the rdc allreduce path.
-//
-//   k_reduce   : op::Reducer<OP,DType> on device (include/core/mpi.h:113-120):
-//                dst[i] = OP::Reduce(dst[i], src[i]) — 16-B coalesced lanes,
-//                4 independent 16-B loads per operand in flight per lane.
-//   k_mesh     : allreduce over all links.  Rank r owns chunk r of
-//                utils::Split(0,count,n) (include/utils/utils.h:59-70);
-//                scatter blocks push every other chunk's tiles to their
-//                owners' scratch; reduce blocks fold the n contributions in
-//                the reference ring's order (communicator_collective.cc:
-//                115-182 => s = x[r-1]; s = OP(x[r-2], s) ... s = OP(x[r], s))
-//                and push the result to every peer; gather blocks land the
-//                peers' results in the user buffer.  Bit-identical to the ring.
-//   k_ring     : the reference schedule itself — TryReduceScatterRing
-//                (:115-182) + TryAllgatherRing (:79-114): n-1 steps each,
-//                send to prev=(r-1)%n, receive from next, pipelined per tile.
-//   k_bcast    : root pushes every tile to all peers (src/comm/
-//                communicator_collective.cc:44-69 semantics, correct for n>=4).
-//   k_fill     : synthetic inputs, bit-identical to oracle rdc_oracle_fill.
-#include <hip/hip_runtime.h>
-
-#include "rdc_device.h"
-#include "rdc_kernels.h"
+// MI355X (gfx950) kernels of the rdc path that do not depend on the reduction
+// operator (broadcast, synthetic fill) and the (dtype, op) dispatch.
+//   per-operator instantiations: rdc_kernels_{max,min,sum,bitor}.hip
+//   device templates:            rdc_kernels_impl.h
+#include "rdc_kernels_impl.h"
 
 namespace rdc_amd {
-
-constexpr int kBlock = 256;
-
-// rank `owner`'s flag word that rank `writer` sets when it finished a launch
-__device__ __forceinline__ uint32_t* done_word(const CollArgs& a, int owner, int writer) {
-    return a.flags[owner] + (uint64_t)(2 * a.n) * a.max_tiles + writer;
-}
-
-// =============================================================== reduce ===
-template <int OP, typename T>
-__device__ __forceinline__ void reduce_elems(char* dst, const char* src, uint64_t nelem, uint64_t first,
-                                             uint64_t stride) {
-    T* d = reinterpret_cast<T*>(dst);
-    const T* s = reinterpret_cast<const T*>(src);
-    for (uint64_t i = first; i < nelem; i += stride) d[i] = OpF<OP>::apply(d[i], s[i]);
-}
-
-// dst and src congruent mod 16; nbytes a multiple of sizeof(T).  Each block
-// streams one contiguous span (DRAM-page friendly: 5.6 vs 4.6 TB/s for a
-// grid-stride walk in tools/bench_reduce.hip), U 16-B loads per operand in
-// flight per lane, non-temporal loads and stores (the bytes are touched once).
-template <int OP, typename T, int U>
-__global__ __launch_bounds__(kBlock) void k_reduce(char* __restrict__ dst, const char* __restrict__ src,
-                                                   uint64_t nbytes) {
-    const uint64_t mis = (uint64_t)(uintptr_t)dst & 15;
-    uint64_t head = mis ? 16 - mis : 0;
-    if (head > nbytes) head = nbytes;
-    const uint64_t nvec = (nbytes - head) >> 4;
-    const uint64_t tail = head + (nvec << 4);
-    if (blockIdx.x == 0) {
-        reduce_elems<OP, T>(dst, src, head / sizeof(T), threadIdx.x, kBlock);
-        reduce_elems<OP, T>(dst + tail, src + tail, (nbytes - tail) / sizeof(T), threadIdx.x, kBlock);
-    }
-    v4u* d = reinterpret_cast<v4u*>(dst + head);
-    const v4u* s = reinterpret_cast<const v4u*>(src + head);
-    const uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
-    const uint64_t lo = (uint64_t)blockIdx.x * per;
-    const uint64_t hi = lo + per < nvec ? lo + per : nvec;
-    uint64_t i = lo + threadIdx.x;
-    for (; i + (U - 1) * kBlock < hi; i += U * kBlock) {
-        v4u a[U], b[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) a[u] = ld16_nt(d + i + u * kBlock);
-#pragma unroll
-        for (int u = 0; u < U; ++u) b[u] = ld16_nt(s + i + u * kBlock);
-#pragma unroll
-        for (int u = 0; u < U; ++u) st16_nt(d + i + u * kBlock, reduce16<OP, T>(a[u], b[u]));
-    }
-    for (; i < hi; i += kBlock) st16_nt(d + i, reduce16<OP, T>(ld16_nt(d + i), ld16_nt(s + i)));
-}
-
-// dst and src NOT congruent mod 16: element-wise grid-stride.
-template <int OP, typename T>
-__global__ __launch_bounds__(kBlock) void k_reduce_unaligned(char* dst, const char* src, uint64_t nelem) {
-    reduce_elems<OP, T>(dst, src, nelem, (uint64_t)blockIdx.x * kBlock + threadIdx.x,
-                        (uint64_t)gridDim.x * kBlock);
-}
-
-// ======================================================= mesh allreduce ===
-// Fold one tile of chunk r: out = ring-order reduction of the n ranks'
-// tile, written to the local user buffer and to every peer's allgather slot.
-// one element at byte offset e of the tile: ring-order fold of the n ranks'
-// values, stored to the local user buffer and every peer's allgather slot
-template <int OP, typename T>
-__device__ __forceinline__ void mesh_fold_elem(const CollArgs& a, char* own, const char* slot0, uint64_t soff,
-                                               uint64_t e) {
-    const int n = a.n, r = a.rank;
-    int q = (r - 1 + n) % n;
-    T acc = *reinterpret_cast<const T*>((q == r ? (const char*)own : slot0 + q * a.slot_bytes) + e);
-    for (int k = 2; k <= n; ++k) {
-        q = (r - k + n) % n;
-        const T v = *reinterpret_cast<const T*>((q == r ? (const char*)own : slot0 + q * a.slot_bytes) + e);
-        acc = OpF<OP>::apply(v, acc);
-    }
-    *reinterpret_cast<T*>(own + e) = acc;
-    for (int p = 0; p < n; ++p)
-        if (p != r) *reinterpret_cast<T*>(a.ag[p] + soff + e) = acc;
-}
-
-// Fold one tile of chunk r: out = ring-order reduction of the n ranks'
-// tile, written to the local user buffer and to every peer's allgather slot.
-template <int OP, typename T, int NMAX>
-__device__ void mesh_reduce_tile(const CollArgs& a, int t, uint64_t tlen) {
-    const int n = a.n, r = a.rank;
-    const uint64_t toff = (uint64_t)t * a.tile_bytes;
-    char* own = a.user + a.off[r] + toff;
-    const char* slot0 = a.rs[r] + a.mis[r] + toff;     // + q*slot_bytes
-    const uint64_t soff = (uint64_t)r * a.slot_bytes + a.mis[r] + toff;  // in peers' ag regions
-    const unsigned tid = threadIdx.x;
-    if ((((uintptr_t)own ^ (uintptr_t)slot0) & 15) != 0) {
-        // this rank's buffer is not 16-B aligned: exact, element by element
-        for (uint64_t e = (uint64_t)tid * sizeof(T); e < tlen; e += (uint64_t)kBlock * sizeof(T))
-            mesh_fold_elem<OP, T>(a, own, slot0, soff, e);
-        return;
-    }
-    const uint64_t mis16 = (uint64_t)(uintptr_t)own & 15;
-    uint64_t head = mis16 ? 16 - mis16 : 0;
-    if (head > tlen) head = tlen;
-    const uint64_t nvec = (tlen - head) >> 4;
-    const uint64_t tail = head + (nvec << 4);
-    {   // element-wise head / tail (< 16 bytes each)
-        const uint64_t nh = head / sizeof(T), nt = (tlen - tail) / sizeof(T);
-        if (tid < nh) mesh_fold_elem<OP, T>(a, own, slot0, soff, tid * sizeof(T));
-        else if (tid >= 64 && tid - 64 < nt) mesh_fold_elem<OP, T>(a, own, slot0, soff, tail + (tid - 64) * sizeof(T));
-    }
-    // All n contributions of U positions are loaded before folding (NMAX x U
-    // 16-B loads in flight per lane); folding one rank at a time inside a
-    // runtime loop would leave the lane latency-bound at n = 8.
-    constexpr int U = NMAX <= 8 ? 2 : 1;
-    const uint64_t stride = kBlock;
-    for (uint64_t i = tid; i < nvec; i += U * stride) {
-        v4u v[U][NMAX];
-        bool live[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) live[u] = i + u * stride < nvec;
-#pragma unroll
-        for (int k = 1; k <= NMAX; ++k) {
-            if (k > n) break;
-            const int q = (r - k + n) % n;  // k-th value in ring order: x[r-1], x[r-2], ..., x[r]
-            const char* src = (q == r ? (const char*)own : slot0 + q * a.slot_bytes) + head;
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (live[u]) v[u][k - 1] = ld16_nt(src + (i + u * stride) * 16);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!live[u]) continue;
-            v4u acc = v[u][0];
-#pragma unroll
-            for (int k = 2; k <= NMAX; ++k)
-                if (k <= n) acc = reduce16<OP, T>(v[u][k - 1], acc);
-            const uint64_t b = head + (i + u * stride) * 16;
-            st16(own + b, acc);
-            for (int p = 0; p < n; ++p)
-                if (p != r) st16_nt(a.ag[p] + soff + b, acc);
-        }
-    }
-}
-
-template <int OP, typename T, int NMAX>
-__device__ void mesh_body(const CollArgs& a) {
-    const int n = a.n, r = a.rank;
-    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
-    int b = blockIdx.x;
-    int tmax = 0;
-    for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
-    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
-
-    if (b < a.nb_scatter) {
-        // ---- scatter: my copy of chunk c's tile t -> owner c's rs slot r
-        const int items = (n - 1) * tmax;
-        for (int it = b; it < items; it += a.nb_scatter) {
-            const int t = it / (n - 1);
-            const int c = (r + 1 + it % (n - 1)) % n;
-            if (t >= a.tiles[c]) continue;
-            const uint64_t toff = (uint64_t)t * a.tile_bytes;
-            uint64_t tlen = a.len[c] - toff;
-            if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-            block_copy(a.rs[c] + (uint64_t)r * a.slot_bytes + a.mis[c] + toff, a.user + a.off[c] + toff, tlen);
-            block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, a.seq);
-        }
-        return;
-    }
-    b -= a.nb_scatter;
-    if (b < a.nb_reduce) {
-        // ---- reduce: chunk r, tile t, once all n-1 contributions landed
-        for (int t = b; t < a.tiles[r]; t += a.nb_reduce) {
-            if (threadIdx.x < (unsigned)(n - 1)) {
-                const int p = (r + 1 + threadIdx.x) % n;
-                s_flags[threadIdx.x] = a.flags[r] + (uint64_t)p * a.max_tiles + t;
-            }
-            __syncthreads();
-            if (!block_wait(s_flags, n - 1, a.seq, ab, RDC_KERR_TIMEOUT_RS)) return;
-            const uint64_t toff = (uint64_t)t * a.tile_bytes;
-            uint64_t tlen = a.len[r] - toff;
-            if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-            mesh_reduce_tile<OP, T, NMAX>(a, t, tlen);
-            if (threadIdx.x < (unsigned)(n - 1)) {
-                const int p = (r + 1 + threadIdx.x) % n;
-                s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
-            }
-            block_publish(s_flags, n - 1, a.seq);
-            __syncthreads();
-        }
-        return;
-    }
-    b -= a.nb_reduce;
-    // ---- gather: owner c's result tile t -> my user buffer
-    const int items = (n - 1) * tmax;
-    for (int it = b; it < items; it += a.nb_gather) {
-        const int t = it / (n - 1);
-        const int c = (r + 1 + it % (n - 1)) % n;
-        if (t >= a.tiles[c]) continue;
-        if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
-        __syncthreads();
-        if (!block_wait(s_flags, 1, a.seq, ab, RDC_KERR_TIMEOUT_AG)) return;
-        const uint64_t toff = (uint64_t)t * a.tile_bytes;
-        uint64_t tlen = a.len[c] - toff;
-        if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-        block_copy(a.user + a.off[c] + toff, a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c] + toff, tlen);
-    }
-}
-
-// ======================================================= ring allreduce ===
-// own[i] = OP(own[i], recv[i]) — reducer(src=reducebuf, dst=sendrecvbuf)
-// (communicator_collective.cc:174-176), element-wise head/tail + 16-B body.
-template <int OP, typename T>
-__device__ void block_reduce_into(char* own, const char* recv, uint64_t len) {
-    if ((((uintptr_t)own ^ (uintptr_t)recv) & 15) != 0) {  // buffer not 16-B aligned: element-wise
-        reduce_elems<OP, T>(own, recv, len / sizeof(T), threadIdx.x, kBlock);
-        return;
-    }
-    const uint64_t mis16 = (uint64_t)(uintptr_t)own & 15;
-    uint64_t head = mis16 ? 16 - mis16 : 0;
-    if (head > len) head = len;
-    const uint64_t nvec = (len - head) >> 4;
-    const uint64_t tail = head + (nvec << 4);
-    const unsigned tid = threadIdx.x;
-    if (tid < head / sizeof(T)) {
-        T* d = reinterpret_cast<T*>(own) + tid;
-        *d = OpF<OP>::apply(*d, reinterpret_cast<const T*>(recv)[tid]);
-    }
-    if (tid < (len - tail) / sizeof(T)) {
-        T* d = reinterpret_cast<T*>(own + tail) + tid;
-        *d = OpF<OP>::apply(*d, reinterpret_cast<const T*>(recv + tail)[tid]);
-    }
-    v4u* d = reinterpret_cast<v4u*>(own + head);
-    const v4u* s = reinterpret_cast<const v4u*>(recv + head);
-    constexpr int U = 4;
-    uint64_t i = tid;
-    for (; i + (U - 1) * kBlock < nvec; i += U * kBlock) {
-        v4u x[U], y[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = ld16(d + i + u * kBlock);
-#pragma unroll
-        for (int u = 0; u < U; ++u) y[u] = ld16_nt(s + i + u * kBlock);
-#pragma unroll
-        for (int u = 0; u < U; ++u) st16(d + i + u * kBlock, reduce16<OP, T>(x[u], y[u]));
-    }
-    for (; i < nvec; i += kBlock) st16(d + i, reduce16<OP, T>(ld16(d + i), ld16_nt(s + i)));
-}
-
-template <int OP, typename T>
-__device__ void ring_body(const CollArgs& a) {
-    const int n = a.n, r = a.rank;
-    const int prev = (r - 1 + n) % n;
-    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
-    __shared__ uint32_t* s_flag[1];
-    int tmax = 0;
-    for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
-    for (int t = blockIdx.x; t < tmax; t += gridDim.x) {
-        const uint64_t toff = (uint64_t)t * a.tile_bytes;
-        // ---- TryReduceScatterRing: step j sends chunk (r+1+j)%n to prev,
-        //      receives chunk (r+2+j)%n from next and reduces it in place.
-        for (int j = 0; j < n - 1; ++j) {
-            const int cs = (r + 1 + j) % n;
-            if (t < a.tiles[cs]) {
-                uint64_t tlen = a.len[cs] - toff;
-                if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_copy(a.rs[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
-                           tlen);
-                block_publish1(a.flags[prev] + (uint64_t)j * a.max_tiles + t, a.seq);
-            }
-            const int cr = (r + 2 + j) % n;
-            if (t < a.tiles[cr]) {
-                if (threadIdx.x == 0) s_flag[0] = a.flags[r] + (uint64_t)j * a.max_tiles + t;
-                __syncthreads();
-                if (!block_wait(s_flag, 1, a.seq, ab, RDC_KERR_TIMEOUT_RING)) return;
-                uint64_t tlen = a.len[cr] - toff;
-                if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_reduce_into<OP, T>(a.user + a.off[cr] + toff,
-                                         a.rs[r] + (uint64_t)j * a.slot_bytes + a.mis[cr] + toff, tlen);
-                __syncthreads();
-            }
-        }
-        // ---- TryAllgatherRing: step j sends chunk (r+j)%n to prev and
-        //      receives chunk (r+1+j)%n from next (in place).
-        for (int j = 0; j < n - 1; ++j) {
-            const int cs = (r + j) % n;
-            if (t < a.tiles[cs]) {
-                uint64_t tlen = a.len[cs] - toff;
-                if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_copy(a.ag[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
-                           tlen);
-                block_publish1(a.flags[prev] + (uint64_t)(n + j) * a.max_tiles + t, a.seq);
-            }
-            const int cr = (r + 1 + j) % n;
-            if (t < a.tiles[cr]) {
-                if (threadIdx.x == 0) s_flag[0] = a.flags[r] + (uint64_t)(n + j) * a.max_tiles + t;
-                __syncthreads();
-                if (!block_wait(s_flag, 1, a.seq, ab, RDC_KERR_TIMEOUT_RING)) return;
-                uint64_t tlen = a.len[cr] - toff;
-                if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_copy(a.user + a.off[cr] + toff, a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr] + toff,
-                           tlen);
-                __syncthreads();
-            }
-        }
-    }
-}
-
-// ============================================================ broadcast ===
-// piece = [off[0], off[0]+len[0]) of the user buffer; tiles[0] tiles.
-__device__ void bcast_body(const CollArgs& a) {
-    const int n = a.n, r = a.rank, root = a.root;
-    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
-    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
-    if (r == root && blockIdx.x < a.tiles[0]) {
-        // A broadcast's receivers never report back, so before overwriting a
-        // peer's allgather region the root waits until that peer finished
-        // its previous launch (done word >= seq-1).  Allreduce launches need
-        // no such gate: their peer writes depend on data the target only
-        // sends once it has entered the same launch.
-        if (threadIdx.x < (unsigned)(n - 1))
-            s_flags[threadIdx.x] = done_word(a, r, (root + 1 + threadIdx.x) % n);
-        __syncthreads();
-        if (!block_wait(s_flags, n - 1, a.seq - 1, ab, RDC_KERR_TIMEOUT_BCAST)) return;
-    }
-    for (int t = blockIdx.x; t < a.tiles[0]; t += gridDim.x) {
-        const uint64_t toff = (uint64_t)t * a.tile_bytes;
-        uint64_t tlen = a.len[0] - toff;
-        if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-        char* mine = a.user + a.off[0] + toff;
-        const uint64_t soff = a.mis[0] + toff;
-        if (r == root) {
-            for (int k = 1; k < n; ++k) block_copy(a.ag[(root + k) % n] + soff, mine, tlen);
-            if (threadIdx.x < (unsigned)(n - 1))
-                s_flags[threadIdx.x] =
-                    a.flags[(root + 1 + threadIdx.x) % n] + (uint64_t)(n + root) * a.max_tiles + t;
-            block_publish(s_flags, n - 1, a.seq);
-            __syncthreads();
-        } else {
-            if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + root) * a.max_tiles + t;
-            __syncthreads();
-            if (!block_wait(s_flags, 1, a.seq, ab, RDC_KERR_TIMEOUT_BCAST)) return;
-            block_copy(mine, a.ag[r] + soff, tlen);
-            __syncthreads();
-        }
-    }
-}
-
-// ======================================================= launch epilogue ===
-// Every block of every collective launch ends here exactly once (also after
-// a timeout).  The last block to arrive resets the local arrival counter and
-// publishes done = seq into every peer's flag array (row 2n, column = this
-// rank): "this rank finished reading its scratch for launch seq".
-__device__ __forceinline__ void launch_done(const CollArgs& a) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        const uint32_t prev = atomicAdd(a.done_ctr, 1u);
-        if (prev == gridDim.x - 1) {
-            __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            for (int p = 0; p < a.n; ++p)
-                if (p != a.rank) flag_store(done_word(a, p, a.rank), a.seq);
-        }
-    }
-}
-
-template <int OP, typename T, int NMAX>
-__global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
-    mesh_body<OP, T, NMAX>(a);
-    launch_done(a);
-}
-
-template <int OP, typename T>
-__global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
-    ring_body<OP, T>(a);
-    launch_done(a);
-}
 
 __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
     bcast_body(a);
@@ -432,91 +42,20 @@ __global__ __launch_bounds__(kBlock) void k_fill(char* buf, uint64_t count, int 
     }
 }
 
-// ============================================================ dispatch ===
-template <int OP, typename T>
-struct Kernels {
-    static hipError_t reduce(char* dst, const char* src, uint64_t nbytes, int grid, hipStream_t s) {
-        if ((((uintptr_t)dst ^ (uintptr_t)src) & 15) == 0) {
-            hipLaunchKernelGGL((k_reduce<OP, T, 4>), dim3(grid), dim3(kBlock), 0, s, dst, src, nbytes);
-        } else {
-            hipLaunchKernelGGL((k_reduce_unaligned<OP, T>), dim3(grid), dim3(kBlock), 0, s, dst, src,
-                               nbytes / sizeof(T));
-        }
-        return hipGetLastError();
-    }
-    static hipError_t mesh(const CollArgs& a, int grid, hipStream_t s) {
-        if (a.n <= 8)
-            hipLaunchKernelGGL((k_mesh<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_mesh<OP, T, 16>), dim3(grid), dim3(kBlock), 0, s, a);
-        return hipGetLastError();
-    }
-    static hipError_t ring(const CollArgs& a, int grid, hipStream_t s) {
-        hipLaunchKernelGGL((k_ring<OP, T>), dim3(grid), dim3(kBlock), 0, s, a);
-        return hipGetLastError();
-    }
-};
-
-template <int OP>
-static bool pick(int dtype, KernelSet* ks) {
-#define RDC_SET(T)                       \
-    ks->reduce = &Kernels<OP, T>::reduce; \
-    ks->mesh = &Kernels<OP, T>::mesh;     \
-    ks->ring = &Kernels<OP, T>::ring;     \
-    return true;
-    switch (dtype) {
-        case RDC_DT_INT8: RDC_SET(int8_t)
-        case RDC_DT_UINT8: RDC_SET(uint8_t)
-        case RDC_DT_INT32: RDC_SET(int32_t)
-        case RDC_DT_UINT32: RDC_SET(uint32_t)
-        case RDC_DT_INT64: case RDC_DT_LONGLONG: RDC_SET(int64_t)
-        case RDC_DT_UINT64: case RDC_DT_ULONGLONG: RDC_SET(uint64_t)
-        default: break;
-    }
-    if (OP != RDC_OP_BITOR) {
-        switch (dtype) {
-            case RDC_DT_FLOAT32: RDC_SET(float)
-            case RDC_DT_FLOAT64: RDC_SET(double)
-            case RDC_DT_FLOAT16: RDC_SET(_Float16)
-            case RDC_DT_BFLOAT16: RDC_SET(bf16_t)
-            default: break;
-        }
-    }
-#undef RDC_SET
-    return false;
-}
-
-// BitOR on floating types is rejected (the reference's op::BitOR does not
-// compile for them, include/core/mpi.h:106-111).
-template <>
-bool pick<RDC_OP_BITOR>(int dtype, KernelSet* ks) {
-#define RDC_SET(T)                                  \
-    ks->reduce = &Kernels<RDC_OP_BITOR, T>::reduce; \
-    ks->mesh = &Kernels<RDC_OP_BITOR, T>::mesh;     \
-    ks->ring = &Kernels<RDC_OP_BITOR, T>::ring;     \
-    return true;
-    switch (dtype) {
-        case RDC_DT_INT8: RDC_SET(int8_t)
-        case RDC_DT_UINT8: RDC_SET(uint8_t)
-        case RDC_DT_INT32: RDC_SET(int32_t)
-        case RDC_DT_UINT32: RDC_SET(uint32_t)
-        case RDC_DT_INT64: case RDC_DT_LONGLONG: RDC_SET(int64_t)
-        case RDC_DT_UINT64: case RDC_DT_ULONGLONG: RDC_SET(uint64_t)
-        default: return false;
-    }
-#undef RDC_SET
-}
+bool pick_max(int dtype, KernelSet* ks);
+bool pick_min(int dtype, KernelSet* ks);
+bool pick_sum(int dtype, KernelSet* ks);
+bool pick_bitor(int dtype, KernelSet* ks);
 
 bool get_kernels(int dtype, int op, KernelSet* ks) {
     switch (op) {
-        case RDC_OP_MAX: return pick<RDC_OP_MAX>(dtype, ks);
-        case RDC_OP_MIN: return pick<RDC_OP_MIN>(dtype, ks);
-        case RDC_OP_SUM: return pick<RDC_OP_SUM>(dtype, ks);
-        case RDC_OP_BITOR: return pick<RDC_OP_BITOR>(dtype, ks);
+        case RDC_OP_MAX: return pick_max(dtype, ks);
+        case RDC_OP_MIN: return pick_min(dtype, ks);
+        case RDC_OP_SUM: return pick_sum(dtype, ks);
+        case RDC_OP_BITOR: return pick_bitor(dtype, ks);
         default: return false;
     }
 }
-
 hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_bcast, dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();

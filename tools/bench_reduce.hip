@@ -144,24 +144,20 @@ int main(int argc, char** argv) {
     CK(hipMemset(s, 0, S));
     std::vector<Variant> vs = {
         {"bc U4 nt/nt B256", (KFn)k_bc<4, true, true, 256>, 256},
-        {"bc U2 nt/nt B256", (KFn)k_bc<2, true, true, 256>, 256},
-        {"bc U4 nt/nt B512", (KFn)k_bc<4, true, true, 512>, 512},
-        {"bc U2 nt/nt B512", (KFn)k_bc<2, true, true, 512>, 512},
         {"bc U4 nt/nt B1024", (KFn)k_bc<4, true, true, 1024>, 1024},
-        {"bc U8 nt/nt B128", (KFn)k_bc<8, true, true, 128>, 128},
-        {"bc U4 ntL/plainS B256", (KFn)k_bc<4, true, false, 256>, 256},
-        {"bcp U2 B256", (KFn)k_bcp<2, 256>, 256},
-        {"bcp U4 B256", (KFn)k_bcp<4, 256>, 256},
-        {"bcp U2 B512", (KFn)k_bcp<2, 512>, 512},
-        {"wc U4 B256", (KFn)k_wc<4, 256>, 256},
-        {"wc U8 B256", (KFn)k_wc<8, 256>, 256},
-        {"wc U4 B512", (KFn)k_wc<4, 512>, 512},
+        {"gs U1 nt/nt B256", (KFn)k_gs<1, true, true, 256>, 256},
         {"gs U2 nt/nt B256", (KFn)k_gs<2, true, true, 256>, 256},
+        {"gs U4 nt/nt B256", (KFn)k_gs<4, true, true, 256>, 256},
+        {"gs U2 nt/nt B512", (KFn)k_gs<2, true, true, 512>, 512},
+        {"gs U2 nt/nt B1024", (KFn)k_gs<2, true, true, 1024>, 1024},
+        {"gs U4 nt/nt B1024", (KFn)k_gs<4, true, true, 1024>, 1024},
+        {"gs U2 plain B256", (KFn)k_gs<2, false, false, 256>, 256},
     };
-    const int grids[] = {256, 512, 1024, 2048, 4096, 8192};
+    const int grids[] = {128, 256, 384, 512, 768, 1024};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    for (int rep = 0; rep < 2; ++rep)
     for (auto& v : vs) {
         for (int g : grids) {
             for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(v.fn, dim3(g), dim3(v.block), 0, 0, d, s, nvec);

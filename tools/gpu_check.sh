@@ -1,5 +1,4 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/t_gpu.log 2>&1; echo "rc=$?"
-grep -E "^E  |passed|failed" gpurun_out/t_gpu.log | head -30
-timeout -k 10 120 python tools/group_perf.py 3 1e6 16e6 64e6 256e6 2>&1 | grep -v amdgpu.ids
+timeout -k 10 300 ./tools/bench_reduce > gpurun_out/sweep3.log 2>&1; echo "sweep rc=$?"
+awk '{for(i=1;i<=NF;i++) if($i=="GB/s") print $(i-1), $0}' gpurun_out/sweep3.log | sort -n -r | head -25
