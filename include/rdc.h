@@ -89,6 +89,10 @@ public:
     virtual void Broadcast(void* sendrecvaddr, uint64_t size, int root) {
         detail::Check(RdcBroadcastOn(handle_, sendrecvaddr, size, root), "Broadcast");
     }
+    /*! \brief bufs[c] holds sizes[c] bytes; bufs[rank] is this rank's data */
+    virtual void Allgather(void** bufs, const size_t* sizes) {
+        detail::Check(RdcAllgatherOn(handle_, bufs, sizes), "Allgather");
+    }
     int GetRank() const { return RdcCommRank(handle_); }
     int GetWorldSize() const { return RdcCommSize(handle_); }
     std::string name() const { return name_; }
@@ -169,6 +173,30 @@ inline void Broadcast(std::string& sendrecv_data, int root, const std::string& c
     Broadcast(&size, sizeof(size), root, comm_name);
     if (sendrecv_data.length() != size) sendrecv_data.resize(size);
     if (size != 0) Broadcast(&sendrecv_data[0], size, root, comm_name);
+}
+
+/*! \brief allgather of per-rank buffers (include/api.h:51-52): sendrecv_data[c]
+ *  holds counts[c] items of type_nbytes bytes; this rank's own entry is the input */
+inline void Allgather(void** sendrecv_data, size_t type_nbytes, size_t* counts,
+                      const std::string& comm_name = kMainCommName) {
+    const int n = GetWorldSize();
+    if (n == 1) return;
+    std::vector<size_t> sizes((size_t)n);
+    for (int i = 0; i < n; ++i) sizes[(size_t)i] = counts[i] * type_nbytes;
+    GetCommunicator(comm_name)->Allgather(sendrecv_data, sizes.data());
+}
+/*! \brief allgather of pre-sized vectors (include/api.h:47-49, rdc-inl.h:112-122) */
+template <typename DType>
+inline void Allgather(std::vector<std::vector<DType>>& sendrecv_data, const std::string& comm_name = kMainCommName) {
+    const int n = GetWorldSize();
+    if (n == 1) return;
+    std::vector<void*> bufs((size_t)n);
+    std::vector<size_t> sizes((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        bufs[(size_t)i] = sendrecv_data[(size_t)i].data();
+        sizes[(size_t)i] = sendrecv_data[(size_t)i].size() * sizeof(DType);
+    }
+    GetCommunicator(comm_name)->Allgather(bufs.data(), sizes.data());
 }
 
 }  // namespace rdc

@@ -75,6 +75,14 @@ int RdcBroadcast(void* sendrecv, unsigned long size, int root);
 int RdcAllreduceOn(void* comm, void* sendrecv, size_t count, int dtype, int op);
 int RdcBroadcastOn(void* comm, void* sendrecv, size_t size, int root);
 
+/* rdc::Allgather (include/api.h:47-52, include/core/rdc-inl.h:106-122;
+ * TryAllgatherRing, communicator_collective.cc:79-114): bufs[c] holds
+ * sizes[c] bytes; on entry bufs[rank] holds this rank's data, on return every
+ * bufs[c] holds rank c's data.  All host or all device memory; synchronous.
+ * RdcAllgather uses the "main" communicator. */
+int RdcAllgather(void** bufs, const size_t* sizes);
+int RdcAllgatherOn(void* comm, void** bufs, const size_t* sizes);
+
 /* rdc::NewCommunicator / GetCommunicator (include/rdc.h:62-71;
  * rdc/comm.py:398-427 calls RdcNewCommunicator(byref(handle), name)).
  * NewCommunicator is collective over all ranks. */
@@ -92,6 +100,8 @@ int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op,
 /* algo: 0 auto, 1 ring (the reference schedule), 2 mesh (all links) */
 int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream);
 int RdcCommBroadcast(void* comm, void* dev_buf, size_t bytes, int root, void* stream);
+/* device-resident allgather of per-rank buffers (see RdcAllgather), stream-ordered */
+int RdcCommAllgather(void* comm, void** dev_bufs, const size_t* sizes, void* stream);
 /* synchronise `stream` and report any device-side collective failure */
 int RdcCommCheck(void* comm, void* stream);
 int RdcCommRank(void* comm);

@@ -45,6 +45,9 @@ def _load():
         "RdcAllreduce": (i, [vp, sz, i, i, vp, vp]),
         "RdcBroadcast": (i, [vp, ctypes.c_ulong, i]),
         "RdcAllreduceOn": (i, [vp, vp, sz, i, i]),
+        "RdcAllgather": (i, [pvp, ctypes.POINTER(ctypes.c_size_t)]),
+        "RdcAllgatherOn": (i, [vp, pvp, ctypes.POINTER(ctypes.c_size_t)]),
+        "RdcCommAllgather": (i, [vp, pvp, ctypes.POINTER(ctypes.c_size_t), vp]),
         "RdcBroadcastOn": (i, [vp, vp, sz, i]),
         "RdcNewCommunicator": (i, [pvp, ctypes.c_char_p]),
         "RdcGetCommunicator": (i, [pvp, ctypes.c_char_p]),

@@ -55,6 +55,20 @@ class Comm(object):
                                          tensor.numel() * tensor.element_size(), root, s))
         return tensor
 
+    def allgather(self, tensors, stream=None):
+        """tensors[c] (contiguous, ROCm) receives rank c's data; tensors[rank] is
+        this rank's input.  Sizes may differ per rank.  In place; returns the list."""
+        n = self.world_size
+        if len(tensors) != n:
+            raise ValueError("rdc_amd: allgather needs one tensor per rank")
+        for t in tensors:
+            _dev._check_tensor(t)
+        ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tensors])
+        sizes = (ctypes.c_size_t * n)(*[t.numel() * t.element_size() for t in tensors])
+        s = stream if stream is not None else _dev.current_stream_ptr(tensors[0].device)
+        check_call(_LIB.RdcCommAllgather(self.handle, ptrs, sizes, s))
+        return tensors
+
     def check(self, stream=None):
         """Synchronise the stream and raise if a device-side wait failed."""
         if stream is None:

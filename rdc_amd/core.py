@@ -149,3 +149,19 @@ def allreduce(data, op, prepare_fun=None):
     check_call(_LIB.RdcAllreduce(buf.ctypes.data_as(ctypes.c_void_p), buf.size, DTYPE_ENUM__[buf.dtype], op,
                                  ctypes.cast(cb, ctypes.c_void_p) if cb is not None else None, None))
     return buf
+
+
+def allgather(arrays):
+    """Allgather of host arrays (rdc::Allgather, include/api.h:47-52): arrays[c]
+    is pre-sized on every rank and arrays[get_rank()] holds this rank's data;
+    on return every arrays[c] holds rank c's data.  In place; returns arrays."""
+    n = get_world_size()
+    if len(arrays) != n:
+        raise ValueError("allgather needs one array per rank")
+    for a in arrays:
+        if not isinstance(a, np.ndarray) or not a.flags.c_contiguous:
+            raise TypeError("allgather takes contiguous numpy arrays")
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrays])
+    sizes = (ctypes.c_size_t * n)(*[a.nbytes for a in arrays])
+    check_call(_LIB.RdcAllgather(ptrs, sizes))
+    return arrays

@@ -15,6 +15,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "../../include/rdc_amd.h"
 #include "rdc_bootstrap.h"
@@ -320,7 +321,70 @@ void broadcast_sync(Manager& m, Communicator* c, void* sendrecv, size_t size, in
     c->Check(s);
 }
 
+void allgather_sync(Manager& m, Communicator* c, void** bufs, const size_t* sizes) {
+    if (!bufs || !sizes) throw std::invalid_argument("rdc: null argument");
+    const int n = c->size();
+    if (n == 1) return;
+    std::vector<uint64_t> sz((size_t)n);
+    for (int i = 0; i < n; ++i) sz[(size_t)i] = sizes[i];
+    hipStream_t s = manager_stream(m, c->device());
+    if (is_device_pointer(bufs[c->rank()]) || sz[(size_t)c->rank()] == 0) {
+        bool dev = true;
+        for (int i = 0; i < n; ++i)
+            if (sz[(size_t)i] && !is_device_pointer(bufs[i])) dev = false;
+        if (dev) {
+            c->Allgather(bufs, sz.data(), s);
+            c->Check(s);
+            return;
+        }
+    }
+    // host buffers: one staging image in HBM (256-B aligned per rank)
+    std::vector<size_t> at((size_t)n);
+    size_t total = 0;
+    for (int i = 0; i < n; ++i) {
+        at[(size_t)i] = total;
+        total += (sz[(size_t)i] + 255) / 256 * 256;
+    }
+    char* d = static_cast<char*>(staging(m, std::max<size_t>(total, 256), c->device()));
+    std::vector<void*> dbufs((size_t)n);
+    for (int i = 0; i < n; ++i) dbufs[(size_t)i] = d + at[(size_t)i];
+    const int r = c->rank();
+    if (sz[(size_t)r])
+        hcheck(hipMemcpyAsync(dbufs[(size_t)r], bufs[r], sz[(size_t)r], hipMemcpyHostToDevice, s), "H2D");
+    c->Allgather(dbufs.data(), sz.data(), s);
+    for (int i = 0; i < n; ++i)
+        if (i != r && sz[(size_t)i])
+            hcheck(hipMemcpyAsync(bufs[i], dbufs[(size_t)i], sz[(size_t)i], hipMemcpyDeviceToHost, s), "D2H");
+    c->Check(s);
+}
+
 }  // namespace
+
+int RdcAllgather(void** bufs, const size_t* sizes) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        require_init(m);
+        if (m.world == 1) return;
+        allgather_sync(m, get_comm(m, "main", true), bufs, sizes);
+    });
+}
+
+int RdcAllgatherOn(void* comm, void** bufs, const size_t* sizes) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] { allgather_sync(m, as_comm(comm), bufs, sizes); });
+}
+
+int RdcCommAllgather(void* comm, void** dev_bufs, const size_t* sizes, void* stream) {
+    return guard([&] {
+        Communicator* c = as_comm(comm);
+        if (!dev_bufs || !sizes) throw std::invalid_argument("rdc: null argument");
+        std::vector<uint64_t> sz((size_t)c->size());
+        for (int i = 0; i < c->size(); ++i) sz[(size_t)i] = sizes[i];
+        c->Allgather(dev_bufs, sz.data(), static_cast<hipStream_t>(stream));
+    });
+}
 
 int RdcAllreduce(void* sendrecv, size_t count, int dtype, int op, void (*prepare_fun)(void*), void* prepare_arg) {
     Manager& m = M();

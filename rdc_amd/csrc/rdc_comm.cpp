@@ -317,6 +317,27 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
     }
 }
 
+void Communicator::Allgather(void* const* bufs, const uint64_t* sizes, hipStream_t stream) {
+    if (n_ == 1) return;
+    for (int c = 0; c < n_; ++c)
+        if (sizes[c] && bufs[c] == nullptr) throw std::invalid_argument("rdc: null allgather buffer");
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    for (const Piece& p : PlanAllgather(n_, sizes, layout(), cfg_.tile_bytes, max_blocks())) {
+        CollArgs a;
+        FillArgsCommon(&a);
+        for (int c = 0; c < n_; ++c) a.cbuf[c] = static_cast<char*>(bufs[c]);
+        memcpy(a.off, p.off, sizeof(a.off));
+        memcpy(a.len, p.len, sizeof(a.len));
+        memcpy(a.mis, p.mis, sizeof(a.mis));
+        memcpy(a.tiles, p.tiles, sizeof(a.tiles));
+        a.tile_bytes = p.tile_bytes;
+        a.nb_scatter = p.nb_scatter;
+        a.nb_gather = p.nb_gather;
+        a.seq = ++seq_;
+        hip_check(launch_allgather(a, p.nb_scatter + p.nb_gather, stream), "launch allgather");
+    }
+}
+
 void Communicator::Check(hipStream_t stream) {
     if (err_ == nullptr) return;  // world size 1: nothing was ever launched
     hip_check(hipSetDevice(device_), "hipSetDevice");
@@ -325,9 +346,10 @@ void Communicator::Check(hipStream_t stream) {
     hip_check(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost), "read error word");
     if (e != RDC_KERR_NONE) {
         static const char* names[] = {"none", "reduce-scatter wait timed out", "allgather wait timed out",
-                                      "broadcast wait timed out", "ring step wait timed out"};
+                                      "broadcast wait timed out", "ring step wait timed out",
+                                      "allgather (buffers) wait timed out"};
         throw std::runtime_error(std::string("rdc: device collective failed on rank ") + std::to_string(rank_) +
-                                 ": " + (e < 5 ? names[e] : "unknown") +
+                                 ": " + (e < 6 ? names[e] : "unknown") +
                                  " (a peer did not join the collective; communicator is now unusable)");
     }
 }

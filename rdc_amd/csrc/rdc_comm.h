@@ -44,6 +44,8 @@ public:
     // in-place device allreduce, stream-ordered; returns hipError_t-style code
     void Allreduce(void* buf, size_t count, int dtype, int op, hipStream_t stream, int algo = RDC_ALGO_AUTO);
     void Broadcast(void* buf, size_t bytes, int root, hipStream_t stream);
+    // bufs[c] (device) holds sizes[c] bytes; bufs[rank] is this rank's data
+    void Allgather(void* const* bufs, const uint64_t* sizes, hipStream_t stream);
     // waits for `stream`, then reads the device error word; throws on error
     void Check(hipStream_t stream);
 

@@ -39,7 +39,8 @@ enum {
     RDC_KERR_TIMEOUT_RS = 1,
     RDC_KERR_TIMEOUT_AG = 2,
     RDC_KERR_TIMEOUT_BCAST = 3,
-    RDC_KERR_TIMEOUT_RING = 4
+    RDC_KERR_TIMEOUT_RING = 4,
+    RDC_KERR_TIMEOUT_ALLGATHER = 5
 };
 
 static inline size_t rdc_dtype_size(int dtype) {
@@ -76,7 +77,8 @@ struct CollArgs {
     char* rs[RDC_MAX_RANKS];             // rank p's reduce-scatter scratch region
     char* ag[RDC_MAX_RANKS];             // rank p's allgather scratch region
     uint32_t* flags[RDC_MAX_RANKS];      // rank p's flag region: [2n][max_tiles] + done[n]
-    int nb_scatter, nb_reduce, nb_gather;  // mesh block roles
+    char* cbuf[RDC_MAX_RANKS];           // allgather: local buffer of rank c's data (off/len index into it)
+    int nb_scatter, nb_reduce, nb_gather;  // mesh block roles (allgather: push / -, gather)
     uint32_t* err;                       // local device error word
     uint32_t* done_ctr;                  // local per-launch block arrival counter (self-resetting)
     uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up

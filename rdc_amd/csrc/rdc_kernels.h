@@ -15,6 +15,7 @@ struct KernelSet {
 // false if (dtype, op) is not a valid reference combination
 bool get_kernels(int dtype, int op, KernelSet* ks);
 hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s);
+hipError_t launch_allgather(const CollArgs& a, int grid, hipStream_t s);
 hipError_t launch_fill(void* buf, uint64_t count, int dtype, uint64_t seed, int rank, hipStream_t s);
 
 }  // namespace rdc_amd

@@ -11,6 +11,61 @@ __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
     launch_done(a);
 }
 
+// ============================================================ allgather ===
+// Allgather of per-rank buffers of any size (rdc::Allgather,
+// include/core/rdc-inl.h:106-122; the reference runs it as TryAllgatherRing,
+// src/comm/communicator_collective.cc:79-114).  A pure copy, so any route
+// gives the reference's bytes: every rank pushes its own buffer's tiles into
+// each peer's AG slot `rank` over all links at once (push blocks) and lands
+// the peers' buffers from its own AG slots (gather blocks).  Like broadcast,
+// receivers never answer, so pushes wait for the targets' done words.
+__device__ void allgather_body(const CollArgs& a) {
+    const int n = a.n, r = a.rank;
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
+    int b = blockIdx.x;
+    if (b < a.nb_scatter) {
+        const int items = (n - 1) * a.tiles[r];
+        if (b < items) {
+            if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = done_word(a, r, (r + 1 + threadIdx.x) % n);
+            __syncthreads();
+            if (!block_wait(s_flags, n - 1, a.seq - 1, ab, RDC_KERR_TIMEOUT_ALLGATHER)) return;
+        }
+        for (int it = b; it < items; it += a.nb_scatter) {
+            const int t = it / (n - 1);
+            const int p = (r + 1 + it % (n - 1)) % n;
+            const uint64_t toff = (uint64_t)t * a.tile_bytes;
+            uint64_t tlen = a.len[r] - toff;
+            if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+            block_copy(a.ag[p] + (uint64_t)r * a.slot_bytes + a.mis[r] + toff, a.cbuf[r] + a.off[r] + toff, tlen);
+            block_publish1(a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t, a.seq);
+        }
+        return;
+    }
+    b -= a.nb_scatter;
+    int tmax = 0;
+    for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
+    const int items = (n - 1) * tmax;
+    for (int it = b; it < items; it += a.nb_gather) {
+        const int t = it / (n - 1);
+        const int c = (r + 1 + it % (n - 1)) % n;
+        if (t >= a.tiles[c]) continue;
+        if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
+        __syncthreads();
+        if (!block_wait(s_flags, 1, a.seq, ab, RDC_KERR_TIMEOUT_ALLGATHER)) return;
+        const uint64_t toff = (uint64_t)t * a.tile_bytes;
+        uint64_t tlen = a.len[c] - toff;
+        if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+        block_copy(a.cbuf[c] + a.off[c] + toff, a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c] + toff, tlen);
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_allgather(CollArgs a) {
+    allgather_body(a);
+    launch_done(a);
+}
+
 // ================================================================= fill ===
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -56,6 +111,11 @@ bool get_kernels(int dtype, int op, KernelSet* ks) {
         default: return false;
     }
 }
+hipError_t launch_allgather(const CollArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_allgather, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_bcast, dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();

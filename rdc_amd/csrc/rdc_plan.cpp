@@ -94,6 +94,44 @@ std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout
     return out;
 }
 
+std::vector<Piece> PlanAllgather(int n, const uint64_t* sizes, const Layout& L, size_t cfg_tile, int max_blocks) {
+    std::vector<Piece> out;
+    if (n <= 1) return out;
+    const uint64_t cap = round_down(L.slot_bytes - RDC_SLOT_ALIGN, RDC_SLOT_ALIGN);
+    uint64_t maxlen = 0;
+    for (int c = 0; c < n; ++c) maxlen = std::max<uint64_t>(maxlen, sizes[c]);
+    const uint64_t npieces = (maxlen + cap - 1) / cap;
+    const int G = std::max(1, max_blocks);
+    for (uint64_t k = 0; k < npieces; ++k) {
+        Piece p;
+        memset(&p, 0, sizeof(p));
+        uint64_t chunk_max = 0;
+        for (int c = 0; c < n; ++c) {
+            const uint64_t b0 = k * cap;
+            if (sizes[c] > b0) {
+                p.off[c] = b0;
+                p.len[c] = std::min<uint64_t>(cap, sizes[c] - b0);
+            }
+            p.mis[c] = (uint32_t)(p.off[c] % 16);
+            chunk_max = std::max<uint64_t>(chunk_max, p.len[c]);
+        }
+        size_t t = cfg_tile ? cfg_tile
+                            : std::min<size_t>(std::max<size_t>(chunk_max / (size_t)std::max(1, G / 2), RDC_MIN_TILE),
+                                               (size_t)1 << 20);
+        t = std::max<size_t>(round_up(t, RDC_SLOT_ALIGN), RDC_MIN_TILE);
+        p.tile_bytes = t;
+        int T = 0;
+        for (int c = 0; c < n; ++c) {
+            p.tiles[c] = (int)((p.len[c] + t - 1) / t);
+            T = std::max(T, p.tiles[c]);
+        }
+        p.nb_scatter = std::max(1, std::min((n - 1) * T, G / 2));
+        p.nb_gather = std::max(1, std::min((n - 1) * T, G - G / 2));
+        out.push_back(p);
+    }
+    return out;
+}
+
 std::vector<Piece> PlanBroadcast(uint64_t bytes, const Layout& L, size_t cfg_tile, int max_blocks) {
     std::vector<Piece> out;
     const size_t cap = round_down(L.region_bytes - RDC_SLOT_ALIGN, RDC_SLOT_ALIGN);

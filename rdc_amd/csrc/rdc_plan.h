@@ -45,6 +45,11 @@ void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blo
 std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout& L, int algo, size_t cfg_tile,
                                  int max_blocks);
 
+// Allgather of n per-rank buffers of sizes[c] bytes: pieces of at most one
+// slot per source rank (off/len/mis/tiles per source c; nb_scatter = push
+// blocks, nb_gather = gather blocks).
+std::vector<Piece> PlanAllgather(int n, const uint64_t* sizes, const Layout& L, size_t cfg_tile, int max_blocks);
+
 // Broadcast pieces of `bytes` (use off/len/mis/tiles [0]).
 std::vector<Piece> PlanBroadcast(uint64_t bytes, const Layout& L, size_t cfg_tile, int max_blocks);
 

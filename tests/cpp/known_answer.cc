@@ -1,5 +1,6 @@
 // Known-answer program over include/rdc.h, following the checks of the
-// reference's test/allreduce.cc:17-55 and test/broadcast.cc: every rank holds
+// reference's test/allreduce.cc:17-55, test/broadcast.cc and test/allgather.cc:
+// every rank holds
 // a[i] = rank + N + i; Allreduce<Max> must give (W-1)+N+i and Allreduce<Sum>
 // sum_j (j+N+i); a broadcast string from rank 0 must arrive intact.
 // Buffers live in host memory (the reference's own setting): the library
@@ -42,6 +43,17 @@ int main(int argc, char* argv[]) {
     if (R == W - 1) v = {1.5, -2.25, 3.0};
     rdc::Broadcast(v, W - 1);
     if (v.size() != 3 || v[1] != -2.25) return fail("broadcast vector", 0, (long)v.size(), 3);
+    // test/allgather.cc: a[i] has i+N items, rank i fills a[i][j] = i + j
+    std::vector<std::vector<int>> g((size_t)W);
+    for (int i = 0; i < W; ++i) {
+        g[(size_t)i].resize((size_t)(i + N));
+        if (i == R)
+            for (int j = 0; j < i + N; ++j) g[(size_t)i][(size_t)j] = i + j;
+    }
+    rdc::Allgather(g);
+    for (int i = 0; i < W; ++i)
+        for (int j = 0; j < i + N; ++j)
+            if (g[(size_t)i][(size_t)j] != i + j) return fail("allgather", j, g[(size_t)i][(size_t)j], i + j);
     printf("rank %d: known-answer OK (world %d, N %d)\n", R, W, N);
     rdc::Finalize();
     return 0;

@@ -46,10 +46,24 @@ def main():
         count, dtype = c["count"], c["dtype"]
         pad = c.get("pad", 0) + rank * c.get("pad_per_rank", 0)
         nbytes = count * esz[dtype]
+        if kind == "allgather":
+            nbytes = 0
         buf = torch.zeros(nbytes + pad + 64, dtype=torch.uint8, device="cuda")
         p = buf.data_ptr() + pad
         check_call(_LIB.RdcFill(ctypes.c_void_p(p), count, dtype, c.get("seed", 0x5EED0000), rank, sp))
         log("rank", rank, "case", i, "filled")
+        if kind == "allgather":
+            # test/allgather.cc shape: buffer i has i + N int32 items, owner fills a[i][j] = i + j
+            N = c["count"]
+            ts = [torch.zeros(i + N, dtype=torch.int32, device="cuda") for i in range(world)]
+            ts[rank].copy_(torch.arange(rank, rank + rank + N, dtype=torch.int32, device="cuda"))
+            torch.cuda.synchronize()
+            comm.allgather(ts, stream=sp)
+            comm.check(sp)
+            out = torch.cat(ts).cpu().numpy().view(np.uint8)
+            np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
+            print("rank %d case %d ok" % (rank, i), flush=True)
+            continue
         if kind == "bcast_chain":
             # stream-ordered chain without host syncs: refill, broadcast from a
             # rotating root, accumulate — exposes a root overwriting a peer's

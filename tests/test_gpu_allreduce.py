@@ -131,6 +131,29 @@ def test_group_broadcast(group3):
                 assert from_dev(bufs[r], 1 + r, nbytes, O.DT_UINT8).tobytes() == data[root].tobytes()
 
 
+def test_group_allgather(group3):
+    """Variable-size per-rank buffers (test/allgather.cc shape, 1 B .. 3 MiB)."""
+    import ctypes
+    from rdc_amd._lib import _LIB
+    rng = np.random.default_rng(4)
+    for sizes in ([1, 2, 3], [1000, 0, 4097], [3 << 20, 5, (1 << 20) + 3], [7 << 20, 7 << 20, 1]):
+        data = [rng.integers(0, 256, s, dtype=np.uint8) for s in sizes]
+        # every rank allocates all n buffers (pads differ per rank and buffer)
+        bufs = [[to_dev(data[c] if c == r else np.zeros(sizes[c], np.uint8), 1 + r + c) for c in range(3)]
+                for r in range(3)]
+        torch.cuda.synchronize()
+        for r in range(3):
+            ptrs = (ctypes.c_void_p * 3)(*[bufs[r][c].data_ptr() + 1 + r + c for c in range(3)])
+            szs = (ctypes.c_size_t * 3)(*sizes)
+            assert _LIB.RdcCommAllgather(group3[r].handle, ptrs, szs,
+                                         ctypes.c_void_p(group3.streams[r].cuda_stream)) == 0, _LIB.RdcGetLastError()
+        for r in range(3):
+            group3[r].check(ctypes.c_void_p(group3.streams[r].cuda_stream))
+            for c in range(3):
+                got = from_dev(bufs[r][c], 1 + r + c, sizes[c], O.DT_UINT8)
+                assert got.tobytes() == data[c].tobytes(), (sizes, r, c)
+
+
 # --------------------------------------------------------------- multi-process
 def run_mp(world, cases, timeout=240, env_extra=None):
     tmp = tempfile.mkdtemp(prefix="rdc_mp_")
@@ -160,6 +183,11 @@ def run_mp(world, cases, timeout=240, env_extra=None):
 
 def expected_for(case, world):
     dt = case["dtype"]
+    if case.get("kind") == "allgather":
+        # test/allgather.cc: buffer i has i + N items, a[i][j] = i + j, gathered everywhere
+        N = case["count"]
+        cat = np.concatenate([np.arange(i, i + i + N, dtype=np.int32) for i in range(world)])
+        return [cat] * world
     if case.get("kind") == "bcast_chain":
         acc = np.zeros(case["count"], dtype=np.int32)
         for k in range(case["steps"]):
@@ -196,6 +224,8 @@ def test_mp_allreduce(world):
         {"count": 100003, "dtype": 6, "op": 2, "algo": 2, "pad_per_rank": 4},   # ranks' buffers differ mod 16
         {"count": 100003, "dtype": 10, "op": 0, "algo": 1, "pad_per_rank": 2},
         {"count": 2, "dtype": 2, "kind": "bcast_chain", "steps": 40},
+        {"count": 1000, "dtype": 2, "kind": "allgather"},
+        {"count": 400001, "dtype": 2, "kind": "allgather"},
         {"count": 300001, "dtype": 2, "kind": "bcast_chain", "steps": 12},
     ]
     tmp = run_mp(world, cases)
