@@ -364,9 +364,18 @@ void DeviceReduce(void* dst, const void* src, size_t count, int dtype, int op, h
         throw std::invalid_argument("rdc: buffer not aligned to its element size");
     if (count == 0) return;
     const uint64_t nbytes = (uint64_t)count * esz;
-    if (grid <= 0) {  // >= 4 KiB per block, at most 4096 blocks (16 per CU)
-        const uint64_t want = (nbytes + 4095) / 4096;
-        grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, 4096));
+    if (grid <= 0) {  // one block per CU (k_reduce's 2 MiB sweep window), fewer for small buffers
+        static int cu_cache[64] = {0};  // per device, filled on first use
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+        int cus = cu_cache[dev];
+        if (cus <= 0) {
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                cus = 256;
+            cu_cache[dev] = cus;
+        }
+        const uint64_t want = (nbytes + 8191) / 8192;  // >= 8 KiB per block
+        grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus));
     }
     hip_check(ks.reduce(static_cast<char*>(dst), static_cast<const char*>(src), nbytes, grid, stream),
               "launch reduce");
