@@ -110,6 +110,8 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # a 1 GiB allreduce takes milliseconds: give up on a missing peer fast
+        os.environ.setdefault("RDC_TIMEOUT", "30")
         dist.init_process_group("gloo")
         rdc_amd.init([])          # RANK/WORLD_SIZE + MASTER_ADDR:MASTER_PORT+1 bootstrap
         comm = rdc_amd.get_comm("main")
@@ -130,7 +132,13 @@ def main():
             check_call(_LIB.RdcReduce(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()), count,
                                       dt_enum, 2, sp))
 
-    for _ in range(args.warmup):
+    # first step checked on its own: a broken peer path fails in seconds
+    # (RDC_TIMEOUT) instead of once per warm-up launch
+    step()
+    torch.cuda.synchronize()
+    if world > 1:
+        comm.check(sp)
+    for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
     if world > 1:

@@ -85,9 +85,10 @@ void Communicator::AllocLocal() {
     scratch_ag_ = static_cast<char*>(alloc_shared(region_bytes_, &k3));
     flags_ = static_cast<uint32_t*>(alloc_shared(flag_bytes_, &k2));
     alloc_kind_ = std::max(std::max(k1, k2), k3);
-    hip_check(hipMalloc(&err_, 64), "hipMalloc err");  // [0] error word, [16] launch arrival counter
+    // [0] error word, [16] block arrival counter, [32] completed-launch counter
+    hip_check(hipMalloc(&err_, 256), "hipMalloc err");
     hip_check(hipMemset(flags_, 0, flag_bytes_), "memset flags");
-    hip_check(hipMemset(err_, 0, 64), "memset err");
+    hip_check(hipMemset(err_, 0, 256), "memset err");
     hip_check(hipDeviceSynchronize(), "sync after alloc");
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_) == hipSuccess && cus > 0)
@@ -249,6 +250,7 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     }
     a->err = err_;
     a->done_ctr = err_ + 16;
+    a->launch_ctr = err_ + 32;
     a->timeout_ticks = (uint64_t)(cfg_.timeout_s * (double)wall_khz_ * 1000.0);
 }
 
@@ -285,7 +287,7 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
         memcpy(a.mis, p.mis, sizeof(a.mis));
         memcpy(a.tiles, p.tiles, sizeof(a.tiles));
         a.tile_bytes = p.tile_bytes;
-        a.seq = ++seq_;
+        ++seq_;
         if (algo == RDC_ALGO_RING) {
             hip_check(ks.ring(a, p.nb_scatter, stream), "launch ring allreduce");
         } else {
@@ -312,7 +314,7 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
         a.mis[0] = p.mis[0];
         a.tiles[0] = p.tiles[0];
         a.tile_bytes = p.tile_bytes;
-        a.seq = ++seq_;
+        ++seq_;
         hip_check(launch_bcast(a, p.nb_scatter, stream), "launch broadcast");
     }
 }
@@ -333,7 +335,7 @@ void Communicator::Allgather(void* const* bufs, const uint64_t* sizes, hipStream
         a.tile_bytes = p.tile_bytes;
         a.nb_scatter = p.nb_scatter;
         a.nb_gather = p.nb_gather;
-        a.seq = ++seq_;
+        ++seq_;
         hip_check(launch_allgather(a, p.nb_scatter + p.nb_gather, stream), "launch allgather");
     }
 }

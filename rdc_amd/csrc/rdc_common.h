@@ -65,7 +65,6 @@ struct CollArgs {
     char* user;                          // local in-place buffer (byte 0 of the whole buffer)
     int n;                               // ranks
     int rank;
-    uint32_t seq;                        // launch sequence number, same on every rank
     int root;                            // broadcast root
     uint64_t tile_bytes;                 // multiple of RDC_SLOT_ALIGN
     int tiles[RDC_MAX_RANKS];            // tiles in chunk c for this launch
@@ -81,5 +80,6 @@ struct CollArgs {
     int nb_scatter, nb_reduce, nb_gather;  // mesh block roles (allgather: push / -, gather)
     uint32_t* err;                       // local device error word
     uint32_t* done_ctr;                  // local per-launch block arrival counter (self-resetting)
+    uint32_t* launch_ctr;                // local count of completed launches (device-side seq)
     uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up
 };

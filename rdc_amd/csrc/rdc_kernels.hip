@@ -7,8 +7,9 @@
 namespace rdc_amd {
 
 __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
-    bcast_body(a);
-    launch_done(a);
+    const uint32_t seq = launch_seq(a);
+    bcast_body(a, seq);
+    launch_done(a, seq);
 }
 
 // ============================================================ allgather ===
@@ -19,7 +20,7 @@ __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
 // each peer's AG slot `rank` over all links at once (push blocks) and lands
 // the peers' buffers from its own AG slots (gather blocks).  Like broadcast,
 // receivers never answer, so pushes wait for the targets' done words.
-__device__ void allgather_body(const CollArgs& a) {
+__device__ void allgather_body(const CollArgs& a, uint32_t seq) {
     const int n = a.n, r = a.rank;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
@@ -29,7 +30,7 @@ __device__ void allgather_body(const CollArgs& a) {
         if (b < items) {
             if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = done_word(a, r, (r + 1 + threadIdx.x) % n);
             __syncthreads();
-            if (!block_wait(s_flags, n - 1, a.seq - 1, ab, RDC_KERR_TIMEOUT_ALLGATHER)) return;
+            if (!block_wait(s_flags, n - 1, seq - 1, ab, RDC_KERR_TIMEOUT_ALLGATHER)) return;
         }
         for (int it = b; it < items; it += a.nb_scatter) {
             const int t = it / (n - 1);
@@ -38,7 +39,7 @@ __device__ void allgather_body(const CollArgs& a) {
             uint64_t tlen = a.len[r] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
             block_copy(a.ag[p] + (uint64_t)r * a.slot_bytes + a.mis[r] + toff, a.cbuf[r] + a.off[r] + toff, tlen);
-            block_publish1(a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t, a.seq);
+            block_publish1(a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t, seq);
         }
         return;
     }
@@ -52,7 +53,7 @@ __device__ void allgather_body(const CollArgs& a) {
         if (t >= a.tiles[c]) continue;
         if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
         __syncthreads();
-        if (!block_wait(s_flags, 1, a.seq, ab, RDC_KERR_TIMEOUT_ALLGATHER)) return;
+        if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_ALLGATHER)) return;
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[c] - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
@@ -62,8 +63,9 @@ __device__ void allgather_body(const CollArgs& a) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_allgather(CollArgs a) {
-    allgather_body(a);
-    launch_done(a);
+    const uint32_t seq = launch_seq(a);
+    allgather_body(a, seq);
+    launch_done(a, seq);
 }
 
 // ================================================================= fill ===

@@ -165,7 +165,7 @@ __device__ void mesh_reduce_tile(const CollArgs& a, int t, uint64_t tlen) {
 }
 
 template <int OP, typename T, int NMAX>
-__device__ void mesh_body(const CollArgs& a) {
+__device__ void mesh_body(const CollArgs& a, uint32_t seq) {
     const int n = a.n, r = a.rank;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     int b = blockIdx.x;
@@ -184,7 +184,7 @@ __device__ void mesh_body(const CollArgs& a) {
             uint64_t tlen = a.len[c] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
             block_copy(a.rs[c] + (uint64_t)r * a.slot_bytes + a.mis[c] + toff, a.user + a.off[c] + toff, tlen);
-            block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, a.seq);
+            block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, seq);
         }
         return;
     }
@@ -197,7 +197,7 @@ __device__ void mesh_body(const CollArgs& a) {
                 s_flags[threadIdx.x] = a.flags[r] + (uint64_t)p * a.max_tiles + t;
             }
             __syncthreads();
-            if (!block_wait(s_flags, n - 1, a.seq, ab, RDC_KERR_TIMEOUT_RS)) return;
+            if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS)) return;
             const uint64_t toff = (uint64_t)t * a.tile_bytes;
             uint64_t tlen = a.len[r] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
@@ -206,7 +206,7 @@ __device__ void mesh_body(const CollArgs& a) {
                 const int p = (r + 1 + threadIdx.x) % n;
                 s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
             }
-            block_publish(s_flags, n - 1, a.seq);
+            block_publish(s_flags, n - 1, seq);
             __syncthreads();
         }
         return;
@@ -220,7 +220,7 @@ __device__ void mesh_body(const CollArgs& a) {
         if (t >= a.tiles[c]) continue;
         if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
         __syncthreads();
-        if (!block_wait(s_flags, 1, a.seq, ab, RDC_KERR_TIMEOUT_AG)) return;
+        if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_AG)) return;
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[c] - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
@@ -268,7 +268,7 @@ __device__ void block_reduce_into(char* own, const char* recv, uint64_t len) {
 }
 
 template <int OP, typename T>
-__device__ void ring_body(const CollArgs& a) {
+__device__ void ring_body(const CollArgs& a, uint32_t seq) {
     const int n = a.n, r = a.rank;
     const int prev = (r - 1 + n) % n;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
@@ -286,13 +286,13 @@ __device__ void ring_body(const CollArgs& a) {
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
                 block_copy(a.rs[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
                            tlen);
-                block_publish1(a.flags[prev] + (uint64_t)j * a.max_tiles + t, a.seq);
+                block_publish1(a.flags[prev] + (uint64_t)j * a.max_tiles + t, seq);
             }
             const int cr = (r + 2 + j) % n;
             if (t < a.tiles[cr]) {
                 if (threadIdx.x == 0) s_flag[0] = a.flags[r] + (uint64_t)j * a.max_tiles + t;
                 __syncthreads();
-                if (!block_wait(s_flag, 1, a.seq, ab, RDC_KERR_TIMEOUT_RING)) return;
+                if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING)) return;
                 uint64_t tlen = a.len[cr] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
                 block_reduce_into<OP, T>(a.user + a.off[cr] + toff,
@@ -309,13 +309,13 @@ __device__ void ring_body(const CollArgs& a) {
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
                 block_copy(a.ag[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
                            tlen);
-                block_publish1(a.flags[prev] + (uint64_t)(n + j) * a.max_tiles + t, a.seq);
+                block_publish1(a.flags[prev] + (uint64_t)(n + j) * a.max_tiles + t, seq);
             }
             const int cr = (r + 1 + j) % n;
             if (t < a.tiles[cr]) {
                 if (threadIdx.x == 0) s_flag[0] = a.flags[r] + (uint64_t)(n + j) * a.max_tiles + t;
                 __syncthreads();
-                if (!block_wait(s_flag, 1, a.seq, ab, RDC_KERR_TIMEOUT_RING)) return;
+                if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING)) return;
                 uint64_t tlen = a.len[cr] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
                 block_copy(a.user + a.off[cr] + toff, a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr] + toff,
@@ -328,7 +328,7 @@ __device__ void ring_body(const CollArgs& a) {
 
 // ============================================================ broadcast ===
 // piece = [off[0], off[0]+len[0]) of the user buffer; tiles[0] tiles.
-__device__ void bcast_body(const CollArgs& a) {
+__device__ void bcast_body(const CollArgs& a, uint32_t seq) {
     const int n = a.n, r = a.rank, root = a.root;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
@@ -341,7 +341,7 @@ __device__ void bcast_body(const CollArgs& a) {
         if (threadIdx.x < (unsigned)(n - 1))
             s_flags[threadIdx.x] = done_word(a, r, (root + 1 + threadIdx.x) % n);
         __syncthreads();
-        if (!block_wait(s_flags, n - 1, a.seq - 1, ab, RDC_KERR_TIMEOUT_BCAST)) return;
+        if (!block_wait(s_flags, n - 1, seq - 1, ab, RDC_KERR_TIMEOUT_BCAST)) return;
     }
     for (int t = blockIdx.x; t < a.tiles[0]; t += gridDim.x) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
@@ -354,12 +354,12 @@ __device__ void bcast_body(const CollArgs& a) {
             if (threadIdx.x < (unsigned)(n - 1))
                 s_flags[threadIdx.x] =
                     a.flags[(root + 1 + threadIdx.x) % n] + (uint64_t)(n + root) * a.max_tiles + t;
-            block_publish(s_flags, n - 1, a.seq);
+            block_publish(s_flags, n - 1, seq);
             __syncthreads();
         } else {
             if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + root) * a.max_tiles + t;
             __syncthreads();
-            if (!block_wait(s_flags, 1, a.seq, ab, RDC_KERR_TIMEOUT_BCAST)) return;
+            if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_BCAST)) return;
             block_copy(mine, a.ag[r] + soff, tlen);
             __syncthreads();
         }
@@ -367,11 +367,20 @@ __device__ void bcast_body(const CollArgs& a) {
 }
 
 // ======================================================= launch epilogue ===
+// Launch sequence numbers live on the device, so a captured hipGraph replays
+// correctly: every block reads the communicator's launch counter when it
+// starts (seq = launches completed + 1, identical on every rank because all
+// ranks issue the same collectives), and the launch's last block advances it.
+__device__ __forceinline__ uint32_t launch_seq(const CollArgs& a) {
+    return __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
 // Every block of every collective launch ends here exactly once (also after
-// a timeout).  The last block to arrive resets the local arrival counter and
+// a timeout).  The last block to arrive resets the local arrival counter,
 // publishes done = seq into every peer's flag array (row 2n, column = this
-// rank): "this rank finished reading its scratch for launch seq".
-__device__ __forceinline__ void launch_done(const CollArgs& a) {
+// rank: "this rank finished reading its scratch for launch seq") and
+// advances the launch counter.
+__device__ __forceinline__ void launch_done(const CollArgs& a, uint32_t seq) {
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence();
@@ -381,21 +390,24 @@ __device__ __forceinline__ void launch_done(const CollArgs& a) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int p = 0; p < a.n; ++p)
-                if (p != a.rank) flag_store(done_word(a, p, a.rank), a.seq);
+                if (p != a.rank) flag_store(done_word(a, p, a.rank), seq);
+            __hip_atomic_store(a.launch_ctr, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
 
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
-    mesh_body<OP, T, NMAX>(a);
-    launch_done(a);
+    const uint32_t seq = launch_seq(a);
+    mesh_body<OP, T, NMAX>(a, seq);
+    launch_done(a, seq);
 }
 
 template <int OP, typename T>
 __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
-    ring_body<OP, T>(a);
-    launch_done(a);
+    const uint32_t seq = launch_seq(a);
+    ring_body<OP, T>(a, seq);
+    launch_done(a, seq);
 }
 
 // ============================================================ dispatch ===

@@ -113,6 +113,43 @@ def test_group_repeated_calls(group3):
             assert same_bits(got[r], want, O.DT_FLOAT32), (it, count, algo)
 
 
+@pytest.mark.parametrize("algo", ["mesh", "ring"])
+def test_group_graph_capture_replay(group2, algo):
+    """Launch sequence numbers live on the device, so a captured allreduce
+    replays correctly (graph per rank, several replays with fresh inputs)."""
+    import ctypes
+    import rdc_amd
+    rng = np.random.default_rng(21)
+    count = 300007
+    ts = [torch.zeros(count, dtype=torch.float32, device="cuda") for _ in range(2)]
+    graphs = []
+    torch.cuda.synchronize()
+    for r in range(2):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=group2.streams[r], capture_error_mode="thread_local"):
+            group2[r].allreduce(ts[r], rdc_amd.Op.SUM, algo=algo,
+                                stream=ctypes.c_void_p(group2.streams[r].cuda_stream))
+        graphs.append(g)
+    torch.cuda.synchronize()
+    for it in range(4):
+        xs = [rng.standard_normal(count).astype(np.float32) for _ in range(2)]
+        for r in range(2):
+            ts[r].copy_(torch.from_numpy(xs[r]))
+        torch.cuda.synchronize()
+        for r in range(2):
+            with torch.cuda.stream(group2.streams[r]):
+                graphs[r].replay()
+        for r in range(2):
+            group2[r].check(ctypes.c_void_p(group2.streams[r].cuda_stream))
+        want = O.expected_allreduce(xs, O.DT_FLOAT32, O.OP_SUM)
+        for r in range(2):
+            assert ts[r].cpu().numpy().tobytes() == want.tobytes(), (algo, it, r)
+    # eager launches interleave with replays on the same communicators
+    xs = [rng.standard_normal(1001).astype(np.float32) for _ in range(2)]
+    got = run_group(group2, xs, O.DT_FLOAT32, O.OP_SUM, 2)
+    assert got[0].tobytes() == O.expected_allreduce(xs, O.DT_FLOAT32, O.OP_SUM).tobytes()
+
+
 def test_group_broadcast(group3):
     import ctypes
     from rdc_amd._lib import _LIB
