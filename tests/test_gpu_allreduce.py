@@ -303,3 +303,27 @@ def test_mp_many_small_buckets_cfg5_shape():
         for r in range(4):
             got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
+
+
+@pytest.mark.parametrize("world", [8, 12])
+def test_mp_many_ranks(world):
+    """n = 8 (the node size; k_mesh NMAX = 8) and n = 12 (NMAX = 16) as processes
+    sharing GPU 0: every schedule, odd counts, a broadcast and an allgather."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [
+        {"count": 1, "dtype": 6, "op": 2},
+        {"count": 7, "dtype": 6, "op": 2, "algo": 1},
+        {"count": 100003, "dtype": 6, "op": 2, "algo": 2},
+        {"count": 100003, "dtype": 6, "op": 2, "algo": 1, "pad_per_rank": 4},
+        {"count": 65537, "dtype": 10, "op": 1},
+        {"count": 3001, "dtype": 4, "op": 2, "reps": 2},
+        {"count": 4099, "dtype": 0, "kind": "broadcast", "root": world // 2},
+        {"count": 333, "dtype": 2, "kind": "allgather"},
+    ]
+    tmp = run_mp(world, cases, timeout=400, env_extra={"RDC_NBLOCKS": "8", "RDC_SCRATCH_BYTES": "16M"})
+    for i, c in enumerate(cases):
+        want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (world, i, c, r)
