@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bytes", type=int, default=1 << 30, help="buffer size per GPU")
     ap.add_argument("--dtype", default="float32", choices=sorted(DTYPES))
-    ap.add_argument("--algo", default="auto", choices=["auto", "mesh", "ring"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "mesh", "ring", "oneshot"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run oracle spot check")
     return ap.parse_args()
@@ -115,7 +115,7 @@ def main():
         dist.init_process_group("gloo")
         rdc_amd.init([])          # RANK/WORLD_SIZE + MASTER_ADDR:MASTER_PORT+1 bootstrap
         comm = rdc_amd.get_comm("main")
-        algo = {"auto": 0, "ring": 1, "mesh": 2}[args.algo]
+        algo = {"auto": 0, "ring": 1, "mesh": 2, "oneshot": 3}[args.algo]
         buf = torch.empty(count, dtype=tdtype, device="cuda")
         rdc_amd.fill_(buf, 0x5EED0000, rank)
 
@@ -194,8 +194,10 @@ def main():
         par = "single GPU"
     else:
         busbw = algbw * 2 * (world - 1) / world
-        algo_name = args.algo if args.algo != "auto" else "mesh"
-        peak = XGMI_LINK_DIR_GBPS * ((world - 1) if algo_name == "mesh" else 1)
+        algo_name = args.algo
+        if algo_name == "auto":  # the library's own choice (rdc_plan.cpp OneshotEligible, 1 MiB push budget)
+            algo_name = "oneshot" if S * (world - 1) <= (1 << 20) else "mesh"
+        peak = XGMI_LINK_DIR_GBPS * (1 if algo_name == "ring" else (world - 1))
         roof = {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 1), "unit": "GB/s",
                 "frac": round(busbw / peak, 4), "traffic": None,
                 "kernel": "k_%s<Sum,%s>" % (algo_name, args.dtype),

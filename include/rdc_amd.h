@@ -40,7 +40,7 @@ extern "C" {
  * key=val override environment variables (communicator_manager.cc:87-104).
  * Keys: RDC_RANK, RDC_WORLD_SIZE|rdc_world_size, RDC_TRACKER_URI,
  * RDC_TRACKER_PORT, rdc_reduce_ring_mincount, RDC_DEVICE, RDC_SCRATCH_BYTES,
- * RDC_ALGO (mesh|ring), RDC_NBLOCKS, RDC_TILE_BYTES, RDC_TIMEOUT.
+ * RDC_ALGO (mesh|ring|oneshot), RDC_NBLOCKS, RDC_TILE_BYTES, RDC_TIMEOUT, RDC_ONESHOT_BYTES.
  * Falls back to torchrun's RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT
  * (tracker port = MASTER_PORT+1).  Does not touch the GPU. */
 int RdcInit(int argc, char** argv);
@@ -97,7 +97,9 @@ int RdcGetCommunicator(void** out, const char* name);
  * (hipStream_t; NULL = default stream).  Asynchronous: errors raised inside
  * the kernels (a peer that never joins) surface at RdcCommCheck. */
 int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op, void* stream);
-/* algo: 0 auto, 1 ring (the reference schedule), 2 mesh (all links) */
+/* algo: 0 auto, 1 ring (the reference schedule), 2 mesh (all links), 3 one-shot (small buffers:
+ * every rank pushes the whole buffer to every peer, one hand-off); auto = one-shot when
+ * (n-1) x bytes <= RDC_ONESHOT_BYTES (default 1 MiB), else mesh.  All bit-identical. */
 int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream);
 int RdcCommBroadcast(void* comm, void* dev_buf, size_t bytes, int root, void* stream);
 /* device-resident allgather of per-rank buffers (see RdcAllgather), stream-ordered */

@@ -10,7 +10,7 @@ include/rdc_amd.h); this package is the Python binding.
 from ._lib import LIB_PATH, RdcError, build  # noqa: F401
 from .core import (DTYPE_ENUM__, Op, allgather, allreduce, barrier, broadcast, finalize, get_processor_name,  # noqa: F401
                    get_rank, get_world_size, init, is_distributed, tracker_print)
-from .comm import ALGO_AUTO, ALGO_MESH, ALGO_RING, Comm, get_comm, init_group, new_comm  # noqa: F401
+from .comm import ALGO_AUTO, ALGO_MESH, ALGO_ONESHOT, ALGO_RING, Comm, get_comm, init_group, new_comm  # noqa: F401
 from .device import dtype_enum, fill_, reduce_  # noqa: F401
 
 __all__ = [

@@ -7,8 +7,8 @@ import ctypes
 from ._lib import _LIB, check_call
 from . import device as _dev
 
-ALGO_AUTO, ALGO_RING, ALGO_MESH = 0, 1, 2
-_ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "mesh": ALGO_MESH}
+ALGO_AUTO, ALGO_RING, ALGO_MESH, ALGO_ONESHOT = 0, 1, 2, 3
+_ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "mesh": ALGO_MESH, "oneshot": ALGO_ONESHOT}
 
 
 class Comm(object):

@@ -78,10 +78,12 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_SCRATCH_BYTES" || k == "rdc_reduce_buffer") m.cfg.scratch_bytes = parse_unit(val);
     else if (k == "RDC_ALGO") {
         std::string v(val);
-        m.cfg.algo = v == "ring" ? RDC_ALGO_RING : v == "mesh" ? RDC_ALGO_MESH : RDC_ALGO_AUTO;
+        m.cfg.algo = v == "ring" ? RDC_ALGO_RING : v == "mesh" ? RDC_ALGO_MESH : v == "oneshot" ? RDC_ALGO_ONESHOT
+                                                                                                : RDC_ALGO_AUTO;
     } else if (k == "RDC_NBLOCKS") m.cfg.max_blocks = atoi(val);
     else if (k == "RDC_TILE_BYTES") m.cfg.tile_bytes = parse_unit(val);
     else if (k == "RDC_TIMEOUT") m.cfg.timeout_s = atof(val);
+    else if (k == "RDC_ONESHOT_BYTES") m.cfg.oneshot_push_max = parse_unit(val);
     else if (k == "RDC_BOOTSTRAP_TIMEOUT") m.bootstrap_timeout_s = atof(val);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
     // to subsystems outside the device path and are accepted silently
@@ -189,7 +191,7 @@ int RdcInit(int argc, char** argv) {
         static const char* keys[] = {"RDC_TRACKER_URI", "RDC_TRACKER_PORT", "RDC_WORLD_SIZE", "rdc_world_size",
                                      "RDC_RANK", "rdc_reduce_ring_mincount", "RDC_DEVICE", "RDC_SCRATCH_BYTES",
                                      "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
-                                     "RDC_BOOTSTRAP_TIMEOUT"};
+                                     "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES"};
         for (const char* k : keys) env_param(m, k);
         for (int i = 0; i < argc; ++i) {
             if (!argv || !argv[i]) continue;
@@ -428,7 +430,7 @@ int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op,
 
 int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream) {
     return guard([&] {
-        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_MESH) throw std::invalid_argument("rdc: bad algo");
+        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_ONESHOT) throw std::invalid_argument("rdc: bad algo");
         as_comm(comm)->Allreduce(dev_buf, count, dtype, op, static_cast<hipStream_t>(stream), algo);
     });
 }
@@ -453,7 +455,7 @@ int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes
         if (!comms || !devices) throw std::invalid_argument("rdc: null argument");
         // parameters from the environment even without RdcInit
         static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
-                                     "RDC_TIMEOUT"};
+                                     "RDC_TIMEOUT", "RDC_ONESHOT_BYTES"};
         if (!m.inited)
             for (const char* k : keys) env_param(m, k);
         CommConfig cfg = m.cfg;

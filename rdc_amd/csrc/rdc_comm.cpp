@@ -237,6 +237,15 @@ int Communicator::PickAlgo(int algo) const {
     return algo;
 }
 
+int Communicator::PickAlgo(int algo, uint64_t bytes) const {
+    if (algo == RDC_ALGO_AUTO) algo = cfg_.algo;
+    if (algo == RDC_ALGO_AUTO)
+        algo = OneshotEligible(n_, bytes, layout(), cfg_.oneshot_push_max) ? RDC_ALGO_ONESHOT : RDC_ALGO_MESH;
+    if (algo == RDC_ALGO_ONESHOT && !OneshotEligible(n_, bytes, layout(), (uint64_t)-1))
+        algo = RDC_ALGO_MESH;  // does not fit half a slot
+    return algo;
+}
+
 void Communicator::FillArgsCommon(CollArgs* a) const {
     memset(a, 0, sizeof(*a));
     a->n = n_;
@@ -251,6 +260,8 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     a->err = err_;
     a->done_ctr = err_ + 16;
     a->launch_ctr = err_ + 32;
+    a->launch_kind = err_ + 48;
+    a->half_bytes = OneshotHalfBytes(layout());
     a->timeout_ticks = (uint64_t)(cfg_.timeout_s * (double)wall_khz_ * 1000.0);
 }
 
@@ -275,8 +286,23 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
     // Communicator::Allreduce returns at world size 1 (communicator_base.h:133-138)
     if (n_ == 1 || count == 0) return;
     if (buf == nullptr) throw std::invalid_argument("rdc: null buffer");
-    algo = PickAlgo(algo);
+    algo = PickAlgo(algo, (uint64_t)count * esz);
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    if (algo == RDC_ALGO_ONESHOT) {
+        const Piece p = PlanOneshot(n_, count, esz, layout(), cfg_.tile_bytes, max_blocks());
+        CollArgs a;
+        FillArgsCommon(&a);
+        a.kind = RDC_KIND_ONESHOT;
+        a.user = static_cast<char*>(buf);
+        memcpy(a.off, p.off, sizeof(a.off));
+        memcpy(a.len, p.len, sizeof(a.len));
+        memcpy(a.tiles, p.tiles, sizeof(a.tiles));
+        a.tile_bytes = p.tile_bytes;
+        a.total_bytes = (uint64_t)count * esz;
+        ++seq_;
+        hip_check(ks.oneshot(a, p.nb_scatter, stream), "launch one-shot allreduce");
+        return;
+    }
     const std::vector<Piece> plan = PlanAllreduce(n_, count, esz, layout(), algo, cfg_.tile_bytes, max_blocks());
     for (const Piece& p : plan) {
         CollArgs a;
@@ -289,11 +315,13 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
         a.tile_bytes = p.tile_bytes;
         ++seq_;
         if (algo == RDC_ALGO_RING) {
+            a.kind = RDC_KIND_RING;
             hip_check(ks.ring(a, p.nb_scatter, stream), "launch ring allreduce");
         } else {
             a.nb_scatter = p.nb_scatter;
             a.nb_reduce = p.nb_reduce;
             a.nb_gather = p.nb_gather;
+            a.kind = RDC_KIND_MESH;
             hip_check(ks.mesh(a, p.nb_scatter + p.nb_reduce + p.nb_gather, stream), "launch mesh allreduce");
         }
     }
@@ -309,6 +337,7 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
         FillArgsCommon(&a);
         a.user = static_cast<char*>(buf);
         a.root = root;
+        a.kind = RDC_KIND_BCAST;
         a.off[0] = p.off[0];
         a.len[0] = p.len[0];
         a.mis[0] = p.mis[0];
@@ -335,6 +364,7 @@ void Communicator::Allgather(void* const* bufs, const uint64_t* sizes, hipStream
         a.tile_bytes = p.tile_bytes;
         a.nb_scatter = p.nb_scatter;
         a.nb_gather = p.nb_gather;
+        a.kind = RDC_KIND_ALLGATHER;
         ++seq_;
         hip_check(launch_allgather(a, p.nb_scatter + p.nb_gather, stream), "launch allgather");
     }

@@ -29,6 +29,7 @@ struct CommConfig {
     int max_blocks = 0;                      // 0 = auto
     size_t tile_bytes = 0;                   // 0 = auto
     double timeout_s = 60.0;                 // device-side wait limit
+    size_t oneshot_push_max = (size_t)1 << 20;  // auto picks one-shot when (n-1) x bytes <= this
 };
 
 class Communicator {
@@ -65,6 +66,7 @@ private:
     void AllocLocal();
     void FillArgsCommon(CollArgs* a) const;
     int PickAlgo(int algo) const;
+    int PickAlgo(int algo, uint64_t bytes) const;
 
     std::string name_;
     int rank_ = 0, n_ = 1, device_ = 0;

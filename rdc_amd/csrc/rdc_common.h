@@ -26,8 +26,13 @@ enum { RDC_OP_MAX = 0, RDC_OP_MIN = 1, RDC_OP_SUM = 2, RDC_OP_BITOR = 3, RDC_OP_
 enum {
     RDC_ALGO_AUTO = 0,
     RDC_ALGO_RING = 1,  // the reference's ring: n-1 reduce-scatter + n-1 allgather steps
-    RDC_ALGO_MESH = 2   // direct all-links exchange, same per-chunk accumulation order
+    RDC_ALGO_MESH = 2,  // direct all-links exchange, same per-chunk accumulation order
+    RDC_ALGO_ONESHOT = 3  // small buffers: every rank pushes all of it, every rank folds (one hand-off)
 };
+
+// launch kinds (recorded on the device: the next launch reads the previous kind)
+enum { RDC_KIND_NONE = 0, RDC_KIND_MESH = 1, RDC_KIND_RING = 2, RDC_KIND_BCAST = 3, RDC_KIND_ALLGATHER = 4,
+       RDC_KIND_ONESHOT = 5 };
 
 #define RDC_MAX_RANKS 16
 #define RDC_SLOT_ALIGN 256         // scratch images keep the user buffer's address mod 256
@@ -81,5 +86,9 @@ struct CollArgs {
     uint32_t* err;                       // local device error word
     uint32_t* done_ctr;                  // local per-launch block arrival counter (self-resetting)
     uint32_t* launch_ctr;                // local count of completed launches (device-side seq)
+    uint32_t* launch_kind;               // local: kind of the last completed launch
+    int kind;                            // this launch's RDC_KIND_*
+    uint64_t half_bytes;                 // one-shot: offset of the slot half used by odd seq
+    uint64_t total_bytes;                // one-shot: whole buffer bytes
     uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up
 };

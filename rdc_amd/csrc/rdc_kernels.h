@@ -10,6 +10,7 @@ struct KernelSet {
     hipError_t (*reduce)(char* dst, const char* src, uint64_t nbytes, int grid, hipStream_t s);
     hipError_t (*mesh)(const CollArgs& a, int grid, hipStream_t s);
     hipError_t (*ring)(const CollArgs& a, int grid, hipStream_t s);
+    hipError_t (*oneshot)(const CollArgs& a, int grid, hipStream_t s);
 };
 
 // false if (dtype, op) is not a valid reference combination

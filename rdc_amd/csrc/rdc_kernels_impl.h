@@ -33,6 +33,30 @@ __device__ __forceinline__ uint32_t* done_word(const CollArgs& a, int owner, int
     return a.flags[owner] + (uint64_t)(2 * a.n) * a.max_tiles + writer;
 }
 
+// ====================================================== launch sequencing ===
+// Launch sequence numbers live on the device, so a captured hipGraph replays
+// correctly: every block reads the communicator's launch counter when it
+// starts (seq = launches completed + 1, identical on every rank because all
+// ranks issue the same collectives), and the launch's last block advances it.
+__device__ __forceinline__ uint32_t launch_seq(const CollArgs& a) {
+    return __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+__device__ __forceinline__ uint32_t prev_kind(const CollArgs& a) {
+    return __hip_atomic_load(a.launch_kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Block-wide: wait until each listed peer finished launch seq-1 (its done word
+// in MY flag array).  Used before writing into peers' scratch when no data
+// dependency already orders the write.
+__device__ __forceinline__ bool gate_on_peers(const CollArgs& a, uint32_t seq, int first, int count,
+                                              const Abort& ab, uint32_t code) {
+    __shared__ uint32_t* s_gate[RDC_MAX_RANKS];
+    if (threadIdx.x < (unsigned)count) s_gate[threadIdx.x] = done_word(a, a.rank, (first + threadIdx.x) % a.n);
+    __syncthreads();
+    return block_wait(s_gate, count, seq - 1, ab, code);
+}
+
+
 // =============================================================== reduce ===
 template <int OP, typename T>
 __device__ __forceinline__ void reduce_elems(char* dst, const char* src, uint64_t nelem, uint64_t first,
@@ -176,6 +200,11 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
     if (b < a.nb_scatter) {
         // ---- scatter: my copy of chunk c's tile t -> owner c's rs slot r
         const int items = (n - 1) * tmax;
+        // after a one-shot launch the owners may still be reading their RS
+        // slots (nothing in this launch orders that): wait for their done words
+        if (b < items && prev_kind(a) == RDC_KIND_ONESHOT &&
+            !gate_on_peers(a, seq, r + 1, n - 1, ab, RDC_KERR_TIMEOUT_RS))
+            return;
         for (int it = b; it < items; it += a.nb_scatter) {
             const int t = it / (n - 1);
             const int c = (r + 1 + it % (n - 1)) % n;
@@ -272,6 +301,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
     const int n = a.n, r = a.rank;
     const int prev = (r - 1 + n) % n;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    if (prev_kind(a) == RDC_KIND_ONESHOT && !gate_on_peers(a, seq, prev, 1, ab, RDC_KERR_TIMEOUT_RING)) return;
     __shared__ uint32_t* s_flag[1];
     int tmax = 0;
     for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
@@ -326,6 +356,106 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
     }
 }
 
+// =================================================== one-shot allreduce ===
+// Small buffers: every rank pushes its WHOLE buffer into every peer's RS slot
+// `rank` (one hand-off instead of the mesh's two), then folds all n
+// contributions itself.  Element i of chunk c (utils::Split) is folded in the
+// ring's order for c — s = x[c-1]; s = OP(x[c-2], s) ... s = OP(x[c], s) —
+// so every rank computes the reference's bits without a second exchange.
+// Consecutive one-shot launches alternate between the two halves of each
+// slot (seq parity): a peer can be at most one launch ahead, so it never
+// overwrites the half a slower rank is still folding.
+
+// fold bytes [lo, hi) of the buffer, all inside chunk c
+template <int OP, typename T, int NMAX>
+__device__ void oneshot_fold_range(const CollArgs& a, int c, const char* slots, uint64_t lo, uint64_t hi) {
+    const int n = a.n, r = a.rank;
+    char* own = a.user;
+    const unsigned tid = threadIdx.x;
+    auto src = [&](int q) -> const char* { return q == r ? (const char*)own : slots + (uint64_t)q * a.slot_bytes; };
+    auto fold_elem = [&](uint64_t x) {
+        T acc = *reinterpret_cast<const T*>(src((c - 1 + n) % n) + x);
+        for (int k = 2; k <= n; ++k) acc = OpF<OP>::apply(*reinterpret_cast<const T*>(src((c - k + n) % n) + x), acc);
+        *reinterpret_cast<T*>(own + x) = acc;
+    };
+    if ((((uintptr_t)own ^ (uintptr_t)slots) & 15) != 0) {  // this rank's buffer is not 16-B aligned
+        for (uint64_t x = lo + (uint64_t)tid * sizeof(T); x < hi; x += (uint64_t)kBlock * sizeof(T)) fold_elem(x);
+        return;
+    }
+    uint64_t vlo = (lo + 15) & ~(uint64_t)15;
+    if (vlo > hi) vlo = hi;
+    const uint64_t vhi = vlo + ((hi - vlo) & ~(uint64_t)15);
+    {
+        const uint64_t nh = (vlo - lo) / sizeof(T), nt = (hi - vhi) / sizeof(T);
+        if (tid < nh) fold_elem(lo + tid * sizeof(T));
+        else if (tid >= 64 && tid - 64 < nt) fold_elem(vhi + (tid - 64) * sizeof(T));
+    }
+    constexpr int U = NMAX <= 8 ? 2 : 1;
+    const uint64_t nvec = (vhi - vlo) >> 4;
+    for (uint64_t i = tid; i < nvec; i += U * kBlock) {
+        v4u v[U][NMAX];
+        bool live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) live[u] = i + u * kBlock < nvec;
+#pragma unroll
+        for (int k = 1; k <= NMAX; ++k) {
+            if (k > n) break;
+            const char* p = src((c - k + n) % n) + vlo;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (live[u]) v[u][k - 1] = ld16_nt(p + (i + u * kBlock) * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!live[u]) continue;
+            v4u acc = v[u][0];
+#pragma unroll
+            for (int k = 2; k <= NMAX; ++k)
+                if (k <= n) acc = reduce16<OP, T>(v[u][k - 1], acc);
+            st16(own + vlo + (i + u * kBlock) * 16, acc);
+        }
+    }
+}
+
+template <int OP, typename T, int NMAX>
+__device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
+    const int n = a.n, r = a.rank;
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
+    const uint64_t half = (seq & 1u) ? a.half_bytes : 0;
+    const uint64_t total = a.total_bytes;
+    const int ntiles = a.tiles[0];
+    // 1) push every tile of my buffer into every peer's slot r (never waits)
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t toff = (uint64_t)t * a.tile_bytes;
+        uint64_t tlen = total - toff;
+        if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+        for (int k = 1; k < n; ++k)
+            block_copy(a.rs[(r + k) % n] + (uint64_t)r * a.slot_bytes + half + toff, a.user + toff, tlen);
+        if (threadIdx.x < (unsigned)(n - 1))
+            s_flags[threadIdx.x] = a.flags[(r + 1 + threadIdx.x) % n] + (uint64_t)r * a.max_tiles + t;
+        block_publish(s_flags, n - 1, seq);
+        __syncthreads();
+    }
+    // 2) fold my tiles once every peer's copy landed
+    const char* slots = a.rs[r] + half;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        if (threadIdx.x < (unsigned)(n - 1))
+            s_flags[threadIdx.x] = a.flags[r] + (uint64_t)((r + 1 + threadIdx.x) % n) * a.max_tiles + t;
+        __syncthreads();
+        if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS)) return;
+        const uint64_t lo = (uint64_t)t * a.tile_bytes;
+        const uint64_t hi = lo + a.tile_bytes < total ? lo + a.tile_bytes : total;
+        for (int c = 0; c < n; ++c) {
+            if (a.len[c] == 0) continue;
+            const uint64_t clo = a.off[c] > lo ? a.off[c] : lo;
+            const uint64_t chi = a.off[c] + a.len[c] < hi ? a.off[c] + a.len[c] : hi;
+            if (clo < chi) oneshot_fold_range<OP, T, NMAX>(a, c, slots, clo, chi);
+        }
+        __syncthreads();
+    }
+}
+
 // ============================================================ broadcast ===
 // piece = [off[0], off[0]+len[0]) of the user buffer; tiles[0] tiles.
 __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
@@ -366,15 +496,6 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
     }
 }
 
-// ======================================================= launch epilogue ===
-// Launch sequence numbers live on the device, so a captured hipGraph replays
-// correctly: every block reads the communicator's launch counter when it
-// starts (seq = launches completed + 1, identical on every rank because all
-// ranks issue the same collectives), and the launch's last block advances it.
-__device__ __forceinline__ uint32_t launch_seq(const CollArgs& a) {
-    return __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-}
-
 // Every block of every collective launch ends here exactly once (also after
 // a timeout).  The last block to arrive resets the local arrival counter,
 // publishes done = seq into every peer's flag array (row 2n, column = this
@@ -391,6 +512,7 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint32_t seq) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int p = 0; p < a.n; ++p)
                 if (p != a.rank) flag_store(done_word(a, p, a.rank), seq);
+            __hip_atomic_store(a.launch_kind, (uint32_t)a.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.launch_ctr, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -400,6 +522,13 @@ template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
     const uint32_t seq = launch_seq(a);
     mesh_body<OP, T, NMAX>(a, seq);
+    launch_done(a, seq);
+}
+
+template <int OP, typename T, int NMAX>
+__global__ __launch_bounds__(kBlock) void k_oneshot(CollArgs a) {
+    const uint32_t seq = launch_seq(a);
+    oneshot_body<OP, T, NMAX>(a, seq);
     launch_done(a, seq);
 }
 
@@ -429,6 +558,13 @@ struct Kernels {
             hipLaunchKernelGGL((k_mesh<OP, T, 16>), dim3(grid), dim3(kBlock), 0, s, a);
         return hipGetLastError();
     }
+    static hipError_t oneshot(const CollArgs& a, int grid, hipStream_t s) {
+        if (a.n <= 8)
+            hipLaunchKernelGGL((k_oneshot<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_oneshot<OP, T, 16>), dim3(grid), dim3(kBlock), 0, s, a);
+        return hipGetLastError();
+    }
     static hipError_t ring(const CollArgs& a, int grid, hipStream_t s) {
         hipLaunchKernelGGL((k_ring<OP, T>), dim3(grid), dim3(kBlock), 0, s, a);
         return hipGetLastError();
@@ -440,6 +576,7 @@ struct Kernels {
     ks->reduce = &Kernels<OP, T>::reduce; \
     ks->mesh = &Kernels<OP, T>::mesh;     \
     ks->ring = &Kernels<OP, T>::ring;     \
+    ks->oneshot = &Kernels<OP, T>::oneshot; \
     return true;
 
 // integer element types (every operator)

@@ -94,6 +94,34 @@ std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout
     return out;
 }
 
+uint64_t OneshotHalfBytes(const Layout& L) { return round_down(L.slot_bytes / 2, RDC_SLOT_ALIGN); }
+
+bool OneshotEligible(int n, uint64_t bytes, const Layout& L, uint64_t push_max) {
+    return n > 1 && bytes > 0 && bytes <= OneshotHalfBytes(L) && bytes * (uint64_t)(n - 1) <= push_max;
+}
+
+Piece PlanOneshot(int n, uint64_t count, size_t esz, const Layout& L, size_t cfg_tile, int max_blocks) {
+    Piece p;
+    memset(&p, 0, sizeof(p));
+    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+    SplitRanges((int64_t)count, n, cb, ce);
+    for (int c = 0; c < n; ++c) {
+        if (ce[c] > cb[c]) {
+            p.off[c] = (uint64_t)cb[c] * esz;
+            p.len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
+        }
+    }
+    const uint64_t total = count * esz;
+    const int G = std::max(1, max_blocks);
+    size_t t = cfg_tile ? cfg_tile : std::max<size_t>(total / (size_t)G, RDC_MIN_TILE);
+    t = std::max<size_t>(round_up(t, RDC_SLOT_ALIGN), RDC_MIN_TILE);
+    (void)L;
+    p.tile_bytes = t;
+    p.tiles[0] = (int)((total + t - 1) / t);
+    p.nb_scatter = std::max(1, std::min(p.tiles[0], G));
+    return p;
+}
+
 std::vector<Piece> PlanAllgather(int n, const uint64_t* sizes, const Layout& L, size_t cfg_tile, int max_blocks) {
     std::vector<Piece> out;
     if (n <= 1) return out;

@@ -45,6 +45,14 @@ void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blo
 std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout& L, int algo, size_t cfg_tile,
                                  int max_blocks);
 
+// One-shot allreduce (whole buffer pushed to every peer): eligible when the
+// buffer fits half a slot and the total pushed bytes (n-1) x S stay within
+// push_max.  off/len = the Split chunk byte ranges; tiles[0] tiles over the
+// whole buffer; nb_scatter = grid.
+bool OneshotEligible(int n, uint64_t bytes, const Layout& L, uint64_t push_max);
+uint64_t OneshotHalfBytes(const Layout& L);
+Piece PlanOneshot(int n, uint64_t count, size_t esz, const Layout& L, size_t cfg_tile, int max_blocks);
+
 // Allgather of n per-rank buffers of sizes[c] bytes: pieces of at most one
 // slot per source rank (off/len/mis/tiles per source c; nb_scatter = push
 // blocks, nb_gather = gather blocks).

@@ -83,6 +83,10 @@ def main():
             if kind == "allreduce":
                 check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(p), count, dtype, c["op"],
                                                    c.get("algo", 0), sp))
+            elif kind == "algo_chain":
+                for algo in c["algos"]:
+                    check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(p), count, dtype, c["op"], algo,
+                                                       sp))
             elif kind == "broadcast":
                 check_call(_LIB.RdcCommBroadcast(comm.handle, ctypes.c_void_p(p), nbytes, c["root"], sp))
             elif kind == "host_allreduce":

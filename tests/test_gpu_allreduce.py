@@ -76,7 +76,7 @@ def run_group(comms, inputs, dtype, op, algo, pads=None):
     return [from_dev(bufs[r], pads[r] * esz, count, dtype) for r in range(n)]
 
 
-@pytest.mark.parametrize("algo", [1, 2])
+@pytest.mark.parametrize("algo", [1, 2, 3])
 @pytest.mark.parametrize("dtype,op", VALID)
 def test_group3_all_types(group3, dtype, op, algo):
     rng = np.random.default_rng(77 + dtype * 8 + op)
@@ -101,11 +101,12 @@ def test_group_multi_piece(group2, algo):
 
 
 def test_group_repeated_calls(group3):
-    """seq-numbered flags: many back-to-back launches on the same communicator."""
+    """seq-numbered flags: many back-to-back launches on the same communicator,
+    schedules interleaved (one-shot parity halves, gates after one-shot)."""
     rng = np.random.default_rng(9)
-    for it in range(20):
+    for it in range(40):
         count = int(rng.integers(1, 70000))
-        algo = 1 + it % 2
+        algo = int(rng.integers(0, 4))
         inputs = [rng.standard_normal(count).astype(np.float32) for _ in range(3)]
         want = O.expected_allreduce(inputs, O.DT_FLOAT32, O.OP_SUM)
         got = run_group(group3, inputs, O.DT_FLOAT32, O.OP_SUM, algo)
@@ -113,7 +114,7 @@ def test_group_repeated_calls(group3):
             assert same_bits(got[r], want, O.DT_FLOAT32), (it, count, algo)
 
 
-@pytest.mark.parametrize("algo", ["mesh", "ring"])
+@pytest.mark.parametrize("algo", ["mesh", "ring", "oneshot"])
 def test_group_graph_capture_replay(group2, algo):
     """Launch sequence numbers live on the device, so a captured allreduce
     replays correctly (graph per rank, several replays with fresh inputs)."""
@@ -261,6 +262,9 @@ def test_mp_allreduce(world):
         {"count": 100003, "dtype": 6, "op": 2, "algo": 2, "pad_per_rank": 4},   # ranks' buffers differ mod 16
         {"count": 100003, "dtype": 10, "op": 0, "algo": 1, "pad_per_rank": 2},
         {"count": 2, "dtype": 2, "kind": "bcast_chain", "steps": 40},
+        {"count": 50001, "dtype": 6, "op": 2, "algo": 3, "pad_per_rank": 4},
+        {"count": 30000, "dtype": 11, "op": 2, "algo": 3, "reps": 5},
+        {"count": 8191, "dtype": 6, "op": 2, "algo": 0, "reps": 7},
         {"count": 1000, "dtype": 2, "kind": "allgather"},
         {"count": 400001, "dtype": 2, "kind": "allgather"},
         {"count": 300001, "dtype": 2, "kind": "bcast_chain", "steps": 12},
@@ -327,3 +331,21 @@ def test_mp_many_ranks(world):
         for r in range(world):
             got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (world, i, c, r)
+
+
+def test_mp_mixed_schedule_chain():
+    """Stream-ordered chains without host syncs mixing every schedule on one
+    communicator: exercises the parity halves and the post-one-shot gates
+    across processes."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [{"count": 20011, "dtype": 6, "op": 2, "kind": "algo_chain", "algos": [3, 3, 2, 3, 1, 3, 3, 2, 2, 1, 3]}]
+    tmp = run_mp(3, cases)
+    c = cases[0]
+    inputs = [O.fill(c["count"], 6, 0x5EED0000, r) for r in range(3)]
+    bufs = [x.copy() for x in inputs]
+    for _ in c["algos"]:
+        O.allreduce_ring(bufs, 6, 2)
+    for r in range(3):
+        got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
+        assert got.tobytes() == np.frombuffer(bufs[r].tobytes(), dtype=np.uint8).tobytes(), r
