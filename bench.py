@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--bytes", type=int, default=1 << 30, help="buffer size per GPU")
     ap.add_argument("--dtype", default="float32", choices=sorted(DTYPES))
     ap.add_argument("--algo", default="auto", choices=["auto", "mesh", "ring", "oneshot"])
+    ap.add_argument("--buckets", type=int, default=1,
+                    help="N>1: split the buffer into this many equal buckets (cfg5: --buckets 1024)")
+    ap.add_argument("--unfused", action="store_true", help="buckets as separate allreduce calls (no coalescing)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run oracle spot check")
     return ap.parse_args()
@@ -116,12 +119,33 @@ def main():
         rdc_amd.init([])          # RANK/WORLD_SIZE + MASTER_ADDR:MASTER_PORT+1 bootstrap
         comm = rdc_amd.get_comm("main")
         algo = {"auto": 0, "ring": 1, "mesh": 2, "oneshot": 3}[args.algo]
-        buf = torch.empty(count, dtype=tdtype, device="cuda")
-        rdc_amd.fill_(buf, 0x5EED0000, rank)
+        K = max(1, args.buckets)
+        if K == 1:
+            buf = torch.empty(count, dtype=tdtype, device="cuda")
+            rdc_amd.fill_(buf, 0x5EED0000, rank)
 
-        def step():
-            check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), count, dt_enum, 2,
-                                               algo, sp))
+            def step():
+                check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), count, dt_enum, 2,
+                                                   algo, sp))
+        else:
+            # cfg5 shape: K separate buckets (own allocations), one coalesced call per step
+            per = count // K
+            count = per * K
+            S = count * esz
+            bks = [torch.empty(per, dtype=tdtype, device="cuda") for _ in range(K)]
+            for b, t in enumerate(bks):
+                rdc_amd.fill_(t, 0x5EED0000 + b, rank)
+            ptrs = (ctypes.c_void_p * K)(*[t.data_ptr() for t in bks])
+            cnts = (ctypes.c_size_t * K)(*([per] * K))
+
+            if args.unfused:
+                def step():
+                    for t in bks:
+                        check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(t.data_ptr()), per, dt_enum,
+                                                           2, algo, sp))
+            else:
+                def step():
+                    check_call(_LIB.RdcCommAllreduceCoalesced(comm.handle, ptrs, cnts, K, dt_enum, 2, algo, sp))
     else:
         dst = torch.empty(count, dtype=tdtype, device="cuda")
         src = torch.empty(count, dtype=tdtype, device="cuda")
@@ -196,7 +220,8 @@ def main():
         busbw = algbw * 2 * (world - 1) / world
         algo_name = args.algo
         if algo_name == "auto":  # the library's own choice (rdc_plan.cpp OneshotEligible, 1 MiB push budget)
-            algo_name = "oneshot" if S * (world - 1) <= (1 << 20) else "mesh"
+            unit = S // args.buckets if args.unfused else min(S, 256 << 20)
+            algo_name = "oneshot" if unit * (world - 1) <= (1 << 20) else "mesh"
         peak = XGMI_LINK_DIR_GBPS * (1 if algo_name == "ring" else (world - 1))
         roof = {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 1), "unit": "GB/s",
                 "frac": round(busbw / peak, 4), "traffic": None,
@@ -205,6 +230,10 @@ def main():
                 "frac_of_bidir_ring_roofline": round(busbw / BIDIR_RING_GBPS, 4)}
         workload = "in-place allreduce(sum) of a %d MiB %s buffer per GPU, %s schedule" % (S >> 20, args.dtype,
                                                                                         algo_name)
+        if args.buckets > 1:
+            workload = "%d x %d KiB %s buckets per GPU (%d MiB), %s, %s schedule" % (
+                args.buckets, (S // args.buckets) >> 10, args.dtype, S >> 20,
+                "separate calls" if args.unfused else "one coalesced call", algo_name)
         par = "dp%d (one process per GPU, xGMI P2P)" % world
     out = {
         "metric": "allreduce GB/s (device-resident fp32) at 1/2/4/8 GPUs; % xGMI roofline",

@@ -85,6 +85,11 @@ public:
     virtual void Allreduce(void* sendrecvbuf, uint64_t count, mpi::DataType dtype, mpi::OpType op) {
         detail::Check(RdcAllreduceOn(handle_, sendrecvbuf, count, (int)dtype, (int)op), "Allreduce");
     }
+    /*! \brief bucketed allreduce: Allreduce of every bufs[b] (counts[b] items), fused launches */
+    virtual void AllreduceCoalesced(void** bufs, const size_t* counts, int nbuf, mpi::DataType dtype,
+                                    mpi::OpType op) {
+        detail::Check(RdcAllreduceCoalescedOn(handle_, bufs, counts, nbuf, (int)dtype, (int)op), "AllreduceCoalesced");
+    }
     /*! \brief broadcast size bytes from root (host or device memory) */
     virtual void Broadcast(void* sendrecvaddr, uint64_t size, int root) {
         detail::Check(RdcBroadcastOn(handle_, sendrecvaddr, size, root), "Broadcast");
@@ -152,6 +157,19 @@ template <typename OP, typename DType>
 inline void Allreduce(DType* sendrecvbuf, uint64_t count, const std::string& comm_name = kMainCommName) {
     if (GetWorldSize() == 1 || count == 0) return;  // communicator_base.h:133-138
     GetCommunicator(comm_name)->Allreduce(sendrecvbuf, count, mpi::GetType<DType>(), OP::kType);
+}
+
+/*! \brief bucketed allreduce (MI355X addition; test/mallreduce.cc's back-to-back shape):
+ *  the result of Allreduce<OP,DType>(bufs[b], counts[b]) for every b, bit-identical,
+ *  moved in fused device launches */
+template <typename OP, typename DType>
+inline void AllreduceCoalesced(DType** bufs, const uint64_t* counts, int nbuf,
+                               const std::string& comm_name = kMainCommName) {
+    if (GetWorldSize() == 1 || nbuf == 0) return;
+    std::vector<size_t> c((size_t)nbuf);
+    for (int b = 0; b < nbuf; ++b) c[(size_t)b] = (size_t)counts[b];
+    GetCommunicator(comm_name)->AllreduceCoalesced(reinterpret_cast<void**>(bufs), c.data(), nbuf,
+                                                   mpi::GetType<DType>(), OP::kType);
 }
 
 /*! \brief broadcast a memory region from root (include/api.h:23-24) */

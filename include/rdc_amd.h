@@ -40,7 +40,8 @@ extern "C" {
  * key=val override environment variables (communicator_manager.cc:87-104).
  * Keys: RDC_RANK, RDC_WORLD_SIZE|rdc_world_size, RDC_TRACKER_URI,
  * RDC_TRACKER_PORT, rdc_reduce_ring_mincount, RDC_DEVICE, RDC_SCRATCH_BYTES,
- * RDC_ALGO (mesh|ring|oneshot), RDC_NBLOCKS, RDC_TILE_BYTES, RDC_TIMEOUT, RDC_ONESHOT_BYTES.
+ * RDC_ALGO (mesh|ring|oneshot), RDC_NBLOCKS, RDC_TILE_BYTES, RDC_TIMEOUT, RDC_ONESHOT_BYTES,
+ * RDC_FUSE_BYTES.
  * Falls back to torchrun's RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT
  * (tracker port = MASTER_PORT+1).  Does not touch the GPU. */
 int RdcInit(int argc, char** argv);
@@ -83,6 +84,15 @@ int RdcBroadcastOn(void* comm, void* sendrecv, size_t size, int root);
 int RdcAllgather(void** bufs, const size_t* sizes);
 int RdcAllgatherOn(void* comm, void** bufs, const size_t* sizes);
 
+/* Coalesced (bucketed) allreduce: the result of one RdcAllreduce per buffer,
+ * in order, bit-identical, but the buffers move in fused launches (groups of
+ * up to RDC_FUSE_BYTES, default 256 MiB, packed chunk-major into one HBM
+ * staging image; BASELINE cfg5 / test/mallreduce.cc's back-to-back shape).
+ * bufs[b] holds counts[b] elements of `dtype`; all host or all device memory;
+ * synchronous.  RdcAllreduceCoalesced uses the "main" communicator. */
+int RdcAllreduceCoalesced(void** bufs, const size_t* counts, int nbuf, int dtype, int op);
+int RdcAllreduceCoalescedOn(void* comm, void** bufs, const size_t* counts, int nbuf, int dtype, int op);
+
 /* rdc::NewCommunicator / GetCommunicator (include/rdc.h:62-71;
  * rdc/comm.py:398-427 calls RdcNewCommunicator(byref(handle), name)).
  * NewCommunicator is collective over all ranks. */
@@ -101,6 +111,12 @@ int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op,
  * every rank pushes the whole buffer to every peer, one hand-off); auto = one-shot when
  * (n-1) x bytes <= RDC_ONESHOT_BYTES (default 1 MiB), else mesh.  All bit-identical. */
 int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream);
+/* device-resident coalesced allreduce (see RdcAllreduceCoalesced), stream-ordered.
+ * The per-group unit table is cached by (buffers, counts): after a first
+ * (warm-up) call with the same buckets, launches need no host->device copy
+ * and can be captured in a hipGraph. */
+int RdcCommAllreduceCoalesced(void* comm, void* const* dev_bufs, const size_t* counts, int nbuf, int dtype, int op,
+                              int algo, void* stream);
 int RdcCommBroadcast(void* comm, void* dev_buf, size_t bytes, int root, void* stream);
 /* device-resident allgather of per-rank buffers (see RdcAllgather), stream-ordered */
 int RdcCommAllgather(void* comm, void** dev_bufs, const size_t* sizes, void* stream);
@@ -137,6 +153,16 @@ int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, voi
 int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4);
 int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int algo, size_t tile_bytes,
                      int max_blocks, uint64_t* out, int max_pieces, int* out_pieces);
+
+/* RdcPlanCoalesced: the staging image of one fusion group.  chunk_out (33
+ * words): packed chunk offsets off[16], lengths len[16], total bytes.  units_out:
+ * 4 words per copy unit {buffer index, byte offset in the buffer, byte offset
+ * in the image, bytes}.  RdcPlanFuseGroups: group boundaries (group g =
+ * buffers [bounds[g], bounds[g+1])); fuse_bytes 0 = default. */
+int RdcPlanCoalesced(int n, const size_t* counts, int nbuf, int dtype, uint64_t* chunk_out, uint64_t* units_out,
+                     int max_units, int* out_units);
+int RdcPlanFuseGroups(const size_t* counts, int nbuf, int dtype, size_t fuse_bytes, int* bounds_out, int max_bounds,
+                      int* out_n);
 
 /* Set a parameter (same keys as RdcInit argv). */
 int RdcSetParam(const char* name, const char* value);

@@ -65,6 +65,13 @@ def _load():
         "RdcFill": (i, [vp, sz, i, u64, i, vp]),
         "RdcPlanLayout": (i, [i, sz, ctypes.POINTER(u64)]),
         "RdcPlanAllreduce": (i, [i, sz, i, sz, i, sz, i, ctypes.POINTER(u64), i, ctypes.POINTER(ctypes.c_int)]),
+        "RdcAllreduceCoalesced": (i, [pvp, ctypes.POINTER(sz), i, i, i]),
+        "RdcAllreduceCoalescedOn": (i, [vp, pvp, ctypes.POINTER(sz), i, i, i]),
+        "RdcCommAllreduceCoalesced": (i, [vp, pvp, ctypes.POINTER(sz), i, i, i, i, vp]),
+        "RdcPlanCoalesced": (i, [i, ctypes.POINTER(sz), i, i, ctypes.POINTER(u64), ctypes.POINTER(u64), i,
+                                 ctypes.POINTER(ctypes.c_int)]),
+        "RdcPlanFuseGroups": (i, [ctypes.POINTER(sz), i, i, sz, ctypes.POINTER(ctypes.c_int), i,
+                                  ctypes.POINTER(ctypes.c_int)]),
         "RdcSetParam": (i, [ctypes.c_char_p, ctypes.c_char_p]),
         "RdcGetLastError": (ctypes.c_char_p, []),
         "RdcVersion": (ctypes.c_char_p, []),

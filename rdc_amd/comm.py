@@ -44,6 +44,24 @@ class Comm(object):
                                            _dev.dtype_enum(tensor.dtype), int(op), _ALGOS[algo], s))
         return tensor
 
+    def allreduce_coalesced(self, tensors, op, algo="auto", stream=None):
+        """Bucketed allreduce of a list of contiguous ROCm tensors of one dtype,
+        in place: the result of ``allreduce`` on each tensor in order
+        (bit-identical), moved in fused launches.  Returns the list."""
+        if not tensors:
+            return tensors
+        for t in tensors:
+            _dev._check_tensor(t)
+            if t.dtype != tensors[0].dtype:
+                raise ValueError("rdc_amd: allreduce_coalesced needs one dtype")
+        nb = len(tensors)
+        ptrs = (ctypes.c_void_p * nb)(*[t.data_ptr() for t in tensors])
+        counts = (ctypes.c_size_t * nb)(*[t.numel() for t in tensors])
+        s = stream if stream is not None else _dev.current_stream_ptr(tensors[0].device)
+        check_call(_LIB.RdcCommAllreduceCoalesced(self.handle, ptrs, counts, nb, _dev.dtype_enum(tensors[0].dtype),
+                                                  int(op), _ALGOS[algo], s))
+        return tensors
+
     def allreduce_ptr(self, ptr, count, dtype, op, algo=ALGO_AUTO, stream=None):
         check_call(_LIB.RdcCommAllreduceEx(self.handle, ctypes.c_void_p(ptr), count, dtype, int(op), algo,
                                            stream))

@@ -151,6 +151,31 @@ def allreduce(data, op, prepare_fun=None):
     return buf
 
 
+def allreduce_coalesced(arrays, op):
+    """Bucketed allreduce of a list of arrays of one dtype, in place: the
+    result of ``allreduce`` on each one (bit-identical), moved in fused device
+    launches (RdcAllreduceCoalesced).  numpy arrays (contiguous) or ROCm
+    tensors (stream-ordered on torch's current stream).  Returns the list."""
+    op = int(Op(op) if not isinstance(op, Op) else op)
+    if not arrays:
+        return arrays
+    if type(arrays[0]).__module__.startswith("torch"):
+        from . import comm as _comm
+        return _comm.get_comm("main").allreduce_coalesced(arrays, op)
+    for a in arrays:
+        if not isinstance(a, np.ndarray) or not a.flags.c_contiguous:
+            raise TypeError("allreduce_coalesced takes contiguous numpy arrays")
+        if a.dtype != arrays[0].dtype:
+            raise TypeError("allreduce_coalesced needs one dtype")
+    if arrays[0].dtype not in DTYPE_ENUM__:
+        raise TypeError("data type %s not supported" % str(arrays[0].dtype))
+    nb = len(arrays)
+    ptrs = (ctypes.c_void_p * nb)(*[a.ctypes.data for a in arrays])
+    counts = (ctypes.c_size_t * nb)(*[a.size for a in arrays])
+    check_call(_LIB.RdcAllreduceCoalesced(ptrs, counts, nb, DTYPE_ENUM__[arrays[0].dtype], op))
+    return arrays
+
+
 def allgather(arrays):
     """Allgather of host arrays (rdc::Allgather, include/api.h:47-52): arrays[c]
     is pre-sized on every rank and arrays[get_rank()] holds this rank's data;

@@ -84,6 +84,7 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_TILE_BYTES") m.cfg.tile_bytes = parse_unit(val);
     else if (k == "RDC_TIMEOUT") m.cfg.timeout_s = atof(val);
     else if (k == "RDC_ONESHOT_BYTES") m.cfg.oneshot_push_max = parse_unit(val);
+    else if (k == "RDC_FUSE_BYTES") m.cfg.fuse_bytes = std::max<size_t>(parse_unit(val), 1);
     else if (k == "RDC_BOOTSTRAP_TIMEOUT") m.bootstrap_timeout_s = atof(val);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
     // to subsystems outside the device path and are accepted silently
@@ -191,7 +192,7 @@ int RdcInit(int argc, char** argv) {
         static const char* keys[] = {"RDC_TRACKER_URI", "RDC_TRACKER_PORT", "RDC_WORLD_SIZE", "rdc_world_size",
                                      "RDC_RANK", "rdc_reduce_ring_mincount", "RDC_DEVICE", "RDC_SCRATCH_BYTES",
                                      "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
-                                     "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES"};
+                                     "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES"};
         for (const char* k : keys) env_param(m, k);
         for (int i = 0; i < argc; ++i) {
             if (!argv || !argv[i]) continue;
@@ -307,6 +308,42 @@ void allreduce_sync(Manager& m, Communicator* c, void* sendrecv, size_t count, i
     c->Check(s);
 }
 
+// synchronous coalesced allreduce of host or device buffers (all of one kind)
+void allreduce_coalesced_sync(Manager& m, Communicator* c, void** bufs, const size_t* counts, int nbuf, int dtype,
+                              int op) {
+    check_dtype_op(dtype, op);
+    if (nbuf < 0 || (nbuf > 0 && (!bufs || !counts))) throw std::invalid_argument("rdc: bad buffer list");
+    if (c->size() == 1 || nbuf == 0) return;
+    hipStream_t s = manager_stream(m, c->device());
+    int ndev = 0, nhost = 0;
+    for (int b = 0; b < nbuf; ++b)
+        if (counts[b]) (is_device_pointer(bufs[b]) ? ndev : nhost)++;
+    if (nhost == 0) {
+        c->AllreduceCoalesced(bufs, counts, nbuf, dtype, op, s);
+        c->Check(s);
+        return;
+    }
+    if (ndev) throw std::invalid_argument("rdc: coalesced allreduce needs all-host or all-device buffers");
+    // host buffers: one HBM image (256-B aligned per buffer), H2D, device path, D2H
+    const size_t esz = rdc_dtype_size(dtype);
+    std::vector<size_t> at((size_t)nbuf);
+    size_t total = 0;
+    for (int b = 0; b < nbuf; ++b) {
+        at[(size_t)b] = total;
+        total += (counts[b] * esz + 255) / 256 * 256;
+    }
+    char* d = static_cast<char*>(staging(m, std::max<size_t>(total, 256), c->device()));
+    std::vector<void*> dbufs((size_t)nbuf);
+    for (int b = 0; b < nbuf; ++b) {
+        dbufs[(size_t)b] = d + at[(size_t)b];
+        if (counts[b]) hcheck(hipMemcpyAsync(dbufs[(size_t)b], bufs[b], counts[b] * esz, hipMemcpyHostToDevice, s), "H2D");
+    }
+    c->AllreduceCoalesced(dbufs.data(), counts, nbuf, dtype, op, s);
+    for (int b = 0; b < nbuf; ++b)
+        if (counts[b]) hcheck(hipMemcpyAsync(bufs[b], dbufs[(size_t)b], counts[b] * esz, hipMemcpyDeviceToHost, s), "D2H");
+    c->Check(s);
+}
+
 void broadcast_sync(Manager& m, Communicator* c, void* sendrecv, size_t size, int root) {
     if (root < 0 || root >= c->size()) throw std::invalid_argument("rdc: broadcast root out of range");
     if (c->size() == 1 || size == 0) return;
@@ -401,6 +438,31 @@ int RdcAllreduce(void* sendrecv, size_t count, int dtype, int op, void (*prepare
     });
 }
 
+int RdcAllreduceCoalesced(void** bufs, const size_t* counts, int nbuf, int dtype, int op) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        require_init(m);
+        check_dtype_op(dtype, op);
+        if (m.world == 1 || nbuf == 0) return;
+        allreduce_coalesced_sync(m, get_comm(m, "main", true), bufs, counts, nbuf, dtype, op);
+    });
+}
+
+int RdcAllreduceCoalescedOn(void* comm, void** bufs, const size_t* counts, int nbuf, int dtype, int op) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] { allreduce_coalesced_sync(m, as_comm(comm), bufs, counts, nbuf, dtype, op); });
+}
+
+int RdcCommAllreduceCoalesced(void* comm, void* const* dev_bufs, const size_t* counts, int nbuf, int dtype, int op,
+                              int algo, void* stream) {
+    return guard([&] {
+        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_ONESHOT) throw std::invalid_argument("rdc: bad algo");
+        as_comm(comm)->AllreduceCoalesced(dev_bufs, counts, nbuf, dtype, op, static_cast<hipStream_t>(stream), algo);
+    });
+}
+
 int RdcBroadcast(void* sendrecv, unsigned long size, int root) {
     Manager& m = M();
     std::lock_guard<std::recursive_mutex> lk(m.mu);
@@ -455,7 +517,7 @@ int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes
         if (!comms || !devices) throw std::invalid_argument("rdc: null argument");
         // parameters from the environment even without RdcInit
         static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
-                                     "RDC_TIMEOUT", "RDC_ONESHOT_BYTES"};
+                                     "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES"};
         if (!m.inited)
             for (const char* k : keys) env_param(m, k);
         CommConfig cfg = m.cfg;
@@ -531,6 +593,45 @@ int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int a
                 o[52 + c] = (uint64_t)p.tiles[c];
             }
         }
+    });
+}
+
+int RdcPlanCoalesced(int n, const size_t* counts, int nbuf, int dtype, uint64_t* chunk_out, uint64_t* units_out,
+                     int max_units, int* out_units) {
+    return guard([&] {
+        const size_t esz = rdc_dtype_size(dtype);
+        if (n < 1 || n > RDC_MAX_RANKS || esz == 0 || nbuf < 0 || (nbuf && !counts) || !out_units)
+            throw std::invalid_argument("rdc: bad argument");
+        std::vector<uint64_t> cnt((size_t)nbuf);
+        for (int b = 0; b < nbuf; ++b) cnt[(size_t)b] = counts[b];
+        const CoalescedPlan P = PlanCoalesced(n, cnt.data(), nbuf, esz);
+        if (chunk_out) {
+            for (int c = 0; c < RDC_MAX_RANKS; ++c) {
+                chunk_out[c] = P.off[c];
+                chunk_out[RDC_MAX_RANKS + c] = P.len[c];
+            }
+            chunk_out[2 * RDC_MAX_RANKS] = P.total;
+        }
+        *out_units = (int)P.units.size();
+        for (int i = 0; i < (int)P.units.size() && i < max_units && units_out; ++i) {
+            units_out[4 * i + 0] = P.units[(size_t)i].buf;
+            units_out[4 * i + 1] = P.units[(size_t)i].buf_off;
+            units_out[4 * i + 2] = P.units[(size_t)i].packed;
+            units_out[4 * i + 3] = P.units[(size_t)i].len;
+        }
+    });
+}
+
+int RdcPlanFuseGroups(const size_t* counts, int nbuf, int dtype, size_t fuse_bytes, int* bounds_out, int max_bounds,
+                      int* out_n) {
+    return guard([&] {
+        const size_t esz = rdc_dtype_size(dtype);
+        if (esz == 0 || nbuf < 0 || (nbuf && !counts) || !out_n) throw std::invalid_argument("rdc: bad argument");
+        std::vector<uint64_t> cnt((size_t)nbuf);
+        for (int b = 0; b < nbuf; ++b) cnt[(size_t)b] = counts[b];
+        const std::vector<int> g = GroupCoalesced(cnt.data(), nbuf, esz, fuse_bytes ? fuse_bytes : CommConfig().fuse_bytes);
+        *out_n = (int)g.size();
+        for (int i = 0; i < (int)g.size() && i < max_bounds && bounds_out; ++i) bounds_out[i] = g[(size_t)i];
     });
 }
 

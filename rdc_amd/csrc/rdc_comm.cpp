@@ -225,6 +225,8 @@ Communicator::~Communicator() {
         } catch (...) {
         }
     }
+    for (auto& kv : pack_cache_) (void)hipFree(kv.second.dtable);
+    if (image_) (void)hipFree(image_);
     if (scratch_) (void)hipFree(scratch_);
     if (scratch_ag_) (void)hipFree(scratch_ag_);
     if (flags_) (void)hipFree(flags_);
@@ -286,28 +288,43 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
     // Communicator::Allreduce returns at world size 1 (communicator_base.h:133-138)
     if (n_ == 1 || count == 0) return;
     if (buf == nullptr) throw std::invalid_argument("rdc: null buffer");
-    algo = PickAlgo(algo, (uint64_t)count * esz);
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+    SplitRanges((int64_t)count, n_, cb, ce);  // utils::Split (include/utils/utils.h:59-70)
+    uint64_t off[RDC_MAX_RANKS] = {0}, len[RDC_MAX_RANKS] = {0};
+    for (int c = 0; c < n_; ++c) {
+        off[c] = (uint64_t)cb[c] * esz;
+        len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
+    }
+    LaunchRanges(ks, static_cast<char*>(buf), off, len, (uint64_t)count * esz, esz, algo, stream);
+}
+
+// The schedule over explicit chunk byte ranges of `buf` (chunk c = [off[c],
+// off[c]+len[c]), folded in the ring order of c).
+void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* off, const uint64_t* len,
+                                uint64_t total, size_t esz, int algo, hipStream_t stream) {
+    algo = PickAlgo(algo, total);
     if (algo == RDC_ALGO_ONESHOT) {
-        const Piece p = PlanOneshot(n_, count, esz, layout(), cfg_.tile_bytes, max_blocks());
+        const Piece p = PlanOneshotRanges(n_, off, len, total, layout(), cfg_.tile_bytes, max_blocks());
         CollArgs a;
         FillArgsCommon(&a);
         a.kind = RDC_KIND_ONESHOT;
-        a.user = static_cast<char*>(buf);
+        a.user = buf;
         memcpy(a.off, p.off, sizeof(a.off));
         memcpy(a.len, p.len, sizeof(a.len));
         memcpy(a.tiles, p.tiles, sizeof(a.tiles));
         a.tile_bytes = p.tile_bytes;
-        a.total_bytes = (uint64_t)count * esz;
+        a.total_bytes = total;
         ++seq_;
         hip_check(ks.oneshot(a, p.nb_scatter, stream), "launch one-shot allreduce");
         return;
     }
-    const std::vector<Piece> plan = PlanAllreduce(n_, count, esz, layout(), algo, cfg_.tile_bytes, max_blocks());
+    const std::vector<Piece> plan =
+        PlanAllreduceRanges(n_, off, len, esz, layout(), algo, cfg_.tile_bytes, max_blocks());
     for (const Piece& p : plan) {
         CollArgs a;
         FillArgsCommon(&a);
-        a.user = static_cast<char*>(buf);
+        a.user = buf;
         memcpy(a.off, p.off, sizeof(a.off));
         memcpy(a.len, p.len, sizeof(a.len));
         memcpy(a.mis, p.mis, sizeof(a.mis));
@@ -324,6 +341,106 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
             a.kind = RDC_KIND_MESH;
             hip_check(ks.mesh(a, p.nb_scatter + p.nb_reduce + p.nb_gather, stream), "launch mesh allreduce");
         }
+    }
+}
+
+// Staging image of the coalesced path, grown on demand (never shrinks).
+char* Communicator::Image(uint64_t bytes) {
+    if (bytes > image_bytes_) {
+        if (image_) {
+            hip_check(hipDeviceSynchronize(), "sync before image regrow");  // launches may still read it
+            (void)hipFree(image_);
+            image_ = nullptr;
+            image_bytes_ = 0;
+        }
+        const uint64_t want = (bytes + ((uint64_t)1 << 20) - 1) & ~(((uint64_t)1 << 20) - 1);
+        hip_check(hipMalloc(&image_, want), "hipMalloc coalesced image");
+        image_bytes_ = want;
+    }
+    return image_;
+}
+
+// Unit table of one fusion group, cached by (dtype size, buffers, counts) so
+// repeated buckets (every training step) launch with no host->device traffic
+// and can be captured in a hipGraph once warm.
+const Communicator::PackEntry& Communicator::PackTable(void* const* bufs, const size_t* counts, int nbuf,
+                                                         size_t esz) {
+    std::vector<uint64_t> key;
+    key.reserve(2 + 2 * (size_t)nbuf);
+    key.push_back(esz);
+    key.push_back((uint64_t)nbuf);
+    for (int b = 0; b < nbuf; ++b) {
+        key.push_back((uint64_t)(uintptr_t)bufs[b]);
+        key.push_back((uint64_t)counts[b]);
+    }
+    auto it = pack_cache_.find(key);
+    if (it != pack_cache_.end()) {
+        it->second.last_use = ++pack_tick_;
+        return it->second;
+    }
+    if (pack_cache_.size() >= kPackCacheMax) {  // evict the least recently used group
+        auto lru = pack_cache_.begin();
+        for (auto j = pack_cache_.begin(); j != pack_cache_.end(); ++j)
+            if (j->second.last_use < lru->second.last_use) lru = j;
+        hip_check(hipDeviceSynchronize(), "sync before pack-table eviction");
+        (void)hipFree(lru->second.dtable);
+        pack_cache_.erase(lru);
+    }
+    std::vector<uint64_t> cnt((size_t)nbuf);
+    for (int b = 0; b < nbuf; ++b) cnt[(size_t)b] = counts[b];
+    CoalescedPlan P = PlanCoalesced(n_, cnt.data(), nbuf, esz);
+    for (PackUnit& u : P.units) {  // buffer index -> user address
+        u.buf = (uint64_t)(uintptr_t)bufs[u.buf] + u.buf_off;
+        u.buf_off = 0;
+    }
+    PackEntry e;
+    memcpy(e.off, P.off, sizeof(e.off));
+    memcpy(e.len, P.len, sizeof(e.len));
+    e.total = P.total;
+    e.nunits = (int)P.units.size();
+    if (e.nunits > 0) {
+        hip_check(hipMalloc(&e.dtable, P.units.size() * sizeof(PackUnit)), "hipMalloc pack table");
+        // fresh memory no launch has seen: a synchronous copy cannot race
+        hip_check(hipMemcpy(e.dtable, P.units.data(), P.units.size() * sizeof(PackUnit), hipMemcpyHostToDevice),
+                  "upload pack table");
+    }
+    e.last_use = ++pack_tick_;
+    return pack_cache_.emplace(std::move(key), e).first->second;
+}
+
+void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, int nbuf, int dtype, int op,
+                                      hipStream_t stream, int algo) {
+    KernelSet ks;
+    if (!get_kernels(dtype, op, &ks))
+        throw std::invalid_argument("rdc: unsupported (dtype, op) = (" + std::to_string(dtype) + ", " +
+                                    std::to_string(op) + ")");
+    if (nbuf < 0 || (nbuf > 0 && (!bufs || !counts))) throw std::invalid_argument("rdc: bad buffer list");
+    const size_t esz = rdc_dtype_size(dtype);
+    for (int b = 0; b < nbuf; ++b) {
+        if (counts[b] && bufs[b] == nullptr) throw std::invalid_argument("rdc: null buffer in coalesced allreduce");
+        if ((uintptr_t)bufs[b] % esz) throw std::invalid_argument("rdc: buffer not aligned to its element size");
+    }
+    if (n_ == 1 || nbuf == 0) return;
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    std::vector<uint64_t> cnt((size_t)nbuf);
+    for (int b = 0; b < nbuf; ++b) cnt[(size_t)b] = counts[b];
+    const std::vector<int> bounds = GroupCoalesced(cnt.data(), nbuf, esz, cfg_.fuse_bytes);
+    for (size_t g = 0; g + 1 < bounds.size(); ++g) {
+        const int b0 = bounds[g], b1 = bounds[g + 1];
+        int live = 0, last = -1;
+        for (int b = b0; b < b1; ++b)
+            if (counts[b]) ++live, last = b;
+        if (live == 0) continue;
+        if (live == 1) {  // nothing to fuse: the buffer's own schedule, no staging
+            Allreduce(bufs[last], counts[last], dtype, op, stream, algo);
+            continue;
+        }
+        const PackEntry& e = PackTable(bufs + b0, counts + b0, b1 - b0, esz);
+        char* img = Image(e.total);
+        const int grid = std::max(1, std::min(e.nunits, 2 * num_cus_));
+        hip_check(launch_pack(e.dtable, e.nunits, img, 0, grid, stream), "launch pack");
+        LaunchRanges(ks, img, e.off, e.len, e.total, esz, algo, stream);
+        hip_check(launch_pack(e.dtable, e.nunits, img, 1, grid, stream), "launch unpack");
     }
 }
 

@@ -13,6 +13,7 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -30,7 +31,10 @@ struct CommConfig {
     size_t tile_bytes = 0;                   // 0 = auto
     double timeout_s = 60.0;                 // device-side wait limit
     size_t oneshot_push_max = (size_t)1 << 20;  // auto picks one-shot when (n-1) x bytes <= this
+    size_t fuse_bytes = (size_t)256 << 20;      // coalesced allreduce: data bytes per fusion group
 };
+
+struct KernelSet;
 
 class Communicator {
 public:
@@ -44,6 +48,10 @@ public:
 
     // in-place device allreduce, stream-ordered; returns hipError_t-style code
     void Allreduce(void* buf, size_t count, int dtype, int op, hipStream_t stream, int algo = RDC_ALGO_AUTO);
+    // bucketed allreduce: the result of Allreduce on every buffer in order
+    // (bit-identical), moved as fused launches over a chunk-major staging image
+    void AllreduceCoalesced(void* const* bufs, const size_t* counts, int nbuf, int dtype, int op,
+                            hipStream_t stream, int algo = RDC_ALGO_AUTO);
     void Broadcast(void* buf, size_t bytes, int root, hipStream_t stream);
     // bufs[c] (device) holds sizes[c] bytes; bufs[rank] is this rank's data
     void Allgather(void* const* bufs, const uint64_t* sizes, hipStream_t stream);
@@ -67,6 +75,18 @@ private:
     void FillArgsCommon(CollArgs* a) const;
     int PickAlgo(int algo) const;
     int PickAlgo(int algo, uint64_t bytes) const;
+    void LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* off, const uint64_t* len, uint64_t total,
+                      size_t esz, int algo, hipStream_t stream);
+    struct PackEntry {
+        PackUnit* dtable = nullptr;  // device unit table (user addresses)
+        int nunits = 0;
+        uint64_t off[RDC_MAX_RANKS] = {}, len[RDC_MAX_RANKS] = {};
+        uint64_t total = 0;
+        uint64_t last_use = 0;
+    };
+    static constexpr size_t kPackCacheMax = 64;
+    const PackEntry& PackTable(void* const* bufs, const size_t* counts, int nbuf, size_t esz);
+    char* Image(uint64_t bytes);
 
     std::string name_;
     int rank_ = 0, n_ = 1, device_ = 0;
@@ -86,6 +106,10 @@ private:
     char* peer_scratch_[RDC_MAX_RANKS] = {};
     char* peer_ag_[RDC_MAX_RANKS] = {};
     uint32_t* peer_flags_[RDC_MAX_RANKS] = {};
+    std::map<std::vector<uint64_t>, PackEntry> pack_cache_;
+    uint64_t pack_tick_ = 0;
+    char* image_ = nullptr;         // coalesced staging image (local HBM)
+    uint64_t image_bytes_ = 0;
 };
 
 // op::Reducer<OP,DType> on device: dst = OP(dst, src) element-wise

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "rdc_common.h"
+#include "rdc_plan.h"
 
 namespace rdc_amd {
 
@@ -17,6 +18,8 @@ struct KernelSet {
 bool get_kernels(int dtype, int op, KernelSet* ks);
 hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s);
 hipError_t launch_allgather(const CollArgs& a, int grid, hipStream_t s);
+// coalesced allreduce: units[i].buf = user address; unpack = image -> buffers
+hipError_t launch_pack(const PackUnit* units, int nunits, char* image, int unpack, int grid, hipStream_t s);
 hipError_t launch_fill(void* buf, uint64_t count, int dtype, uint64_t seed, int rank, hipStream_t s);
 
 }  // namespace rdc_amd

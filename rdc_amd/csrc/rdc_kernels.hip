@@ -68,6 +68,21 @@ __global__ __launch_bounds__(kBlock) void k_allgather(CollArgs a) {
     launch_done(a, seq);
 }
 
+// ============================================================ pack ===
+// Coalesced allreduce (rdc_plan.h PlanCoalesced): copy every unit between its
+// user buffer and the chunk-major staging image.  Unit table in device memory
+// (buf = user address of the unit's first byte); unpack = image -> buffers.
+__global__ __launch_bounds__(kBlock) void k_pack(const PackUnit* __restrict__ units, int nunits,
+                                                 char* __restrict__ image, int unpack) {
+    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+        char* usr = reinterpret_cast<char*>(units[u].buf);
+        char* img = image + units[u].packed;
+        const uint64_t len = units[u].len;
+        if (unpack) block_copy(usr, img, len);
+        else block_copy(img, usr, len);
+    }
+}
+
 // ================================================================= fill ===
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -120,6 +135,12 @@ hipError_t launch_allgather(const CollArgs& a, int grid, hipStream_t s) {
 
 hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_bcast, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(const PackUnit* units, int nunits, char* image, int unpack, int grid, hipStream_t s) {
+    if (nunits <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack, dim3(grid), dim3(kBlock), 0, s, units, nunits, image, unpack);
     return hipGetLastError();
 }
 

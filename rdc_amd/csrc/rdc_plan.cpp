@@ -62,26 +62,25 @@ void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blo
     p->nb_gather = g;
 }
 
-std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout& L, int algo, size_t cfg_tile,
-                                 int max_blocks) {
+std::vector<Piece> PlanAllreduceRanges(int n, const uint64_t* off, const uint64_t* len, size_t esz,
+                                       const Layout& L, int algo, size_t cfg_tile, int max_blocks) {
     std::vector<Piece> out;
-    if (n <= 1 || count == 0 || esz == 0) return out;
-    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
-    SplitRanges((int64_t)count, n, cb, ce);
-    const int64_t maxlen = ce[0] - cb[0];  // the first chunk is never shorter
+    if (n <= 1 || esz == 0) return out;
+    uint64_t maxlen = 0;
+    for (int c = 0; c < n; ++c) maxlen = std::max<uint64_t>(maxlen, len[c]);
+    if (maxlen == 0) return out;
     // a piece occupies at most slot - 256 bytes (+ < 16 bytes of alignment slack)
-    const int64_t pe = (int64_t)(round_down(L.slot_bytes - RDC_SLOT_ALIGN, RDC_SLOT_ALIGN) / esz);
-    const int64_t npieces = (maxlen + pe - 1) / pe;
-    for (int64_t k = 0; k < npieces; ++k) {
+    const uint64_t pe = (uint64_t)(round_down(L.slot_bytes - RDC_SLOT_ALIGN, RDC_SLOT_ALIGN) / esz) * esz;
+    const uint64_t npieces = (maxlen + pe - 1) / pe;
+    for (uint64_t k = 0; k < npieces; ++k) {
         Piece p;
         memset(&p, 0, sizeof(p));
         size_t chunk_max = 0;
         for (int c = 0; c < n; ++c) {
-            const int64_t b0 = cb[c] + k * pe;
-            const int64_t e0 = std::min(ce[c], b0 + pe);
-            if (e0 > b0) {
-                p.off[c] = (uint64_t)b0 * esz;
-                p.len[c] = (uint64_t)(e0 - b0) * esz;
+            const uint64_t b0 = k * pe;
+            if (len[c] > b0) {
+                p.off[c] = off[c] + b0;
+                p.len[c] = std::min<uint64_t>(len[c] - b0, pe);
             }
             // buffer-relative: every rank places chunk c's bytes identically
             p.mis[c] = (uint32_t)(p.off[c] % 16);
@@ -94,6 +93,19 @@ std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout
     return out;
 }
 
+std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout& L, int algo, size_t cfg_tile,
+                                 int max_blocks) {
+    if (n <= 1 || count == 0 || esz == 0) return std::vector<Piece>();
+    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+    SplitRanges((int64_t)count, n, cb, ce);
+    uint64_t off[RDC_MAX_RANKS] = {0}, len[RDC_MAX_RANKS] = {0};
+    for (int c = 0; c < n; ++c) {
+        off[c] = (uint64_t)cb[c] * esz;
+        len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
+    }
+    return PlanAllreduceRanges(n, off, len, esz, L, algo, cfg_tile, max_blocks);
+}
+
 uint64_t OneshotHalfBytes(const Layout& L) { return round_down(L.slot_bytes / 2, RDC_SLOT_ALIGN); }
 
 bool OneshotEligible(int n, uint64_t bytes, const Layout& L, uint64_t push_max) {
@@ -101,17 +113,26 @@ bool OneshotEligible(int n, uint64_t bytes, const Layout& L, uint64_t push_max) 
 }
 
 Piece PlanOneshot(int n, uint64_t count, size_t esz, const Layout& L, size_t cfg_tile, int max_blocks) {
-    Piece p;
-    memset(&p, 0, sizeof(p));
     int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
     SplitRanges((int64_t)count, n, cb, ce);
+    uint64_t off[RDC_MAX_RANKS] = {0}, len[RDC_MAX_RANKS] = {0};
     for (int c = 0; c < n; ++c) {
         if (ce[c] > cb[c]) {
-            p.off[c] = (uint64_t)cb[c] * esz;
-            p.len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
+            off[c] = (uint64_t)cb[c] * esz;
+            len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
         }
     }
-    const uint64_t total = count * esz;
+    return PlanOneshotRanges(n, off, len, count * esz, L, cfg_tile, max_blocks);
+}
+
+Piece PlanOneshotRanges(int n, const uint64_t* off, const uint64_t* len, uint64_t total, const Layout& L,
+                        size_t cfg_tile, int max_blocks) {
+    Piece p;
+    memset(&p, 0, sizeof(p));
+    for (int c = 0; c < n; ++c) {
+        p.off[c] = len[c] ? off[c] : 0;
+        p.len[c] = len[c];
+    }
     const int G = std::max(1, max_blocks);
     size_t t = cfg_tile ? cfg_tile : std::max<size_t>(total / (size_t)G, RDC_MIN_TILE);
     t = std::max<size_t>(round_up(t, RDC_SLOT_ALIGN), RDC_MIN_TILE);
@@ -179,6 +200,56 @@ std::vector<Piece> PlanBroadcast(uint64_t bytes, const Layout& L, size_t cfg_til
         out.push_back(p);
     }
     return out;
+}
+
+CoalescedPlan PlanCoalesced(int n, const uint64_t* counts, int nbuf, size_t esz, uint64_t unit_max) {
+    CoalescedPlan P;
+    memset(P.off, 0, sizeof(P.off));
+    memset(P.len, 0, sizeof(P.len));
+    P.total = 0;
+    unit_max = std::max<uint64_t>(round_down(unit_max, 16), 16);
+    std::vector<int64_t> cb((size_t)nbuf * RDC_MAX_RANKS), ce((size_t)nbuf * RDC_MAX_RANKS);
+    for (int b = 0; b < nbuf; ++b) SplitRanges((int64_t)counts[b], n, &cb[(size_t)b * RDC_MAX_RANKS], &ce[(size_t)b * RDC_MAX_RANKS]);
+    uint64_t end = 0;
+    for (int c = 0; c < n; ++c) {
+        uint64_t at = round_up(end, RDC_SLOT_ALIGN);  // every packed chunk starts 256-B aligned (mis = 0)
+        P.off[c] = at;
+        for (int b = 0; b < nbuf; ++b) {
+            const int64_t b0 = cb[(size_t)b * RDC_MAX_RANKS + c], e0 = ce[(size_t)b * RDC_MAX_RANKS + c];
+            if (e0 <= b0) continue;
+            const uint64_t so = (uint64_t)b0 * esz, sl = (uint64_t)(e0 - b0) * esz;
+            for (uint64_t x = 0; x < sl; x += unit_max) {
+                PackUnit u;
+                u.buf = (uint64_t)b;
+                u.buf_off = so + x;
+                u.packed = at + x;
+                u.len = std::min<uint64_t>(unit_max, sl - x);
+                P.units.push_back(u);
+            }
+            at = round_up(at + sl, 16);  // next segment 16-B aligned
+        }
+        P.len[c] = at - P.off[c];
+        if (P.len[c] == 0) P.off[c] = 0;
+        else end = at;
+    }
+    P.total = end;
+    return P;
+}
+
+std::vector<int> GroupCoalesced(const uint64_t* counts, int nbuf, size_t esz, uint64_t fuse_bytes) {
+    std::vector<int> bounds;
+    bounds.push_back(0);
+    uint64_t acc = 0;
+    for (int b = 0; b < nbuf; ++b) {
+        const uint64_t s = counts[b] * esz;
+        if (b > bounds.back() && acc + s > fuse_bytes) {
+            bounds.push_back(b);
+            acc = 0;
+        }
+        acc += s;
+    }
+    if (nbuf > 0) bounds.push_back(nbuf);
+    return bounds;
 }
 
 }  // namespace rdc_amd

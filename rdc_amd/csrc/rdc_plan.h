@@ -61,4 +61,42 @@ std::vector<Piece> PlanAllgather(int n, const uint64_t* sizes, const Layout& L, 
 // Broadcast pieces of `bytes` (use off/len/mis/tiles [0]).
 std::vector<Piece> PlanBroadcast(uint64_t bytes, const Layout& L, size_t cfg_tile, int max_blocks);
 
+// Allreduce pieces over explicit per-chunk byte ranges [off[c], off[c]+len[c])
+// of one buffer (PlanAllreduce is this with the Split ranges; the coalesced
+// path passes the packed chunk ranges).  Each range length is a multiple of esz.
+std::vector<Piece> PlanAllreduceRanges(int n, const uint64_t* off, const uint64_t* len, size_t esz,
+                                       const Layout& L, int algo, size_t cfg_tile, int max_blocks);
+Piece PlanOneshotRanges(int n, const uint64_t* off, const uint64_t* len, uint64_t total, const Layout& L,
+                        size_t cfg_tile, int max_blocks);
+
+// ---------------------------------------------------- coalesced allreduce ---
+// Many buffers reduced as one launch sequence (BASELINE cfg5: 1024 x 1 MiB,
+// test/mallreduce.cc's back-to-back shape).  The ring order of an element
+// depends only on its Split chunk index c (s = x[c-1]; ...;
+// s = OP(x[c], s)), so chunk c of EVERY buffer can be owned and folded
+// together: the buffers are packed chunk-major into one staging image
+//     [ chunk 0: buf0.c0 | buf1.c0 | ... ][ chunk 1: buf0.c1 | buf1.c1 | ... ] ...
+// (each segment 16-B aligned), the normal schedule runs on that image with
+// chunk c = the packed chunk-c range, and the segments are copied back.
+// Every element is folded in its own buffer's ring order: bit-identical to
+// one rdc::Allreduce per buffer.
+struct PackUnit {       // one copy between a user buffer and the staging image
+    uint64_t buf;       // buffer index (host plan) / user address (device table)
+    uint64_t buf_off;   // byte offset in that buffer
+    uint64_t packed;    // byte offset in the staging image
+    uint64_t len;       // bytes (<= unit_max)
+};
+struct CoalescedPlan {
+    uint64_t off[RDC_MAX_RANKS];  // packed chunk c = [off[c], off[c]+len[c])
+    uint64_t len[RDC_MAX_RANKS];
+    uint64_t total;               // staging bytes
+    std::vector<PackUnit> units;
+};
+constexpr uint64_t kPackUnitMax = 128 << 10;
+CoalescedPlan PlanCoalesced(int n, const uint64_t* counts, int nbuf, size_t esz, uint64_t unit_max = kPackUnitMax);
+// Cut the buffer list (in order) into fusion groups of at most fuse_bytes of
+// data each; a buffer larger than fuse_bytes forms a group of its own.
+// Returns group boundaries: group g = buffers [bounds[g], bounds[g+1]).
+std::vector<int> GroupCoalesced(const uint64_t* counts, int nbuf, size_t esz, uint64_t fuse_bytes);
+
 }  // namespace rdc_amd

@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -54,6 +55,27 @@ int main(int argc, char* argv[]) {
     for (int i = 0; i < W; ++i)
         for (int j = 0; j < i + N; ++j)
             if (g[(size_t)i][(size_t)j] != i + j) return fail("allgather", j, g[(size_t)i][(size_t)j], i + j);
+    // test/mallreduce.cc's rounds k = 0..iter-1 (a[i] = rank + N + k + i), all
+    // rounds' buffers reduced by ONE coalesced call, then Max the same way
+    const int iter = 5;
+    std::vector<std::vector<int>> rounds((size_t)iter, std::vector<int>((size_t)N + 0));
+    std::vector<int*> ptrs((size_t)iter);
+    std::vector<uint64_t> counts((size_t)iter, (uint64_t)N);
+    for (int op = 0; op < 2; ++op) {
+        for (int k = 0; k < iter; ++k) {
+            for (int i = 0; i < N; ++i) rounds[(size_t)k][(size_t)i] = R + N + k + i;
+            ptrs[(size_t)k] = rounds[(size_t)k].data();
+        }
+        if (op == 0) rdc::AllreduceCoalesced<rdc::op::Sum>(ptrs.data(), counts.data(), iter);
+        else rdc::AllreduceCoalesced<rdc::op::Max>(ptrs.data(), counts.data(), iter);
+        for (int k = 0; k < iter; ++k)
+            for (int i = 0; i < N; ++i) {
+                long want = 0;
+                for (int j = 0; j < W; ++j) want = op == 0 ? want + (j + N + k + i) : std::max<long>(want, j + N + k + i);
+                if (rounds[(size_t)k][(size_t)i] != want)
+                    return fail(op == 0 ? "coalesced sum" : "coalesced max", i, rounds[(size_t)k][(size_t)i], want);
+            }
+    }
     printf("rank %d: known-answer OK (world %d, N %d)\n", R, W, N);
     rdc::Finalize();
     return 0;

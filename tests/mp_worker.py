@@ -78,6 +78,33 @@ def main():
             np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), acc.cpu().numpy().view(np.uint8))
             print("rank %d case %d ok" % (rank, i), flush=True)
             continue
+        if kind == "coalesced":
+            # bucketed allreduce: buffer b filled with seed + b, one fused call per rep
+            counts = c["counts"]
+            pads = [(rank * 3 + b) % 5 * esz[dtype] for b in range(len(counts))]
+            bufs = [torch.zeros(k * esz[dtype] + pd + 64, dtype=torch.uint8, device="cuda")
+                    for k, pd in zip(counts, pads)]
+            ptrs = [t.data_ptr() + pd for t, pd in zip(bufs, pads)]
+            for b, k in enumerate(counts):
+                check_call(_LIB.RdcFill(ctypes.c_void_p(ptrs[b]), k, dtype, c.get("seed", 0x5EED0000) + b, rank, sp))
+            arr = (ctypes.c_void_p * len(counts))(*ptrs)
+            cnt = (ctypes.c_size_t * len(counts))(*counts)
+            for _ in range(c.get("reps", 1)):
+                if c.get("host"):
+                    hosts = [t[pd: pd + k * esz[dtype]].cpu().numpy().copy() for t, pd, k in zip(bufs, pads, counts)]
+                    harr = (ctypes.c_void_p * len(counts))(*[h.ctypes.data for h in hosts])
+                    check_call(_LIB.RdcAllreduceCoalesced(harr, cnt, len(counts), dtype, c["op"]))
+                    for t, pd, h in zip(bufs, pads, hosts):
+                        if h.size:
+                            t[pd: pd + h.size] = torch.from_numpy(h).cuda()
+                else:
+                    check_call(_LIB.RdcCommAllreduceCoalesced(comm.handle, arr, cnt, len(counts), dtype, c["op"],
+                                                              c.get("algo", 0), sp))
+            comm.check(sp)
+            out = np.concatenate([t[pd: pd + k * esz[dtype]].cpu().numpy() for t, pd, k in zip(bufs, pads, counts)])
+            np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
+            print("rank %d case %d ok" % (rank, i), flush=True)
+            continue
         reps = c.get("reps", 1)
         for _ in range(reps):
             if kind == "allreduce":

@@ -233,6 +233,15 @@ def expected_for(case, world):
             O.reducer(O.fill(case["count"], O.DT_INT32, case.get("seed", 0x5EED0000) + k, root), acc, O.DT_INT32,
                       O.OP_SUM)
         return [acc] * world
+    if case.get("kind") == "coalesced":
+        per = []
+        for b, k in enumerate(case["counts"]):
+            xs = [O.fill(k, dt, case.get("seed", 0x5EED0000) + b, r) for r in range(world)]
+            for _ in range(case.get("reps", 1)):
+                O.allreduce_ring(xs, dt, case["op"])
+            per.append(xs)
+        return [np.concatenate([per[b][r] for b in range(len(per))]) if per else np.zeros(0, np.uint8)
+                for r in range(world)]
     inputs = [O.fill(case["count"], dt, case.get("seed", 0x5EED0000), r) for r in range(world)]
     kind = case.get("kind", "allreduce")
     if kind == "broadcast":
@@ -268,6 +277,10 @@ def test_mp_allreduce(world):
         {"count": 1000, "dtype": 2, "kind": "allgather"},
         {"count": 400001, "dtype": 2, "kind": "allgather"},
         {"count": 300001, "dtype": 2, "kind": "bcast_chain", "steps": 12},
+        {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1024, 7, 0, 100003, 1, 65536], "reps": 2},
+        {"count": 0, "dtype": 10, "op": 0, "kind": "coalesced", "counts": [4099] * 9, "algo": 1},
+        {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [333, 20000, 5], "algo": 3, "reps": 3},
+        {"count": 0, "dtype": 2, "op": 2, "kind": "coalesced", "counts": [3, 1000, 77], "host": True},
     ]
     tmp = run_mp(world, cases)
     for i, c in enumerate(cases):
@@ -349,3 +362,131 @@ def test_mp_mixed_schedule_chain():
     for r in range(3):
         got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
         assert got.tobytes() == np.frombuffer(bufs[r].tobytes(), dtype=np.uint8).tobytes(), r
+
+
+# ------------------------------------------------------- coalesced (buckets)
+def run_group_coalesced(comms, bufsets, dtype, op, algo, pads):
+    """bufsets[r][b]: rank r's input of bucket b.  One fused call per rank."""
+    import ctypes
+    from rdc_amd._lib import _LIB
+    n = len(comms)
+    nb = len(bufsets[0])
+    esz = np.dtype(O.NP_DTYPE[dtype]).itemsize
+    devs = [[to_dev(bufsets[r][b], pads[r][b] * esz) for b in range(nb)] for r in range(n)]
+    torch.cuda.synchronize()
+    for r in range(n):
+        arr = (ctypes.c_void_p * nb)(*[devs[r][b].data_ptr() + pads[r][b] * esz for b in range(nb)])
+        cnt = (ctypes.c_size_t * nb)(*[bufsets[r][b].size for b in range(nb)])
+        rc = _LIB.RdcCommAllreduceCoalesced(comms[r].handle, arr, cnt, nb, dtype, op, algo,
+                                            ctypes.c_void_p(comms.streams[r].cuda_stream))
+        assert rc == 0, _LIB.RdcGetLastError()
+    for r in range(n):
+        comms[r].check(ctypes.c_void_p(comms.streams[r].cuda_stream))
+    return [[from_dev(devs[r][b], pads[r][b] * esz, bufsets[r][b].size, dtype) for b in range(nb)]
+            for r in range(n)]
+
+
+BUCKETS = [[1024] * 6, [1, 2, 3, 1001, 0, 7], [4099, 1 << 16, 3], [0, 0, 5], [17, 100003, 1, 2]]
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+@pytest.mark.parametrize("dtype,op", [(6, 2), (10, 2), (11, 2), (7, 1), (2, 0), (0, 3), (4, 2)])
+def test_group3_coalesced(group3, dtype, op, algo):
+    """Coalesced allreduce == one reference allreduce per bucket, bit for bit:
+    ragged bucket sizes (incl. empty buckets and buckets shorter than n),
+    every bucket its own allocation at a per-rank, per-bucket misalignment."""
+    rng = np.random.default_rng(1000 + dtype * 8 + op)
+    for counts in BUCKETS:
+        sets = [[rand_input(rng, k, dtype) for k in counts] for _ in range(3)]
+        pads = [[(r + 2 * b) % 4 for b in range(len(counts))] for r in range(3)]
+        got = run_group_coalesced(group3, sets, dtype, op, algo, pads)
+        for b, k in enumerate(counts):
+            want = O.expected_allreduce([sets[r][b] for r in range(3)], dtype, op)
+            for r in range(3):
+                assert same_bits(got[r][b], want, dtype), (counts, algo, b, r)
+
+
+def test_group_coalesced_fusion_groups_and_cache(group2):
+    """Small fuse groups (RDC_FUSE_BYTES) split the list into several fused
+    launch sequences; repeated calls with the same buffers reuse the cached
+    unit table and still produce fresh results."""
+    import ctypes
+    import rdc_amd
+    from rdc_amd._lib import _LIB
+    rng = np.random.default_rng(11)
+    assert _LIB.RdcSetParam(b"RDC_FUSE_BYTES", b"64K") == 0
+    try:
+        g = make_group(2, 16 << 20)
+    finally:
+        assert _LIB.RdcSetParam(b"RDC_FUSE_BYTES", b"256M") == 0
+    try:
+        counts = [5000, 9000, 30000, 1, 16384, 2000]      # 20 KB .. 120 KB fp32 -> several groups
+        ts = [[torch.zeros(k, dtype=torch.float32, device="cuda") for k in counts] for _ in range(2)]
+        for it in range(3):
+            xs = [[rng.standard_normal(k).astype(np.float32) for k in counts] for _ in range(2)]
+            for r in range(2):
+                for b in range(len(counts)):
+                    ts[r][b].copy_(torch.from_numpy(xs[r][b]))
+            torch.cuda.synchronize()
+            for r in range(2):
+                g[r].allreduce_coalesced(ts[r], rdc_amd.Op.SUM, stream=ctypes.c_void_p(g.streams[r].cuda_stream))
+            for r in range(2):
+                g[r].check(ctypes.c_void_p(g.streams[r].cuda_stream))
+            for b in range(len(counts)):
+                want = O.expected_allreduce([xs[0][b], xs[1][b]], O.DT_FLOAT32, O.OP_SUM)
+                for r in range(2):
+                    assert ts[r][b].cpu().numpy().tobytes() == want.tobytes(), (it, b, r)
+    finally:
+        for c in g:
+            c.destroy()
+
+
+def test_group_coalesced_graph_capture(group2):
+    """After a warm-up call (unit table cached), a coalesced allreduce is
+    capturable in a hipGraph and replays with fresh inputs."""
+    import ctypes
+    import rdc_amd
+    rng = np.random.default_rng(12)
+    counts = [4096, 333, 70001, 8]
+    ts = [[torch.zeros(k, dtype=torch.float32, device="cuda") for k in counts] for _ in range(2)]
+    sp = [ctypes.c_void_p(group2.streams[r].cuda_stream) for r in range(2)]
+    torch.cuda.synchronize()
+    for r in range(2):
+        group2[r].allreduce_coalesced(ts[r], rdc_amd.Op.SUM, stream=sp[r])
+    for r in range(2):
+        group2[r].check(sp[r])
+    graphs = []
+    for r in range(2):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=group2.streams[r], capture_error_mode="thread_local"):
+            group2[r].allreduce_coalesced(ts[r], rdc_amd.Op.SUM, stream=sp[r])
+        graphs.append(gr)
+    torch.cuda.synchronize()
+    for it in range(3):
+        xs = [[rng.standard_normal(k).astype(np.float32) for k in counts] for _ in range(2)]
+        for r in range(2):
+            for b in range(len(counts)):
+                ts[r][b].copy_(torch.from_numpy(xs[r][b]))
+        torch.cuda.synchronize()
+        for r in range(2):
+            with torch.cuda.stream(group2.streams[r]):
+                graphs[r].replay()
+        for r in range(2):
+            group2[r].check(sp[r])
+        for b in range(len(counts)):
+            want = O.expected_allreduce([xs[0][b], xs[1][b]], O.DT_FLOAT32, O.OP_SUM)
+            for r in range(2):
+                assert ts[r][b].cpu().numpy().tobytes() == want.tobytes(), (it, b, r)
+
+
+def test_mp_coalesced_cfg5_shape():
+    """BASELINE cfg5 shape (scaled): 64 x 1 MiB fp32 buckets in one coalesced
+    call on 4 processes, twice (cached unit table), vs one oracle ring per bucket."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [{"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1 << 18] * 64, "reps": 2}]
+    tmp = run_mp(4, cases, env_extra={"RDC_SCRATCH_BYTES": "256M"})
+    want = expected_for(cases[0], 4)
+    for r in range(4):
+        got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
+        assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), r

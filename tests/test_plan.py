@@ -93,3 +93,78 @@ def test_default_scratch_fits_cfg3_in_one_launch():
 def test_empty_and_world1():
     assert plan(4, 0, O.DT_FLOAT32, 0) == []
     assert plan(1, 100, O.DT_FLOAT32, 0) == []
+
+
+# ------------------------------------------------------------ coalesced ---
+def plan_coalesced(n, counts, dtype):
+    from rdc_amd._lib import _LIB
+    nb = len(counts)
+    cnt = (ctypes.c_size_t * max(1, nb))(*counts)
+    chunk = (ctypes.c_uint64 * 33)()
+    nu = ctypes.c_int()
+    assert _LIB.RdcPlanCoalesced(n, cnt, nb, dtype, chunk, None, 0, ctypes.byref(nu)) == 0, _LIB.RdcGetLastError()
+    units = (ctypes.c_uint64 * (4 * max(1, nu.value)))()
+    assert _LIB.RdcPlanCoalesced(n, cnt, nb, dtype, chunk, units, nu.value, ctypes.byref(nu)) == 0
+    u = np.frombuffer(units, dtype=np.uint64).reshape(-1, 4)[: nu.value].astype(np.int64)
+    return [int(x) for x in chunk[:n]], [int(x) for x in chunk[16:16 + n]], int(chunk[32]), u
+
+
+COALESCED = [
+    (2, [1024] * 8), (3, [1, 2, 3, 1001, 0, 7]), (5, [4099, 1 << 16, 3]), (8, [(1 << 20) // 4] * 16),
+    (8, [0, 0, 5]), (16, [17, 100003, 1]), (4, [(1 << 18) + 5]),
+]
+
+
+@pytest.mark.parametrize("n,counts", COALESCED)
+@pytest.mark.parametrize("dt", [O.DT_INT8, O.DT_FLOAT16, O.DT_FLOAT32, O.DT_FLOAT64])
+def test_coalesced_plan_packs_chunk_major(n, counts, dt):
+    """Every (buffer, Split chunk c) segment lands once, 16-B aligned, inside
+    packed chunk c's range; chunk ranges are disjoint, 256-B aligned and in
+    order; copy units cover each segment contiguously."""
+    esz = np.dtype(O.NP_DTYPE[dt]).itemsize
+    off, ln, total, units = plan_coalesced(n, counts, dt)
+    prev_end = 0
+    for c in range(n):
+        if ln[c]:
+            assert off[c] % 256 == 0 and off[c] >= prev_end and ln[c] % esz == 0
+            prev_end = off[c] + ln[c]
+    assert total == prev_end
+    covered = {}
+    for b, boff, packed, l in units:
+        assert 0 < l <= 128 << 10 and packed + l <= total
+        covered.setdefault(int(b), []).append((int(boff), int(packed), int(l)))
+    for b, cnt in enumerate(counts):
+        segs = sorted(covered.get(b, []))
+        pos = 0
+        for c, (s0, s1) in enumerate(O.split(cnt, n)):
+            lo, hi = s0 * esz, s1 * esz
+            while pos < len(segs) and segs[pos][0] < hi:
+                boff, packed, l = segs[pos]
+                assert lo <= boff and boff + l <= hi           # inside buffer b's chunk c
+                assert off[c] <= packed and packed + l <= off[c] + ln[c]  # inside packed chunk c
+                if boff == lo:
+                    assert packed % 16 == 0                    # segment start aligned
+                pos += 1
+        assert sum(s[2] for s in segs) == cnt * esz           # every byte exactly once
+    # image ranges of distinct units never overlap
+    spans = sorted((int(p), int(p + l)) for _, _, p, l in units)
+    for (a0, a1), (b0, _) in zip(spans, spans[1:]):
+        assert a1 <= b0
+
+
+def fuse_groups(counts, dt, fuse):
+    from rdc_amd._lib import _LIB
+    nb = len(counts)
+    cnt = (ctypes.c_size_t * max(1, nb))(*counts)
+    out = (ctypes.c_int * (nb + 2))()
+    k = ctypes.c_int()
+    assert _LIB.RdcPlanFuseGroups(cnt, nb, dt, fuse, out, nb + 2, ctypes.byref(k)) == 0
+    return list(out[: k.value])
+
+
+def test_fuse_groups():
+    f32 = O.DT_FLOAT32
+    assert fuse_groups([], f32, 1 << 20) == [0]
+    assert fuse_groups([256] * 8, f32, 4096) == [0, 4, 8]           # 1 KiB each, 4 KiB groups
+    assert fuse_groups([256, 10000, 256], f32, 4096) == [0, 1, 2, 3]  # an oversized buffer is alone
+    assert fuse_groups([(1 << 20) // 4] * 1024, f32, 0) == list(range(0, 1025, 256))  # cfg5: 4 x 256 MiB
