@@ -1,0 +1,154 @@
+"""Single-node launcher — the counterpart of the reference's
+``python -m tracker.launcher_local -n N prog args`` (tracker/launcher_local.py,
+tracker/args.py) for the MI355X path:
+
+    python -m rdc_amd.launcher -n 8 ./test_allreduce 1024
+    python -m rdc_amd.launcher -n 8 python train.py
+
+Starts N worker processes on this node, one per GPU (rank r -> GPU
+r % #GPUs via LOCAL_RANK), with the reference's environment contract
+(tracker/tracker.py:467-477): RDC_TRACKER_URI / RDC_TRACKER_PORT (here the
+rendezvous of rank 0's TCP bootstrap, which exchanges HIP IPC handles — no
+Python tracker process and no data over TCP), RDC_HEARTBEAT_INTERVAL,
+plus RDC_RANK / RDC_WORLD_SIZE so ranks are fixed up front.  Like
+launcher_local's keepalive loop (launcher_local.py:17-27), a worker that
+exits with code 254 is restarted with RDC_NUM_ATTEMPT incremented (before the
+rendezvous completes; rejoining a running job is the tracker's recovery
+protocol, out of scope like checkpointing).  Unlike
+it, the first worker that fails for good stops the others and its exit code
+is returned (the reference raises inside a daemon thread and hangs).
+"""
+import argparse
+import os
+import socket
+import subprocess
+import sys
+import threading
+import time
+
+RESTART_RC = 254
+HEARTBEAT_INTERVAL_MS = 5000  # tracker/tracker.py HEARTBEAT_INTERVAL_MS (accepted, unused on the device path)
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description="launch rdc workers on this node (one process per GPU)")
+    p.add_argument("-n", "--num-workers", type=int, required=True, help="number of worker processes")
+    p.add_argument("--host-ip", default="127.0.0.1", help="address rank 0's bootstrap listens on")
+    p.add_argument("--port", type=int, default=0, help="bootstrap port (0 = pick a free one)")
+    p.add_argument("--gpus", type=int, default=0, help="GPUs to spread ranks over (0 = all visible)")
+    p.add_argument("--max-attempts", type=int, default=10, help="restarts per worker on exit code 254")
+    p.add_argument("command", nargs=argparse.REMAINDER, help="command for launching the program")
+    args, unknown = p.parse_known_args(argv)
+    # the reference appends unknown options to the command (launcher_local.py:34)
+    args.command = list(args.command) + list(unknown)
+    if not args.command:
+        p.error("missing command")
+    if args.num_workers < 1:
+        p.error("--num-workers must be >= 1")
+    return args
+
+
+def free_port(host):
+    s = socket.socket()
+    s.bind((host, 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def count_gpus():
+    """GPUs visible to the workers, without initialising HIP in this process."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            return len([x for x in v.split(",") if x.strip()])
+    try:
+        return len([d for d in os.listdir("/dev/dri") if d.startswith("renderD")]) or 1
+    except OSError:
+        return 1
+
+
+def worker_env(args, rank, port, ngpu):
+    env = dict(os.environ)
+    env.update({
+        "RDC_TRACKER_URI": args.host_ip,
+        "RDC_TRACKER_PORT": str(port),
+        "RDC_HEARTBEAT_INTERVAL": str(HEARTBEAT_INTERVAL_MS),
+        "RDC_RANK": str(rank),
+        "RDC_WORLD_SIZE": str(args.num_workers),
+        "LOCAL_RANK": str(rank % max(1, ngpu)),
+    })
+    # torchrun-style names would override the rdc ones inside RdcInit's
+    # fallbacks only where rdc names are absent; drop stale ones anyway
+    for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def run(args):
+    port = args.port or free_port(args.host_ip)
+    ngpu = args.gpus or count_gpus()
+    procs = [None] * args.num_workers
+    rcs = [None] * args.num_workers
+    lock = threading.Lock()
+    stop = threading.Event()
+    first_fail = []  # exit code of the worker that failed first
+
+    def keepalive(rank):
+        env = worker_env(args, rank, port, ngpu)
+        attempt = 0
+        while not stop.is_set():
+            env["RDC_NUM_ATTEMPT"] = str(attempt)
+            with lock:
+                if stop.is_set():
+                    return
+                procs[rank] = subprocess.Popen(args.command, env=env)
+            rc = procs[rank].wait()
+            if rc == RESTART_RC and attempt + 1 < args.max_attempts:
+                attempt += 1
+                continue
+            rcs[rank] = rc
+            if rc != 0:
+                with lock:
+                    if not stop.is_set():
+                        first_fail.append(rc)
+                    stop.set()
+            return
+
+    threads = [threading.Thread(target=keepalive, args=(r,), daemon=True) for r in range(args.num_workers)]
+    for t in threads:
+        t.start()
+    try:
+        while any(t.is_alive() for t in threads):
+            if stop.is_set():
+                break
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        stop.set()
+    if stop.is_set():
+        # one worker failed for good: stop the rest (they would wait on it)
+        with lock:
+            live = [p for p in procs if p is not None and p.poll() is None]
+        for p in live:
+            p.terminate()
+        deadline = time.time() + 10
+        for p in live:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+    for t in threads:
+        t.join(timeout=15)
+    if first_fail:
+        return first_fail[0]
+    if any(rc is None for rc in rcs):
+        return 1
+    return 0
+
+
+def main(argv=None):
+    return run(parse_args(argv))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -58,3 +58,16 @@ def test_bench_torchrun_two_ranks():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["roofline"]["bound"] == "xgmi"
     assert out["config"]["bytes_per_gpu"] == 64 << 20
+
+
+def test_launcher_cpp_known_answer(known_answer_exe):
+    """The reference's workflow (launcher -n N prog args) with rdc_amd's
+    launcher: the C++ known-answer program at 3 ranks, rendezvous from env."""
+    env = dict(os.environ, RDC_SCRATCH_BYTES="64M", RDC_NBLOCKS="32")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-m", "rdc_amd.launcher", "-n", "3", "--gpus", "1", known_answer_exe, "4099"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(3):
+        assert "rank %d: known-answer OK" % r in p.stdout, p.stdout

@@ -137,3 +137,48 @@ def test_gloo_owner_computes_matches_ring(world, count, dtype, op):
     for p in ps:
         p.join(timeout=60)
     assert all(res[r] is True for r in range(world)), res
+
+
+# ------------------------------------------------------------- launcher ---
+LAUNCHED = r'''
+import os, sys
+att = int(os.environ["RDC_NUM_ATTEMPT"])
+if sys.argv[1] == "restart" and os.environ["RDC_RANK"] == "1" and att == 0:
+    sys.exit(254)                # asks the keepalive loop for a restart (launcher_local.py:17-27)
+import rdc_amd as r
+r.init([])                       # rank / world / rendezvous from the launcher's env
+if sys.argv[1] == "fail" and r.get_rank() == 2:
+    sys.exit(3)
+r.barrier()
+print("rank %d/%d attempt %d local %s ok" % (r.get_rank(), r.get_world_size(), att, os.environ["LOCAL_RANK"]),
+      flush=True)
+r.finalize()
+'''
+
+
+def launch(n, mode, timeout=180):
+    return subprocess.run([sys.executable, "-m", "rdc_amd.launcher", "-n", str(n), "--gpus", "2",
+                           sys.executable, "-c", LAUNCHED, mode],
+                          cwd=ROOT, env=clean_env(), capture_output=True, text=True, timeout=timeout)
+
+
+def test_launcher_runs_workers_with_reference_env():
+    p = launch(3, "ok")
+    assert p.returncode == 0, p.stdout + p.stderr
+    for r in range(3):
+        assert "rank %d/3 attempt 0 local %d ok" % (r, r % 2) in p.stdout, p.stdout
+
+
+def test_launcher_restarts_on_254():
+    """A worker that exits 254 before the rendezvous is restarted and joins
+    (mid-job recovery is the tracker's fault-tolerance protocol: out of scope)."""
+    p = launch(2, "restart")
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "rank 1/2 attempt 1" in p.stdout and "rank 0/2 attempt 0" in p.stdout, p.stdout
+
+
+def test_launcher_stops_all_on_failure():
+    """rank 2 exits 3: the others (blocked in the bootstrap) are stopped and
+    the launcher returns 3 instead of hanging."""
+    p = launch(3, "fail", timeout=120)
+    assert p.returncode == 3, p.stdout + p.stderr

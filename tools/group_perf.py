@@ -2,6 +2,8 @@
 (all ranks share GPU 0, so this measures the protocol + HBM side, not xGMI).
 
     RDC_ALLOC=uncached|fine|coarse python tools/group_perf.py n size [size...]
+    GP_BUCKETS=K: each size split into K buckets, one coalesced call (plus the
+    same K buckets as separate calls, for comparison)
 """
 import ctypes
 import os
@@ -35,11 +37,22 @@ def main():
         for r in range(n):
             rdc_amd.fill_(bufs[r], 1, r)
         torch.cuda.synchronize()
-        for algo in (2, 1):
+        K = int(os.environ.get("GP_BUCKETS", "1"))
+        modes = (2, 1) if K == 1 else ("coalesced", "separate")
+        per = count // K
+        views = [[bufs[r][b * per:(b + 1) * per] for b in range(K)] for r in range(n)]
+        for algo in modes:
             def once():
                 for r in range(n):
-                    check_call(_LIB.RdcCommAllreduceEx(comms[r].handle, ctypes.c_void_p(bufs[r].data_ptr()), count,
-                                                       6, 2, algo, ctypes.c_void_p(streams[r].cuda_stream)))
+                    sp = ctypes.c_void_p(streams[r].cuda_stream)
+                    if algo == "coalesced":
+                        comms[r].allreduce_coalesced(views[r], 2, stream=sp)
+                    elif algo == "separate":
+                        for v in views[r]:
+                            comms[r].allreduce(v, 2, stream=sp)
+                    else:
+                        check_call(_LIB.RdcCommAllreduceEx(comms[r].handle, ctypes.c_void_p(bufs[r].data_ptr()),
+                                                           count, 6, 2, algo, sp))
             once()
             for r in range(n):
                 comms[r].check(ctypes.c_void_p(streams[r].cuda_stream))
@@ -50,8 +63,8 @@ def main():
             for r in range(n):
                 comms[r].check(ctypes.c_void_p(streams[r].cuda_stream))
             dt = (time.perf_counter() - t0) / it
-            print("n=%d S=%9d algo=%s  %.3f ms  algbw %.1f GB/s" % (n, S, "mesh" if algo == 2 else "ring",
-                                                                   dt * 1e3, S / dt / 1e9), flush=True)
+            name = {2: "mesh", 1: "ring"}.get(algo, "%s x%d" % (algo, K))
+            print("n=%d S=%9d algo=%s  %.3f ms  algbw %.1f GB/s" % (n, S, name, dt * 1e3, S / dt / 1e9), flush=True)
     for c in comms:
         c.destroy()
 
