@@ -31,6 +31,8 @@ HBM_PEAK_GBPS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_DIR_GBPS = 76.8     # one xGMI link, one direction (153.6 GB/s bidirectional)
 BIDIR_RING_GBPS = 153.6       # north-star roofline: two counter-rotating rings (busbw)
 DTYPES = {"float32": (6, 4), "float16": (10, 2), "bfloat16": (11, 2), "float64": (7, 8)}
+DT_SHORT = {"float32": "f32", "float16": "f16", "bfloat16": "bf16", "float64": "f64"}
+CXX_TYPE = {"float32": "float", "float16": "_Float16", "bfloat16": "bf16_t", "float64": "double"}
 
 
 def parse():
@@ -199,7 +201,7 @@ def main():
         acc = d0.copy()
         for _ in range(args.warmup + args.steps):
             O.reducer(s0, acc, dt_enum, 2)
-        got = dst[:m].cpu().numpy()
+        got = dst[:m].cpu().view(torch.uint8).numpy()  # bytes (numpy has no bfloat16)
         check = bool(got.tobytes() == acc.tobytes())
 
     if rank != 0:
@@ -212,7 +214,8 @@ def main():
         achieved = 3 * S / (kern_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": load_traffic("reduce_sum_f32_%d" % S), "kernel": "k_reduce<Sum,float>",
+                "traffic": load_traffic("reduce_sum_%s_%d" % (DT_SHORT[args.dtype], S)),
+                "kernel": "k_reduce<Sum,%s>" % CXX_TYPE[args.dtype],
                 "algorithmic_bytes_per_launch": 3 * S, "kernel_avg_ms": round(kern_ms, 4)}
         workload = "reduce kernel alone (n=1): dst += src, %s, %d MiB per buffer" % (args.dtype, S >> 20)
         par = "single GPU"
@@ -246,7 +249,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {"float32": "f32", "float16": "f16", "bfloat16": "bf16", "float64": "f64"}[args.dtype],
+        "dtype": DT_SHORT[args.dtype],
         "data": "synthetic (splitmix64 device generator, seed 0x5EED0000)",
         "config": {"workload": workload, "bytes_per_gpu": S, "parallelism": par},
         "algbw_GBps": round(algbw, 2),

@@ -40,13 +40,24 @@ def rand_input(rng, count, dtype, special=True):
         return x
     if dtype == O.DT_BFLOAT16:
         f = (rng.standard_normal(count) * 3).astype(np.float32)
-        return np.array([O.lib().rdc_oracle_f32_to_bf16(float(v)) for v in f], dtype=np.uint16)
+        x = np.array([O.lib().rdc_oracle_f32_to_bf16(float(v)) for v in f], dtype=np.uint16)
+        if special and count >= 8:
+            # +-0, +-inf, a denormal, the largest finite (sums overflow to inf), a quiet NaN, -denormal
+            vals = np.array([0x0000, 0x8000, 0x7F80, 0xFF80, 0x0001, 0x7F7F, 0x7FC1, 0x8003], dtype=np.uint16)
+            idx = rng.choice(count, 8, replace=False)
+            x[idx] = vals
+        return x
     info = np.iinfo(npd)
     return rng.integers(info.min, info.max, count, dtype=npd, endpoint=True)
 
 
 def same_bits(a, b, dtype):
     """Bit-exact equality, treating any two NaNs as equal (NaN payloads are not pinned)."""
+    if dtype == O.DT_BFLOAT16:
+        an, bn = (a & 0x7FFF) > 0x7F80, (b & 0x7FFF) > 0x7F80
+        if not np.array_equal(an, bn):
+            return False
+        return a[~an].tobytes() == b[~bn].tobytes()
     if dtype in (O.DT_FLOAT32, O.DT_FLOAT64, O.DT_FLOAT16):
         an, bn = np.isnan(a), np.isnan(b)
         if not np.array_equal(an, bn):

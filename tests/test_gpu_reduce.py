@@ -66,3 +66,20 @@ def test_fill_matches_oracle(lib):
         got = from_dev(t, 0, count, dtype)
         want = O.fill(count, dtype, 0x5EED0000, 3)
         assert got.tobytes() == want.tobytes(), dtype
+
+
+@pytest.mark.parametrize("op", [O.OP_SUM, O.OP_MAX, O.OP_MIN])
+def test_reduce_bf16_every_bit_pattern(lib, op):
+    """bf16 (hardware v_cvt_pk_bf16_f32 on the Sum path): every one of the
+    65536 bit patterns as dst against random patterns (NaNs, infs, denormals
+    included), 16-B body and element-wise head/tail, vs the oracle."""
+    rng = np.random.default_rng(99 + op)
+    d = np.tile(np.arange(65536, dtype=np.uint16), 8)
+    s = rng.integers(0, 65536, d.size, dtype=np.uint16)
+    for pad in (0, 6):
+        td, ts = to_dev(d, pad), to_dev(s, pad)
+        assert lib.RdcReduce(ptr(td, pad), ptr(ts, pad), d.size, O.DT_BFLOAT16, op, None) == 0
+        torch.cuda.synchronize()
+        got = from_dev(td, pad, d.size, O.DT_BFLOAT16)
+        want = O.reducer(s.copy(), d.copy(), O.DT_BFLOAT16, op)
+        assert same_bits(got, want, O.DT_BFLOAT16), (op, pad)
