@@ -8,12 +8,14 @@
 * the ring schedule (which chunk each rank sends / receives per step) and
   IEEE binary16 / bfloat16 conversions against numpy.
 """
+import json
 import os
 
 import numpy as np
 import pytest
 
 from oracle import oracle as O
+from tests.conftest import ROOT
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ring_allreduce.npz")
 
@@ -178,3 +180,25 @@ def test_generator(oracle):
     assert a.tobytes() != b.tobytes() and np.all(np.abs(a) <= 1.0)
     assert len(np.unique(a)) > 990
     assert O.fill(10, O.DT_FLOAT32, 0x5EED0000, 0).tobytes() == a[:10].tobytes()
+
+
+# ----------------------------------------------- CPU TCP ring (baseline port)
+@pytest.mark.parametrize("n,count,dtype,op", [(2, 1024, 6, 2), (3, 1001, 6, 2), (5, 4099, 10, 2),
+                                              (8, 100003, 6, 2), (4, 777, 2, 0), (3, 5, 7, 1), (2, 1, 6, 2)])
+def test_tcp_ring_port_matches_oracle(oracle, tmp_path, n, count, dtype, op):
+    """oracle/tcp_ring (the reference's CPU ring over loopback TCP, restated as
+    n processes) produces exactly the oracle ring's bytes on every rank."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "tcp_ring")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    out = subprocess.run([exe, "-n", str(n), "-c", str(count), "-t", str(dtype), "-o", str(op), "-i", "2", "-w", "1",
+                          "-d", str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["n"] == n and rec["iters"] == 2
+    bufs = [oracle.fill(count, dtype, 0x5EED0000, r) for r in range(n)]
+    oracle.allreduce_ring(bufs, dtype, op)
+    for r in range(n):
+        got = open(os.path.join(str(tmp_path), "rank%d.bin" % r), "rb").read()
+        assert got == bufs[r].tobytes(), (n, count, dtype, op, r)
