@@ -20,6 +20,7 @@
 #include "../../include/rdc_amd.h"
 #include "rdc_bootstrap.h"
 #include "rdc_comm.h"
+#include "rdc_host.h"
 
 using namespace rdc_amd;
 
@@ -42,6 +43,7 @@ struct Manager {
     void* stage = nullptr;
     size_t stage_bytes = 0;
     hipStream_t stream = nullptr;
+    std::unique_ptr<HostPath> host;  // pipelined host-buffer allreduce (rdc_host.h)
 };
 
 Manager& M() {
@@ -213,6 +215,7 @@ int RdcFinalize(void) {
     std::lock_guard<std::recursive_mutex> lk(m.mu);
     if (!m.inited) return 0;
     return guard([&] {
+        m.host.reset();
         m.comms.clear();  // collective destroys (barriers) in name order on every rank
         if (m.stage) (void)hipFree(m.stage);
         m.stage = nullptr;
@@ -299,13 +302,10 @@ void allreduce_sync(Manager& m, Communicator* c, void* sendrecv, size_t count, i
         c->Check(s);
         return;
     }
-    // host-resident buffer: H2D, device allreduce, D2H (host path)
-    const size_t bytes = count * rdc_dtype_size(dtype);
-    void* d = staging(m, bytes, c->device());
-    hcheck(hipMemcpyAsync(d, sendrecv, bytes, hipMemcpyHostToDevice, s), "H2D");
-    c->Allreduce(d, count, dtype, op, s);
-    hcheck(hipMemcpyAsync(sendrecv, d, bytes, hipMemcpyDeviceToHost, s), "D2H");
-    c->Check(s);
+    // host-resident buffer: pieces of every chunk through pinned slots, H2D /
+    // allreduce / D2H overlapped on three streams
+    if (!m.host) m.host.reset(new HostPath(c->device()));
+    m.host->Allreduce(c, sendrecv, count, dtype, op, s);
 }
 
 // synchronous coalesced allreduce of host or device buffers (all of one kind)

@@ -299,6 +299,27 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
     LaunchRanges(ks, static_cast<char*>(buf), off, len, (uint64_t)count * esz, esz, algo, stream);
 }
 
+void Communicator::AllreduceRanges(void* buf, const uint64_t* off, const uint64_t* len, int dtype, int op,
+                                   hipStream_t stream) {
+    KernelSet ks;
+    if (!get_kernels(dtype, op, &ks))
+        throw std::invalid_argument("rdc: unsupported (dtype, op) = (" + std::to_string(dtype) + ", " +
+                                    std::to_string(op) + ")");
+    if (n_ == 1) return;
+    const size_t esz = rdc_dtype_size(dtype);
+    uint64_t total = 0;
+    for (int c = 0; c < n_; ++c) {
+        if (off[c] % esz || len[c] % esz) throw std::invalid_argument("rdc: range not element-aligned");
+        if (len[c]) total = std::max<uint64_t>(total, off[c] + len[c]);
+    }
+    if (total == 0) return;
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    // a piece's ranges are not one contiguous span: never one-shot (it pushes [0, total))
+    int algo = PickAlgo(RDC_ALGO_AUTO);
+    if (algo == RDC_ALGO_ONESHOT) algo = RDC_ALGO_MESH;
+    LaunchRanges(ks, static_cast<char*>(buf), off, len, total, esz, algo, stream);
+}
+
 // The schedule over explicit chunk byte ranges of `buf` (chunk c = [off[c],
 // off[c]+len[c]), folded in the ring order of c).
 void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* off, const uint64_t* len,

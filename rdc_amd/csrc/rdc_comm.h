@@ -52,6 +52,10 @@ public:
     // (bit-identical), moved as fused launches over a chunk-major staging image
     void AllreduceCoalesced(void* const* bufs, const size_t* counts, int nbuf, int dtype, int op,
                             hipStream_t stream, int algo = RDC_ALGO_AUTO);
+    // allreduce of explicit chunk byte ranges of buf (chunk c = [off[c], off[c]+len[c]),
+    // folded in chunk c's ring order): one piece of a larger buffer (host path pipeline)
+    void AllreduceRanges(void* buf, const uint64_t* off, const uint64_t* len, int dtype, int op,
+                         hipStream_t stream);
     void Broadcast(void* buf, size_t bytes, int root, hipStream_t stream);
     // bufs[c] (device) holds sizes[c] bytes; bufs[rank] is this rank's data
     void Allgather(void* const* bufs, const uint64_t* sizes, hipStream_t stream);

@@ -268,6 +268,9 @@ def test_mp_allreduce(world):
         {"count": 70000, "dtype": 11, "op": 2, "reps": 3},
         {"count": 123457, "dtype": 0, "kind": "broadcast", "root": world - 1},
         {"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"},
+        {"count": 25000003, "dtype": 6, "op": 2, "kind": "host_allreduce", "reps": 2},   # 7 pipelined pieces
+        {"count": 3000001, "dtype": 10, "op": 0, "kind": "host_allreduce"},
+        {"count": 5, "dtype": 4, "op": 2, "kind": "host_allreduce"},
         {"count": 100003, "dtype": 6, "op": 2, "algo": 2, "pad_per_rank": 4},   # ranks' buffers differ mod 16
         {"count": 100003, "dtype": 10, "op": 0, "algo": 1, "pad_per_rank": 2},
         {"count": 2, "dtype": 2, "kind": "bcast_chain", "steps": 40},
