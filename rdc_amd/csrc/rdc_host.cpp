@@ -99,43 +99,40 @@ HostPath::HostPath(int device) : device_(device), pool_(std::max(0, env_int("RDC
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "stream");
     hip_check(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking), "stream");
-    for (int i = 0; i < kSlots; ++i) {
-        hip_check(hipEventCreateWithFlags(&in_done_[i], hipEventDisableTiming), "event");
-        hip_check(hipEventCreateWithFlags(&ar_done_[i], hipEventDisableTiming), "event");
-        hip_check(hipEventCreateWithFlags(&out_done_[i], hipEventDisableTiming), "event");
-    }
+    for (int i = 0; i < kSlots; ++i) hip_check(hipEventCreateWithFlags(&in_done_[i], hipEventDisableTiming), "event");
+    drain_ = std::thread([this] { DrainLoop(); });
 }
 
 HostPath::~HostPath() {
+    {
+        std::lock_guard<std::mutex> lk(dmu_);
+        dstop_ = true;
+    }
+    dcv_.notify_all();
+    drain_.join();
     (void)hipSetDevice(device_);
     (void)hipDeviceSynchronize();
     for (int i = 0; i < kSlots; ++i) {
         if (pin_in_[i]) (void)hipHostFree(pin_in_[i]);
-        if (pin_out_[i]) (void)hipHostFree(pin_out_[i]);
         (void)hipEventDestroy(in_done_[i]);
-        (void)hipEventDestroy(ar_done_[i]);
-        (void)hipEventDestroy(out_done_[i]);
     }
+    for (hipEvent_t e : ar_done_) (void)hipEventDestroy(e);
     if (dev_) (void)hipFree(dev_);
     if (h2d_) (void)hipStreamDestroy(h2d_);
     if (d2h_) (void)hipStreamDestroy(d2h_);
 }
 
-void HostPath::Reserve(size_t piece_bytes, size_t total_bytes) {
+void HostPath::Reserve(size_t piece_bytes, size_t total_bytes, int pieces) {
     if (piece_bytes > slot_bytes_) {
         hip_check(hipDeviceSynchronize(), "sync before regrow");
         for (int i = 0; i < kSlots; ++i) {
             if (pin_in_[i]) (void)hipHostFree(pin_in_[i]);
-            if (pin_out_[i]) (void)hipHostFree(pin_out_[i]);
-            pin_in_[i] = pin_out_[i] = nullptr;
+            pin_in_[i] = nullptr;
         }
         slot_bytes_ = 0;
-        for (int i = 0; i < kSlots; ++i) {
+        for (int i = 0; i < kSlots; ++i)
             hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_in_[i]), piece_bytes, hipHostMallocDefault),
                       "hipHostMalloc");
-            hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_out_[i]), piece_bytes, hipHostMallocDefault),
-                      "hipHostMalloc");
-        }
         slot_bytes_ = piece_bytes;
     }
     if (total_bytes > dev_bytes_) {
@@ -147,6 +144,11 @@ void HostPath::Reserve(size_t piece_bytes, size_t total_bytes) {
         }
         hip_check(hipMalloc(reinterpret_cast<void**>(&dev_), total_bytes), "hipMalloc host-path image");
         dev_bytes_ = total_bytes;
+    }
+    while ((int)ar_done_.size() < pieces) {
+        hipEvent_t e;
+        hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+        ar_done_.push_back(e);
     }
 }
 
@@ -164,6 +166,36 @@ void HostPath::Copy(char* dst, const char* src, size_t bytes) {
     });
 }
 
+void HostPath::DrainLoop() {
+    for (;;) {
+        Drain d;
+        char* dst;
+        {
+            std::unique_lock<std::mutex> lk(dmu_);
+            dcv_.wait(lk, [&] { return dstop_ || qhead_ < queue_.size(); });
+            if (dstop_) return;
+            d = queue_[qhead_++];
+            dst = dst_;
+        }
+        std::string err;
+        try {
+            hip_check(hipSetDevice(device_), "hipSetDevice");
+            hip_check(hipEventSynchronize(d.ready), "wait allreduce");
+            for (int q = 0; q < d.nslice; ++q)
+                if (d.len[q])
+                    hip_check(hipMemcpyAsync(dst + d.off[q], dev_ + d.off[q], d.len[q], hipMemcpyDeviceToHost, d2h_),
+                              "D2H");
+            hip_check(hipStreamSynchronize(d2h_), "D2H sync");
+        } catch (const std::exception& e) {
+            err = e.what();
+        }
+        std::lock_guard<std::mutex> lk(dmu_);
+        if (!err.empty() && derr_.empty()) derr_ = err;
+        ++drained_;
+        ddone_cv_.notify_all();
+    }
+}
+
 void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, int op, hipStream_t comm_stream) {
     const int n = c->size();
     if (n == 1 || count == 0) return;
@@ -179,61 +211,61 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
     const uint64_t K0 = std::max<uint64_t>(1, (S + kPieceTarget - 1) / kPieceTarget);
     const uint64_t sl = std::max<uint64_t>(4096, ((maxlen + K0 - 1) / K0 + 4095) & ~(uint64_t)4095);
     const int K = (int)((maxlen + sl - 1) / sl);
-    Reserve((size_t)sl * (size_t)n, S);
-
-    struct Slice {
-        uint64_t off[RDC_MAX_RANKS], len[RDC_MAX_RANKS], pos[RDC_MAX_RANKS];  // pos: offset in the pinned slot
-        uint64_t bytes;
-    };
-    auto slice = [&](int k) {
-        Slice s;
-        memset(&s, 0, sizeof(s));
-        for (int q = 0; q < n; ++q) {
-            const uint64_t lo = (uint64_t)cb[q] * esz + (uint64_t)k * sl;
-            const uint64_t hi = std::min<uint64_t>((uint64_t)ce[q] * esz, lo + sl);
-            s.pos[q] = s.bytes;
-            if (hi > lo && (uint64_t)k * sl < (uint64_t)(ce[q] - cb[q]) * esz) {
-                s.off[q] = lo;
-                s.len[q] = hi - lo;
-                s.bytes += hi - lo;
-            }
-        }
-        return s;
-    };
-    auto drain = [&](int k) {  // D2H of piece k landed: copy its slices back into the user buffer
-        const int slot = k % kSlots;
-        hip_check(hipEventSynchronize(out_done_[slot]), "wait D2H");
-        const Slice s = slice(k);
-        for (int q = 0; q < n; ++q)
-            if (s.len[q]) Copy(h + s.off[q], pin_out_[slot] + s.pos[q], s.len[q]);
-    };
-    for (int k = 0; k < K; ++k) {
-        const int slot = k % kSlots;
-        const Slice s = slice(k);
-        // the slot's previous H2D has been consumed before we overwrite it
-        if (k >= kSlots) hip_check(hipEventSynchronize(in_done_[slot]), "wait H2D slot");
-        for (int q = 0; q < n; ++q)
-            if (s.len[q]) Copy(pin_in_[slot] + s.pos[q], h + s.off[q], s.len[q]);
-        for (int q = 0; q < n; ++q)
-            if (s.len[q])
-                hip_check(hipMemcpyAsync(dev_ + s.off[q], pin_in_[slot] + s.pos[q], s.len[q], hipMemcpyHostToDevice,
-                                         h2d_),
-                          "H2D");
-        hip_check(hipEventRecord(in_done_[slot], h2d_), "record");
-        hip_check(hipStreamWaitEvent(comm_stream, in_done_[slot], 0), "wait");
-        c->AllreduceRanges(dev_, s.off, s.len, dtype, (int)op, comm_stream);
-        hip_check(hipEventRecord(ar_done_[slot], comm_stream), "record");
-        hip_check(hipStreamWaitEvent(d2h_, ar_done_[slot], 0), "wait");
-        // pin_out_[slot] was drained at iteration k-1 (piece k - kSlots)
-        for (int q = 0; q < n; ++q)
-            if (s.len[q])
-                hip_check(hipMemcpyAsync(pin_out_[slot] + s.pos[q], dev_ + s.off[q], s.len[q], hipMemcpyDeviceToHost,
-                                         d2h_),
-                          "D2H");
-        hip_check(hipEventRecord(out_done_[slot], d2h_), "record");
-        if (k - (kSlots - 1) >= 0) drain(k - (kSlots - 1));
+    Reserve((size_t)sl * (size_t)n, S, K);
+    {
+        std::lock_guard<std::mutex> lk(dmu_);
+        queue_.clear();
+        qhead_ = drained_ = 0;
+        dst_ = h;
+        derr_.clear();
     }
-    for (int k = std::max(0, K - (kSlots - 1)); k < K; ++k) drain(k);
+    int issued = 0;
+    std::string err;
+    try {
+        for (int k = 0; k < K; ++k) {
+            const int slot = k % kSlots;
+            Drain d;
+            d.ready = ar_done_[(size_t)k];
+            d.nslice = n;
+            uint64_t pos[RDC_MAX_RANKS], bytes = 0;
+            for (int q = 0; q < n; ++q) {
+                const uint64_t lo = (uint64_t)cb[q] * esz + (uint64_t)k * sl;
+                const uint64_t hi = std::min<uint64_t>((uint64_t)ce[q] * esz, lo + sl);
+                pos[q] = bytes;
+                d.off[q] = hi > lo ? lo : 0;
+                d.len[q] = hi > lo ? hi - lo : 0;
+                bytes += d.len[q];
+            }
+            // the slot's previous H2D has been consumed before we overwrite it
+            if (k >= kSlots) hip_check(hipEventSynchronize(in_done_[slot]), "wait H2D slot");
+            for (int q = 0; q < n; ++q)
+                if (d.len[q]) Copy(pin_in_[slot] + pos[q], h + d.off[q], d.len[q]);
+            for (int q = 0; q < n; ++q)
+                if (d.len[q])
+                    hip_check(hipMemcpyAsync(dev_ + d.off[q], pin_in_[slot] + pos[q], d.len[q],
+                                             hipMemcpyHostToDevice, h2d_),
+                              "H2D");
+            hip_check(hipEventRecord(in_done_[slot], h2d_), "record");
+            hip_check(hipStreamWaitEvent(comm_stream, in_done_[slot], 0), "wait");
+            c->AllreduceRanges(dev_, d.off, d.len, dtype, op, comm_stream);
+            hip_check(hipEventRecord(d.ready, comm_stream), "record");
+            {
+                std::lock_guard<std::mutex> lk(dmu_);
+                queue_.push_back(d);
+            }
+            dcv_.notify_all();
+            ++issued;
+        }
+    } catch (const std::exception& e) {
+        err = e.what();
+    }
+    {   // every issued piece drained (the drain thread owns the user buffer until then)
+        std::unique_lock<std::mutex> lk(dmu_);
+        ddone_cv_.wait(lk, [&] { return (int)drained_ == issued; });
+        if (err.empty()) err = derr_;
+        dst_ = nullptr;
+    }
+    if (!err.empty()) throw std::runtime_error(err);
     c->Check(comm_stream);  // a device-side failure surfaces here
 }
 

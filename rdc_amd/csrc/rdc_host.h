@@ -8,16 +8,19 @@
 // Per piece, on three streams:
 //   host threads memcpy the slices into a pinned slot -> H2D DMA (copy stream)
 //   -> allreduce of the slices on the communicator's stream
-//   -> D2H DMA into a pinned slot (second copy stream) -> host threads copy back,
+//   -> a drain thread waits for it and copies the slices straight back into
+//      the pageable buffer (D2H on a second copy stream),
 // so piece k+1's H2D and piece k-1's D2H run under piece k's allreduce.
-// Pageable H2D runs 12-22 GB/s on the box, pinned DMA 57 GB/s each way
-// (tools/host_copy_bench.cpp).
+// On the box pageable H2D runs 12-22 GB/s but pinned DMA 57 GB/s, while
+// pageable D2H already runs 56 GB/s (tools/host_copy_bench.cpp):
+// stage the input only.
 #pragma once
 #include <hip/hip_runtime_api.h>
 
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -53,18 +56,33 @@ public:
 
 private:
     static constexpr int kSlots = 3;
-    void Reserve(size_t piece_bytes, size_t total_bytes);
+    struct Drain {                 // one piece for the drain thread
+        hipEvent_t ready;          // the piece's allreduce finished
+        int nslice;
+        uint64_t off[RDC_MAX_RANKS], len[RDC_MAX_RANKS];
+    };
+    void Reserve(size_t piece_bytes, size_t total_bytes, int pieces);
     void Copy(char* dst, const char* src, size_t bytes);  // parallel memcpy
+    void DrainLoop();
 
     int device_;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
-    hipEvent_t in_done_[kSlots] = {}, ar_done_[kSlots] = {}, out_done_[kSlots] = {};
+    hipEvent_t in_done_[kSlots] = {};
+    std::vector<hipEvent_t> ar_done_;  // one per piece of the current call
     char* pin_in_[kSlots] = {};
-    char* pin_out_[kSlots] = {};
     size_t slot_bytes_ = 0;
     char* dev_ = nullptr;  // device image of the buffer
     size_t dev_bytes_ = 0;
     CopyPool pool_;
+    // drain thread: D2H of finished pieces into the user's buffer
+    std::thread drain_;
+    std::mutex dmu_;
+    std::condition_variable dcv_, ddone_cv_;
+    std::vector<Drain> queue_;
+    size_t qhead_ = 0, drained_ = 0;
+    char* dst_ = nullptr;          // user buffer of the current call
+    std::string derr_;             // first drain-thread error of the current call
+    bool dstop_ = false;
 };
 
 }  // namespace rdc_amd
