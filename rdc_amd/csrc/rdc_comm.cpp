@@ -514,6 +514,16 @@ void Communicator::Check(hipStream_t stream) {
     hip_check(hipStreamSynchronize(stream), "stream sync");
     uint32_t e = 0;
     hip_check(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost), "read error word");
+    RaiseIfError(e);
+}
+
+void Communicator::EnqueueErrorCopy(hipStream_t stream, uint32_t* host_word) {
+    *host_word = 0;
+    if (err_ == nullptr) return;
+    hip_check(hipMemcpyAsync(host_word, err_, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "copy error word");
+}
+
+void Communicator::RaiseIfError(uint32_t e) const {
     if (e != RDC_KERR_NONE) {
         static const char* names[] = {"none", "reduce-scatter wait timed out", "allgather wait timed out",
                                       "broadcast wait timed out", "ring step wait timed out",

@@ -61,6 +61,10 @@ public:
     void Allgather(void* const* bufs, const uint64_t* sizes, hipStream_t stream);
     // waits for `stream`, then reads the device error word; throws on error
     void Check(hipStream_t stream);
+    // split form of Check: enqueue a copy of the error word into `host_word`
+    // (pinned) on `stream`; after the caller synchronises, RaiseIfError(*host_word)
+    void EnqueueErrorCopy(hipStream_t stream, uint32_t* host_word);
+    void RaiseIfError(uint32_t e) const;
 
     int rank() const { return rank_; }
     int size() const { return n_; }

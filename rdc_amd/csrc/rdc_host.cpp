@@ -1,8 +1,10 @@
 // Pipelined host-resident allreduce (see rdc_host.h).
 #include "rdc_host.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <stdexcept>
@@ -22,6 +24,16 @@ int env_int(const char* name, int dflt) {
 }
 constexpr size_t kPieceTarget = (size_t)16 << 20;  // bytes of all chunks' slices per piece
 constexpr size_t kParallelMin = (size_t)1 << 20;   // below this a copy runs on the caller alone
+// RDC_HOST_TRACE=1: per-piece timeline on stderr (diagnostics)
+double trace_now() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+bool tracing() {
+    static const bool on = getenv("RDC_HOST_TRACE") != nullptr;
+    return on;
+}
 }  // namespace
 
 // ---------------------------------------------------------------- CopyPool --
@@ -117,6 +129,8 @@ HostPath::~HostPath() {
         (void)hipEventDestroy(in_done_[i]);
     }
     for (hipEvent_t e : ar_done_) (void)hipEventDestroy(e);
+    if (pin_small_) (void)hipHostFree(pin_small_);
+    if (dev_small_) (void)hipFree(dev_small_);
     if (dev_) (void)hipFree(dev_);
     if (h2d_) (void)hipStreamDestroy(h2d_);
     if (d2h_) (void)hipStreamDestroy(d2h_);
@@ -180,12 +194,16 @@ void HostPath::DrainLoop() {
         std::string err;
         try {
             hip_check(hipSetDevice(device_), "hipSetDevice");
+            const double t0 = tracing() ? trace_now() : 0;
             hip_check(hipEventSynchronize(d.ready), "wait allreduce");
+            const double t1 = tracing() ? trace_now() : 0;
             for (int q = 0; q < d.nslice; ++q)
                 if (d.len[q])
                     hip_check(hipMemcpyAsync(dst + d.off[q], dev_ + d.off[q], d.len[q], hipMemcpyDeviceToHost, d2h_),
                               "D2H");
             hip_check(hipStreamSynchronize(d2h_), "D2H sync");
+            if (tracing())
+                fprintf(stderr, "[host %.3f] drain: waited AR %.3f ms, D2H %.3f ms\n", t1, t1 - t0, trace_now() - t1);
         } catch (const std::exception& e) {
             err = e.what();
         }
@@ -196,6 +214,26 @@ void HostPath::DrainLoop() {
     }
 }
 
+// Small buffers are latency-bound: copy into pinned memory, H2D, allreduce,
+// D2H and the error word all on the communicator's stream, ONE sync.
+void HostPath::AllreduceSmall(Communicator* c, char* h, size_t count, size_t S, int dtype, int op,
+                              hipStream_t comm_stream) {
+    if (!pin_small_) {
+        hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_small_), kSmall + 64, hipHostMallocDefault),
+                  "hipHostMalloc");
+        hip_check(hipMalloc(reinterpret_cast<void**>(&dev_small_), kSmall), "hipMalloc");
+    }
+    uint32_t* err_word = reinterpret_cast<uint32_t*>(pin_small_ + kSmall);
+    memcpy(pin_small_, h, S);
+    hip_check(hipMemcpyAsync(dev_small_, pin_small_, S, hipMemcpyHostToDevice, comm_stream), "H2D");
+    c->Allreduce(dev_small_, count, dtype, op, comm_stream);
+    hip_check(hipMemcpyAsync(pin_small_, dev_small_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
+    c->EnqueueErrorCopy(comm_stream, err_word);
+    hip_check(hipStreamSynchronize(comm_stream), "sync");
+    c->RaiseIfError(*err_word);
+    memcpy(h, pin_small_, S);
+}
+
 void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, int op, hipStream_t comm_stream) {
     const int n = c->size();
     if (n == 1 || count == 0) return;
@@ -203,6 +241,10 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
     const size_t S = count * esz;
     char* h = static_cast<char*>(host);
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    if (S <= kSmall) {
+        AllreduceSmall(c, h, count, S, dtype, op, comm_stream);
+        return;
+    }
 
     int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
     SplitRanges((int64_t)count, n, cb, ce);
@@ -237,9 +279,14 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
                 bytes += d.len[q];
             }
             // the slot's previous H2D has been consumed before we overwrite it
+            const double t0 = tracing() ? trace_now() : 0;
             if (k >= kSlots) hip_check(hipEventSynchronize(in_done_[slot]), "wait H2D slot");
+            const double t1 = tracing() ? trace_now() : 0;
             for (int q = 0; q < n; ++q)
                 if (d.len[q]) Copy(pin_in_[slot] + pos[q], h + d.off[q], d.len[q]);
+            if (tracing())
+                fprintf(stderr, "[host %.3f] piece %d: slot wait %.3f ms, copy-in %.3f ms (%llu B)\n", t0, k, t1 - t0,
+                        trace_now() - t1, (unsigned long long)bytes);
             for (int q = 0; q < n; ++q)
                 if (d.len[q])
                     hip_check(hipMemcpyAsync(dev_ + d.off[q], pin_in_[slot] + pos[q], d.len[q],

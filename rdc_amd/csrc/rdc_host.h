@@ -65,8 +65,15 @@ private:
     void Copy(char* dst, const char* src, size_t bytes);  // parallel memcpy
     void DrainLoop();
 
+    // buffers up to kSmall: one pinned round trip, one synchronisation
+    static constexpr size_t kSmall = (size_t)1 << 20;
+    void AllreduceSmall(Communicator* c, char* host, size_t count, size_t bytes, int dtype, int op,
+                        hipStream_t comm_stream);
+
     int device_;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
+    char* pin_small_ = nullptr;      // kSmall bytes + the error word
+    char* dev_small_ = nullptr;
     hipEvent_t in_done_[kSlots] = {};
     std::vector<hipEvent_t> ar_done_;  // one per piece of the current call
     char* pin_in_[kSlots] = {};

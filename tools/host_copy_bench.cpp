@@ -10,6 +10,9 @@
 #include <string.h>
 #include <time.h>
 
+#include <thread>
+#include <vector>
+
 #define CK(x)                                                                              \
     do {                                                                                   \
         hipError_t e = (x);                                                                \
@@ -78,6 +81,40 @@ int main(int argc, char** argv) {
     t0 = now();
     memcpy(p, h, S);
     rate("host memcpy pageable -> pinned (1 thread)", now() - t0);
+    for (int T : {2, 4, 8}) {
+        t0 = now();
+        std::vector<std::thread> th;
+        for (int i = 0; i < T; ++i)
+            th.emplace_back([&, i] { memcpy(p + S / T * i, h + S / T * i, S / T); });
+        for (auto& x : th) x.join();
+        char what[64];
+        snprintf(what, sizeof(what), "host memcpy pageable -> pinned (%d threads)", T);
+        rate(what, now() - t0);
+    }
+    {   // full duplex: pinned H2D and D2H of S each, concurrently on two streams
+        char* p2;
+        char* d2;
+        CK(hipHostMalloc(&p2, S, hipHostMallocDefault));
+        CK(hipMalloc(&d2, S));
+        hipStream_t s2;
+        CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        for (int rep = 0; rep < 2; ++rep) {
+            t0 = now();
+            CK(hipMemcpyAsync(d, p, S, hipMemcpyHostToDevice, s));
+            CK(hipMemcpyAsync(p2, d2, S, hipMemcpyDeviceToHost, s2));
+            CK(hipStreamSynchronize(s));
+            CK(hipStreamSynchronize(s2));
+            rate("pinned H2D || D2H, 2 streams (S each way)", now() - t0);
+            t0 = now();
+            CK(hipMemcpyAsync(d, p, S, hipMemcpyHostToDevice, s));
+            CK(hipMemcpyAsync(h, d2, S, hipMemcpyDeviceToHost, s2));  // pageable D2H
+            CK(hipStreamSynchronize(s));
+            CK(hipStreamSynchronize(s2));
+            rate("pinned H2D || pageable D2H (S each way)", now() - t0);
+        }
+        CK(hipHostFree(p2));
+        CK(hipFree(d2));
+    }
     CK(hipHostFree(p));
     CK(hipFree(d));
     free(h);
