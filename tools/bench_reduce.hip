@@ -117,6 +117,76 @@ __global__ __launch_bounds__(B) void k_wc(v4u* __restrict__ d, const v4u* __rest
     for (; i < hi; i += 64) ST<true>(d + i, reduce16<RDC_OP_SUM, float>(LD<true, true>(d + i), LD<true, true>(s + i)));
 }
 
+// grid-stride with an XCD-aware block order: hardware dispatches block b to
+// XCD b % 8, so logical block = (b % 8) * (G / 8) + b / 8 gives every XCD one
+// contiguous eighth of each sweep window (G a multiple of 8)
+template <int U, int B>
+__global__ __launch_bounds__(B) void k_gsx(v4u* __restrict__ d, const v4u* __restrict__ s, uint64_t nvec) {
+    const unsigned G = gridDim.x;
+    const unsigned lb = (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8;
+    const uint64_t stride = (uint64_t)G * B;
+    uint64_t i = (uint64_t)lb * B + threadIdx.x;
+    for (; i + (U - 1) * stride < nvec; i += U * stride) {
+        v4u a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = LD<true, true>(d + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) b[u] = LD<true, true>(s + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) ST<true>(d + i + u * stride, reduce16<RDC_OP_SUM, float>(a[u], b[u]));
+    }
+    for (; i < nvec; i += stride) ST<true>(d + i, reduce16<RDC_OP_SUM, float>(LD<true, true>(d + i), LD<true, true>(s + i)));
+}
+
+// grid-stride, loads interleaved d0 s0 d1 s1 (same bytes in flight as k_gs)
+template <int U, int B>
+__global__ __launch_bounds__(B) void k_gsi(v4u* __restrict__ d, const v4u* __restrict__ s, uint64_t nvec) {
+    const uint64_t stride = (uint64_t)gridDim.x * B;
+    uint64_t i = (uint64_t)blockIdx.x * B + threadIdx.x;
+    for (; i + (U - 1) * stride < nvec; i += U * stride) {
+        v4u a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = LD<true, true>(d + i + u * stride);
+            b[u] = LD<true, true>(s + i + u * stride);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) ST<true>(d + i + u * stride, reduce16<RDC_OP_SUM, float>(a[u], b[u]));
+    }
+    for (; i < nvec; i += stride) ST<true>(d + i, reduce16<RDC_OP_SUM, float>(LD<true, true>(d + i), LD<true, true>(s + i)));
+}
+
+// grid-stride, software-pipelined: the next window's loads are issued before
+// this window's stores (2 x U x 32 B in flight per lane)
+template <int U, int B>
+__global__ __launch_bounds__(B) void k_gsp(v4u* __restrict__ d, const v4u* __restrict__ s, uint64_t nvec) {
+    const uint64_t stride = (uint64_t)gridDim.x * B;
+    uint64_t i = (uint64_t)blockIdx.x * B + threadIdx.x;
+    const uint64_t full = nvec / (U * stride) * (U * stride);  // whole windows
+    v4u a[U], b[U];
+    if (i < full) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) { a[u] = LD<true, true>(d + i + u * stride); b[u] = LD<true, true>(s + i + u * stride); }
+    }
+    for (; i < full; i += U * stride) {
+        v4u na[U], nb[U];
+        const uint64_t ni = i + U * stride;
+        const bool more = ni < full;
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) { na[u] = LD<true, true>(d + ni + u * stride); nb[u] = LD<true, true>(s + ni + u * stride); }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) ST<true>(d + i + u * stride, reduce16<RDC_OP_SUM, float>(a[u], b[u]));
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) { a[u] = na[u]; b[u] = nb[u]; }
+        }
+    }
+    for (i = full + (uint64_t)blockIdx.x * B + threadIdx.x; i < nvec; i += stride)
+        ST<true>(d + i, reduce16<RDC_OP_SUM, float>(LD<true, true>(d + i), LD<true, true>(s + i)));
+}
+
 #define CK(x)                                                                  \
     do {                                                                       \
         hipError_t e = (x);                                                    \
@@ -142,6 +212,17 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&s, S));
     CK(hipMemset(d, 0, S));
     CK(hipMemset(s, 0, S));
+    const bool quick = getenv("SWEEP_QUICK") != nullptr;
+    std::vector<Variant> qv = {
+        {"gs U2 nt/nt B256", (KFn)k_gs<2, true, true, 256>, 256},
+        {"gsx U2 B256 (XCD order)", (KFn)k_gsx<2, 256>, 256},
+        {"gsx U4 B256 (XCD order)", (KFn)k_gsx<4, 256>, 256},
+        {"gsi U2 B256 (interleaved)", (KFn)k_gsi<2, 256>, 256},
+        {"gsp U1 B256 (pipelined)", (KFn)k_gsp<1, 256>, 256},
+        {"gsp U2 B256 (pipelined)", (KFn)k_gsp<2, 256>, 256},
+        {"gs U1 nt/nt B512", (KFn)k_gs<1, true, true, 512>, 512},
+        {"gsx U1 B512 (XCD order)", (KFn)k_gsx<1, 512>, 512},
+    };
     std::vector<Variant> vs = {
         {"bc U4 nt/nt B256", (KFn)k_bc<4, true, true, 256>, 256},
         {"bc U4 nt/nt B1024", (KFn)k_bc<4, true, true, 1024>, 1024},
@@ -153,6 +234,7 @@ int main(int argc, char** argv) {
         {"gs U4 nt/nt B1024", (KFn)k_gs<4, true, true, 1024>, 1024},
         {"gs U2 plain B256", (KFn)k_gs<2, false, false, 256>, 256},
     };
+    if (quick) vs = qv;
     const int grids[] = {128, 256, 384, 512, 768, 1024};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -160,6 +242,7 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 2; ++rep)
     for (auto& v : vs) {
         for (int g : grids) {
+            if (quick && g != 256 && g != 512) continue;
             for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(v.fn, dim3(g), dim3(v.block), 0, 0, d, s, nvec);
             CK(hipDeviceSynchronize());
             const int it = 30;
