@@ -493,3 +493,31 @@ def test_mp_coalesced_cfg5_shape():
     for r in range(4):
         got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
         assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), r
+
+
+@pytest.mark.parametrize("algo", ["mesh", "ring", "oneshot"])
+def test_missing_peer_times_out_instead_of_hanging(algo):
+    """Rank 1 never joins: rank 0's launch gives up after RDC_TIMEOUT (device
+    wall clock), every block drains, and RdcCommCheck reports the failure
+    (the reference's TCP ring can hang forever, SURVEY finding 4)."""
+    import ctypes
+    import time
+    import rdc_amd
+    from rdc_amd._lib import _LIB, RdcError
+    assert _LIB.RdcSetParam(b"RDC_TIMEOUT", b"1") == 0
+    try:
+        g = make_group(2, 8 << 20)
+    finally:
+        assert _LIB.RdcSetParam(b"RDC_TIMEOUT", b"30") == 0
+    try:
+        t = torch.ones(100003, dtype=torch.float32, device="cuda")
+        sp = ctypes.c_void_p(g.streams[0].cuda_stream)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        g[0].allreduce(t, rdc_amd.Op.SUM, algo=algo, stream=sp)
+        with pytest.raises(RdcError, match="timed out"):
+            g[0].check(sp)
+        assert time.time() - t0 < 20
+    finally:
+        for c in g:
+            c.destroy()
