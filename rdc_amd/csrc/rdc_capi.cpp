@@ -31,6 +31,7 @@ thread_local std::string g_last_error;
 struct Manager {
     std::recursive_mutex mu;
     bool inited = false;
+    bool env_loaded = false;  // environment parameters applied (RdcSetParam overrides them afterwards)
     int rank = 0, world = 1, device = -1;
     std::string tracker_uri = "127.0.0.1";
     int tracker_port = 29571;
@@ -196,6 +197,7 @@ int RdcInit(int argc, char** argv) {
                                      "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
                                      "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES"};
         for (const char* k : keys) env_param(m, k);
+        m.env_loaded = true;
         for (int i = 0; i < argc; ++i) {
             if (!argv || !argv[i]) continue;
             char name[256], val[256];
@@ -518,8 +520,10 @@ int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes
         // parameters from the environment even without RdcInit
         static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
                                      "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES"};
-        if (!m.inited)
+        if (!m.inited && !m.env_loaded) {
             for (const char* k : keys) env_param(m, k);
+            m.env_loaded = true;
+        }
         CommConfig cfg = m.cfg;
         if (scratch_bytes) cfg.scratch_bytes = scratch_bytes;
         std::vector<Communicator*> out;
