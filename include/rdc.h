@@ -75,6 +75,24 @@ inline void Check(int rc, const char* what) {
 }
 }  // namespace detail
 
+/*! \brief completion of an ISend / IRecv (include/core/work_request.h:240-270).
+ *  Owned by the caller; deleting a pending completion is safe. */
+class WorkCompletion {
+public:
+    explicit WorkCompletion(void* h) : h_(h) {}
+    ~WorkCompletion() { RdcDelWorkCompletion(h_); }
+    WorkCompletion(const WorkCompletion&) = delete;
+    WorkCompletion& operator=(const WorkCompletion&) = delete;
+    /*! \brief block until done; true on success (the reference's Wait) */
+    bool Wait() { return RdcWorkCompletionWait(h_) == 0; }
+    /*! \brief WorkStatus bits: 2 pending, 8 finished, 64 error */
+    int Status() const { return RdcWorkCompletionStatus(h_); }
+    std::string Error() const { return RdcWorkCompletionError(h_); }
+
+private:
+    void* h_;
+};
+
 namespace comm {
 /*! \brief a named communicator (include/comm/communicator.h:41-146) */
 class ICommunicator {
@@ -97,6 +115,35 @@ public:
     /*! \brief bufs[c] holds sizes[c] bytes; bufs[rank] is this rank's data */
     virtual void Allgather(void** bufs, const size_t* sizes) {
         detail::Check(RdcAllgatherOn(handle_, bufs, sizes), "Allgather");
+    }
+    /*! \brief non-blocking point-to-point (communicator.h:69-80); host or device
+     *  memory; messages on one (src, dst) pair match in order, equal sizes */
+    virtual WorkCompletion* ISend(const void* sendaddr, uint64_t size_in_bytes, int dest) {
+        void* wc = nullptr;
+        detail::Check(RdcCommISend(&wc, handle_, sendaddr, size_in_bytes, dest, nullptr), "ISend");
+        return new WorkCompletion(wc);
+    }
+    virtual WorkCompletion* IRecv(void* recvaddr, uint64_t size_in_bytes, int src) {
+        void* wc = nullptr;
+        detail::Check(RdcCommIRecv(&wc, handle_, recvaddr, size_in_bytes, src, nullptr), "IRecv");
+        return new WorkCompletion(wc);
+    }
+    /*! \brief blocking point-to-point (communicator.h:56-67); aborts on failure */
+    virtual void Send(const void* sendaddr, uint64_t size_in_bytes, int dest) {
+        WorkCompletion* w = ISend(sendaddr, size_in_bytes, dest);
+        if (!w->Wait()) {
+            fprintf(stderr, "rdc: Send failed: %s\n", w->Error().c_str());
+            abort();
+        }
+        delete w;
+    }
+    virtual void Recv(void* recvaddr, uint64_t size_in_bytes, int src) {
+        WorkCompletion* w = IRecv(recvaddr, size_in_bytes, src);
+        if (!w->Wait()) {
+            fprintf(stderr, "rdc: Recv failed: %s\n", w->Error().c_str());
+            abort();
+        }
+        delete w;
     }
     int GetRank() const { return RdcCommRank(handle_); }
     int GetWorldSize() const { return RdcCommSize(handle_); }
@@ -151,6 +198,14 @@ inline int GetWorldSize() { return RdcGetWorldSize(); }
 inline bool IsDistributed() { return RdcIsDistributed() != 0; }
 inline void TrackerPrint(const std::string& msg) { RdcTrackerPrint(msg.c_str()); }
 inline void Barrier() { detail::Check(RdcBarrier(), "Barrier"); }
+
+/*! \brief blocking point-to-point on a communicator (include/api.h:10-11, rdc-inl.h:53-66) */
+inline void Send(const void* send_data, uint64_t size, int dest, const std::string& comm_name = kMainCommName) {
+    GetCommunicator(comm_name)->Send(send_data, size, dest);
+}
+inline void Recv(void* recv_data, uint64_t size, int src, const std::string& comm_name = kMainCommName) {
+    GetCommunicator(comm_name)->Recv(recv_data, size, src);
+}
 
 /*! \brief in-place allreduce (include/api.h:62-64, rdc-inl.h:125-135) */
 template <typename OP, typename DType>

@@ -99,6 +99,35 @@ int RdcAllreduceCoalescedOn(void* comm, void** bufs, const size_t* counts, int n
 int RdcNewCommunicator(void** out, const char* name);
 int RdcGetCommunicator(void** out, const char* name);
 
+/* Point-to-point (ICommunicator::ISend/IRecv, include/comm/communicator.h:
+ * 56-80; rdc/comm.py:46-80 binds RdcISend / RdcIRecv / RdcWorkCompletion*).
+ * Buffers are rdc Buffer handles (rdc/buffer.py:34-38: RdcNewBuffer(byref(h),
+ * addr, size, pinned)) over host OR device memory; `pinned` page-locks a host
+ * range (hipHostRegister) for the buffer's lifetime.  Data moves GPU to GPU
+ * over xGMI through the receiver's IPC-mapped slots; messages on one (src,
+ * dst) pair are matched in order and must have equal sizes on both sides.
+ * A request that makes no progress for RDC_TIMEOUT seconds ends in error.
+ * Completion handles are freed with RdcDelWorkCompletion (safe while
+ * pending).  RdcIRecv returns the handle (NULL on failure), as comm.py:73
+ * expects; every other function returns a status code. */
+int RdcNewBuffer(void** out, void* addr, size_t size, int pinned);
+int RdcDelBuffer(void* buf);
+int RdcISend(void** wc, void* comm, void* buf, int dest);
+void* RdcIRecv(void* comm, void* buf, int src);
+/* 0 = finished, 1 = error (RdcWorkCompletionError describes it) */
+int RdcWorkCompletionWait(void* wc);
+/* WorkStatus (include/core/work_request.h:23-30): 2 pending, 8 finished, 64 error */
+int RdcWorkCompletionStatus(void* wc);
+const char* RdcWorkCompletionError(void* wc);
+int RdcDelWorkCompletion(void* wc);
+/* blocking rdc::Send / rdc::Recv on "main" (include/api.h:10-11) */
+int RdcSend(void* buf, size_t size, int dest);
+int RdcRecv(void* buf, size_t size, int src);
+/* raw-pointer forms on `comm`; for device memory the copies start after the
+ * work already queued on `stream` (NULL = default stream) */
+int RdcCommISend(void** wc, void* comm, const void* buf, size_t bytes, int dest, void* stream);
+int RdcCommIRecv(void** wc, void* comm, void* buf, size_t bytes, int src, void* stream);
+
 /* ------------------------------------------------------------------ */
 /* MI355X device-resident extensions                                    */
 /* ------------------------------------------------------------------ */

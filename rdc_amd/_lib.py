@@ -72,6 +72,18 @@ def _load():
                                  ctypes.POINTER(ctypes.c_int)]),
         "RdcPlanFuseGroups": (i, [ctypes.POINTER(sz), i, i, sz, ctypes.POINTER(ctypes.c_int), i,
                                   ctypes.POINTER(ctypes.c_int)]),
+        "RdcNewBuffer": (i, [pvp, vp, sz, i]),
+        "RdcDelBuffer": (i, [vp]),
+        "RdcISend": (i, [pvp, vp, vp, i]),
+        "RdcIRecv": (vp, [vp, vp, i]),
+        "RdcWorkCompletionWait": (i, [vp]),
+        "RdcWorkCompletionStatus": (i, [vp]),
+        "RdcWorkCompletionError": (ctypes.c_char_p, [vp]),
+        "RdcDelWorkCompletion": (i, [vp]),
+        "RdcSend": (i, [vp, sz, i]),
+        "RdcRecv": (i, [vp, sz, i]),
+        "RdcCommISend": (i, [pvp, vp, vp, sz, i, vp]),
+        "RdcCommIRecv": (i, [pvp, vp, vp, sz, i, vp]),
         "RdcSetParam": (i, [ctypes.c_char_p, ctypes.c_char_p]),
         "RdcGetLastError": (ctypes.c_char_p, []),
         "RdcVersion": (ctypes.c_char_p, []),

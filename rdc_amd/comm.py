@@ -4,8 +4,44 @@ multi-rank groups (``init_group``) for driving several GPUs from one process.
 """
 import ctypes
 
-from ._lib import _LIB, check_call
+from ._lib import _LIB, RdcError, check_call
 from . import device as _dev
+from .buffer import Buffer
+
+# WorkStatus (include/core/work_request.h:23-30)
+WS_PENDING, WS_RUNNING, WS_FINISHED, WS_ERROR = 1 << 1, 1 << 2, 1 << 3, 1 << 6
+
+
+class WorkComp(object):
+    """Completion of an isend / irecv (rdc/comm.py:11-33).  Holds the buffer
+    alive until the handle is dropped."""
+    __slots__ = ("handle", "own_handle", "_buf")
+
+    def __init__(self, handle=None, own_handle=True, buf=None):
+        self.handle = handle if handle is not None else ctypes.c_void_p()
+        self.own_handle = own_handle
+        self._buf = buf
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if getattr(self, "own_handle", False) and h:
+            _LIB.RdcDelWorkCompletion(h)
+            self.handle = ctypes.c_void_p()
+
+    def wait(self):
+        """Block until the transfer finished; 0 on success (raises on error)."""
+        rc = _LIB.RdcWorkCompletionWait(self.handle)
+        if rc != 0:
+            raise RdcError(_LIB.RdcWorkCompletionError(self.handle).decode("utf-8", "replace"))
+        return rc
+
+    def status(self):
+        """WorkStatus bits: WS_PENDING, WS_FINISHED or WS_ERROR."""
+        return _LIB.RdcWorkCompletionStatus(self.handle)
+
+
+def _is_tensor(x):
+    return hasattr(x, "data_ptr") and hasattr(x, "is_cuda")
 
 ALGO_AUTO, ALGO_RING, ALGO_MESH, ALGO_ONESHOT = 0, 1, 2, 3
 _ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "mesh": ALGO_MESH, "oneshot": ALGO_ONESHOT}
@@ -86,6 +122,48 @@ class Comm(object):
         s = stream if stream is not None else _dev.current_stream_ptr(tensors[0].device)
         check_call(_LIB.RdcCommAllgather(self.handle, ptrs, sizes, s))
         return tensors
+
+    # ----------------------------------------------------- point-to-point --
+    def isend(self, buf, dest_rank):
+        """Non-blocking send of a Buffer, ndarray, bytes/bytearray or ROCm
+        tensor to ``dest_rank`` (rdc/comm.py:46-63).  A device tensor is sent
+        after the work already queued on torch's current stream."""
+        if _is_tensor(buf) and buf.is_cuda:
+            _dev._check_tensor(buf)
+            wc = WorkComp(buf=buf)
+            check_call(_LIB.RdcCommISend(ctypes.byref(wc.handle), self.handle, ctypes.c_void_p(buf.data_ptr()),
+                                         buf.numel() * buf.element_size(), int(dest_rank),
+                                         _dev.current_stream_ptr(buf.device)))
+            return wc
+        b = buf if isinstance(buf, Buffer) else Buffer(buf)
+        wc = WorkComp(buf=b)
+        check_call(_LIB.RdcISend(ctypes.byref(wc.handle), self.handle, b.handle, int(dest_rank)))
+        return wc
+
+    def irecv(self, buf, src_rank):
+        """Non-blocking receive into a Buffer, ndarray, bytearray or ROCm tensor
+        from ``src_rank`` (rdc/comm.py:65-80)."""
+        if _is_tensor(buf) and buf.is_cuda:
+            _dev._check_tensor(buf)
+            wc = WorkComp(buf=buf)
+            check_call(_LIB.RdcCommIRecv(ctypes.byref(wc.handle), self.handle, ctypes.c_void_p(buf.data_ptr()),
+                                         buf.numel() * buf.element_size(), int(src_rank),
+                                         _dev.current_stream_ptr(buf.device)))
+            return wc
+        b = buf if isinstance(buf, Buffer) else Buffer(buf)
+        h = _LIB.RdcIRecv(self.handle, b.handle, int(src_rank))
+        if not h:
+            raise RdcError(_LIB.RdcGetLastError().decode("utf-8", "replace"))
+        return WorkComp(ctypes.c_void_p(h), buf=b)
+
+    def send(self, buf, dest_rank):
+        """Blocking send (ICommunicator::Send, include/comm/communicator.h:56-62)."""
+        self.isend(buf, dest_rank).wait()
+
+    def recv(self, buf, src_rank):
+        """Blocking receive (ICommunicator::Recv); returns ``buf``."""
+        self.irecv(buf, src_rank).wait()
+        return buf
 
     def check(self, stream=None):
         """Synchronise the stream and raise if a device-side wait failed."""

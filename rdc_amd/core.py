@@ -190,3 +190,17 @@ def allgather(arrays):
     sizes = (ctypes.c_size_t * n)(*[a.nbytes for a in arrays])
     check_call(_LIB.RdcAllgather(ptrs, sizes))
     return arrays
+
+
+def send(buf, dest):
+    """rdc::Send on the main communicator (include/api.h:10, rdc-inl.h:53-62):
+    blocking send of a Buffer / ndarray / bytes / ROCm tensor to rank ``dest``."""
+    from .comm import get_comm
+    get_comm("main").send(buf, dest)
+
+
+def recv(buf, src):
+    """rdc::Recv on the main communicator (include/api.h:11): blocking receive
+    into ``buf`` from rank ``src``; returns ``buf``."""
+    from .comm import get_comm
+    return get_comm("main").recv(buf, src)

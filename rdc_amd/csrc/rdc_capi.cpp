@@ -21,6 +21,7 @@
 #include "rdc_bootstrap.h"
 #include "rdc_comm.h"
 #include "rdc_host.h"
+#include "rdc_p2p.h"
 
 using namespace rdc_amd;
 
@@ -89,6 +90,7 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_ONESHOT_BYTES") m.cfg.oneshot_push_max = parse_unit(val);
     else if (k == "RDC_FUSE_BYTES") m.cfg.fuse_bytes = std::max<size_t>(parse_unit(val), 1);
     else if (k == "RDC_BOOTSTRAP_TIMEOUT") m.bootstrap_timeout_s = atof(val);
+    else if (k == "RDC_P2P_SLOT_BYTES") m.cfg.p2p_slot_bytes = std::max<size_t>(parse_unit(val) / 4096 * 4096, 4096);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
     // to subsystems outside the device path and are accepted silently
 }
@@ -195,7 +197,8 @@ int RdcInit(int argc, char** argv) {
         static const char* keys[] = {"RDC_TRACKER_URI", "RDC_TRACKER_PORT", "RDC_WORLD_SIZE", "rdc_world_size",
                                      "RDC_RANK", "rdc_reduce_ring_mincount", "RDC_DEVICE", "RDC_SCRATCH_BYTES",
                                      "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
-                                     "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES"};
+                                     "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES",
+                                     "RDC_P2P_SLOT_BYTES"};
         for (const char* k : keys) env_param(m, k);
         m.env_loaded = true;
         for (int i = 0; i < argc; ++i) {
@@ -519,7 +522,7 @@ int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes
         if (!comms || !devices) throw std::invalid_argument("rdc: null argument");
         // parameters from the environment even without RdcInit
         static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
-                                     "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES"};
+                                     "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES", "RDC_P2P_SLOT_BYTES"};
         if (!m.inited && !m.env_loaded) {
             for (const char* k : keys) env_param(m, k);
             m.env_loaded = true;
@@ -638,6 +641,120 @@ int RdcPlanFuseGroups(const size_t* counts, int nbuf, int dtype, size_t fuse_byt
         for (int i = 0; i < (int)g.size() && i < max_bounds && bounds_out; ++i) bounds_out[i] = g[(size_t)i];
     });
 }
+
+// ------------------------------------------------------- point-to-point --
+namespace {
+struct BufferH {  // rdc::Buffer (include/transport/buffer.h:15-66): a view, not an owner
+    void* addr = nullptr;
+    size_t size = 0;
+    bool registered = false;  // pinned: hipHostRegister'ed by RdcNewBuffer
+};
+BufferH* as_buffer(void* h) {
+    if (!h) throw std::invalid_argument("rdc: null buffer handle");
+    return static_cast<BufferH*>(h);
+}
+WorkComp* as_wc(void* h) {
+    if (!h) throw std::invalid_argument("rdc: null work completion handle");
+    return static_cast<WorkComp*>(h);
+}
+}  // namespace
+
+int RdcNewBuffer(void** out, void* addr, size_t size, int pinned) {
+    return guard([&] {
+        if (!out) throw std::invalid_argument("rdc: null argument");
+        if (size && !addr) throw std::invalid_argument("rdc: null buffer address");
+        std::unique_ptr<BufferH> b(new BufferH());
+        b->addr = addr;
+        b->size = size;
+        if (pinned && size && !is_device_pointer(addr)) {
+            // a performance hint: an unregistrable range stays pageable
+            b->registered = hipHostRegister(addr, size, hipHostRegisterDefault) == hipSuccess;
+            (void)hipGetLastError();
+        }
+        *out = b.release();
+    });
+}
+
+int RdcDelBuffer(void* buf) {
+    return guard([&] {
+        if (!buf) return;
+        BufferH* b = static_cast<BufferH*>(buf);
+        if (b->registered) (void)hipHostUnregister(b->addr);
+        delete b;
+    });
+}
+
+int RdcCommISend(void** wc, void* comm, const void* buf, size_t bytes, int dest, void* stream) {
+    return guard([&] {
+        if (!wc) throw std::invalid_argument("rdc: null argument");
+        *wc = as_comm(comm)->ISend(buf, bytes, dest, static_cast<hipStream_t>(stream));
+    });
+}
+
+int RdcCommIRecv(void** wc, void* comm, void* buf, size_t bytes, int src, void* stream) {
+    return guard([&] {
+        if (!wc) throw std::invalid_argument("rdc: null argument");
+        *wc = as_comm(comm)->IRecv(buf, bytes, src, static_cast<hipStream_t>(stream));
+    });
+}
+
+int RdcISend(void** wc, void* comm, void* buf, int dest) {
+    return guard([&] {
+        if (!wc) throw std::invalid_argument("rdc: null argument");
+        BufferH* b = as_buffer(buf);
+        *wc = as_comm(comm)->ISend(b->addr, b->size, dest, nullptr);
+    });
+}
+
+void* RdcIRecv(void* comm, void* buf, int src) {
+    void* wc = nullptr;
+    guard([&] {
+        BufferH* b = as_buffer(buf);
+        wc = as_comm(comm)->IRecv(b->addr, b->size, src, nullptr);
+    });
+    return wc;
+}
+
+int RdcWorkCompletionWait(void* wc) {
+    int rc = 1;
+    if (guard([&] { rc = as_wc(wc)->Wait(); }) != 0) return 1;
+    if (rc != 0) g_last_error = static_cast<WorkComp*>(wc)->error();
+    return rc;
+}
+
+int RdcWorkCompletionStatus(void* wc) { return wc ? static_cast<WorkComp*>(wc)->Status() : RDC_WS_ERROR; }
+
+const char* RdcWorkCompletionError(void* wc) {
+    thread_local std::string s;
+    s = wc ? static_cast<WorkComp*>(wc)->error() : std::string("rdc: null work completion handle");
+    return s.c_str();
+}
+
+int RdcDelWorkCompletion(void* wc) {
+    return guard([&] {
+        if (wc) static_cast<WorkComp*>(wc)->Release();
+    });
+}
+
+namespace {
+void p2p_sync(bool send, void* buf, size_t size, int peer) {
+    Manager& m = M();
+    Communicator* c;
+    {
+        std::lock_guard<std::recursive_mutex> lk(m.mu);
+        require_init(m);
+        c = get_comm(m, "main", true);
+    }
+    WorkComp* w = send ? c->ISend(buf, size, peer, nullptr) : c->IRecv(buf, size, peer, nullptr);
+    const int rc = w->Wait();
+    const std::string err = rc ? w->error() : std::string();
+    w->Release();
+    if (rc) throw std::runtime_error(err);
+}
+}  // namespace
+
+int RdcSend(void* buf, size_t size, int dest) { return guard([&] { p2p_sync(true, buf, size, dest); }); }
+int RdcRecv(void* buf, size_t size, int src) { return guard([&] { p2p_sync(false, buf, size, src); }); }
 
 int RdcSetParam(const char* name, const char* value) {
     Manager& m = M();

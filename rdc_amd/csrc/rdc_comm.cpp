@@ -4,13 +4,18 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <stdexcept>
 #include <string>
 
 #include "rdc_kernels.h"
+#include "rdc_p2p.h"
 #include "rdc_plan.h"
 
 namespace rdc_amd {
@@ -62,16 +67,56 @@ struct PeerInfo {
     hipIpcMemHandle_t scratch;
     hipIpcMemHandle_t ag;
     hipIpcMemHandle_t flags;
+    hipIpcMemHandle_t p2p;
     int32_t device;
     int32_t pid;
     int32_t alloc_kind;
     int32_t pad;
     uint64_t slot_bytes;
     uint64_t max_tiles;
+    uint64_t p2p_slot_bytes;
     char host[64];
 };
 
+// The point-to-point control block (rdc_p2p.h) in POSIX shared memory: rank 0
+// creates it, every rank maps it, rank 0 unlinks the name once all mapped.
+std::shared_ptr<P2PCtl> map_p2p_ctl(Bootstrap* bs) {
+    char name[64];
+    memset(name, 0, sizeof(name));
+    int fd = -1;
+    std::string err;
+    if (bs->rank() == 0) {
+        static std::atomic<int> counter{0};
+        snprintf(name, sizeof(name), "/rdc_p2p_%d_%d", (int)getpid(), counter++);
+        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0 || ftruncate(fd, sizeof(P2PCtl)) != 0) {
+            err = std::string("rdc: cannot create shared memory ") + name + ": " + strerror(errno);
+            if (fd >= 0) {
+                close(fd);
+                shm_unlink(name);
+            }
+            fd = -1;
+            memset(name, 0, sizeof(name));  // tells the others
+        }
+    }
+    bs->broadcast(name, sizeof(name), 0);
+    if (!name[0]) throw std::runtime_error(err.empty() ? "rdc: rank 0 could not create the p2p control block" : err);
+    if (bs->rank() != 0) {
+        fd = shm_open(name, O_RDWR, 0600);
+        if (fd < 0) throw std::runtime_error(std::string("rdc: cannot open shared memory ") + name + ": " + strerror(errno));
+    }
+    void* p = mmap(nullptr, sizeof(P2PCtl), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) throw std::runtime_error(std::string("rdc: cannot map shared memory: ") + strerror(errno));
+    std::shared_ptr<P2PCtl> ctl(static_cast<P2PCtl*>(p), [](P2PCtl* q) { munmap(q, sizeof(P2PCtl)); });
+    bs->barrier();
+    if (bs->rank() == 0) shm_unlink(name);
+    return ctl;
+}
+
 }  // namespace
+
+Communicator::Communicator() {}
 
 void Communicator::AllocLocal() {
     hip_check(hipSetDevice(device_), "hipSetDevice");
@@ -84,7 +129,9 @@ void Communicator::AllocLocal() {
     scratch_ = static_cast<char*>(alloc_shared(region_bytes_, &k1));
     scratch_ag_ = static_cast<char*>(alloc_shared(region_bytes_, &k3));
     flags_ = static_cast<uint32_t*>(alloc_shared(flag_bytes_, &k2));
-    alloc_kind_ = std::max(std::max(k1, k2), k3);
+    int k4 = 0;
+    p2p_ = static_cast<char*>(alloc_shared((size_t)n_ * kP2PSlots * cfg_.p2p_slot_bytes, &k4));
+    alloc_kind_ = std::max(std::max(k1, k2), std::max(k3, k4));
     // [0] error word, [16] block arrival counter, [32] completed-launch counter
     hip_check(hipMalloc(&err_, 256), "hipMalloc err");
     hip_check(hipMemset(flags_, 0, flag_bytes_), "memset flags");
@@ -100,6 +147,7 @@ void Communicator::AllocLocal() {
     peer_scratch_[rank_] = scratch_;
     peer_ag_[rank_] = scratch_ag_;
     peer_flags_[rank_] = flags_;
+    peer_p2p_[rank_] = p2p_;
 }
 
 Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int device, const CommConfig& cfg) {
@@ -123,6 +171,8 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     hip_check(hipIpcGetMemHandle(&mine.scratch, c->scratch_), "hipIpcGetMemHandle(scratch)");
     hip_check(hipIpcGetMemHandle(&mine.ag, c->scratch_ag_), "hipIpcGetMemHandle(ag)");
     hip_check(hipIpcGetMemHandle(&mine.flags, c->flags_), "hipIpcGetMemHandle(flags)");
+    hip_check(hipIpcGetMemHandle(&mine.p2p, c->p2p_), "hipIpcGetMemHandle(p2p)");
+    mine.p2p_slot_bytes = cfg.p2p_slot_bytes;
     mine.device = device;
     mine.pid = (int32_t)getpid();
     mine.alloc_kind = c->alloc_kind_;
@@ -134,7 +184,8 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     bs->allgather(&mine, sizeof(mine), all.data());
     dbg("[rdc %d] %s\n", c->rank_, "handles exchanged");
     for (int p = 0; p < c->n_; ++p) {
-        if (all[(size_t)p].slot_bytes != mine.slot_bytes || all[(size_t)p].max_tiles != mine.max_tiles)
+        if (all[(size_t)p].slot_bytes != mine.slot_bytes || all[(size_t)p].max_tiles != mine.max_tiles ||
+            all[(size_t)p].p2p_slot_bytes != mine.p2p_slot_bytes)
             throw std::runtime_error("rdc: ranks disagree on scratch size (set RDC_SCRATCH_BYTES identically)");
         if (strncmp(all[(size_t)p].host, mine.host, sizeof(mine.host)) != 0)
             throw std::runtime_error("rdc: xGMI path needs every rank on one node (rank " + std::to_string(p) +
@@ -166,7 +217,11 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
                   "hipIpcOpenMemHandle(flags)");
         c->peer_scratch_[p] = static_cast<char*>(ps);
         c->peer_flags_[p] = static_cast<uint32_t*>(pf);
+        void* pp = nullptr;
+        hip_check(hipIpcOpenMemHandle(&pp, all[(size_t)p].p2p, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(p2p)");
+        c->peer_p2p_[p] = static_cast<char*>(pp);
     }
+    c->p2p_ctl_ = map_p2p_ctl(bs);
     dbg("[rdc %d] %s\n", c->rank_, "peers mapped");
     c->owns_peers_ipc_ = true;
     bs->barrier();
@@ -187,11 +242,14 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
         c->AllocLocal();
         cs.push_back(std::move(c));
     }
+    std::shared_ptr<P2PCtl> ctl = std::make_shared<P2PCtl>();  // value-initialised: all words 0
     for (int i = 0; i < n; ++i) {
+        cs[(size_t)i]->p2p_ctl_ = ctl;
         for (int j = 0; j < n; ++j) {
             cs[(size_t)i]->peer_scratch_[j] = cs[(size_t)j]->scratch_;
             cs[(size_t)i]->peer_ag_[j] = cs[(size_t)j]->scratch_ag_;
             cs[(size_t)i]->peer_flags_[j] = cs[(size_t)j]->flags_;
+            cs[(size_t)i]->peer_p2p_[j] = cs[(size_t)j]->p2p_;
             if (devices[i] != devices[j]) {
                 int can = 0;
                 (void)hipSetDevice(devices[i]);
@@ -207,6 +265,7 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
 
 Communicator::~Communicator() {
     if (n_ == 1 && scratch_ == nullptr) return;  // trivial communicator
+    p2p_engine_.reset();  // joins the progress thread; pending requests end in error
     (void)hipSetDevice(device_);
     (void)hipDeviceSynchronize();
     if (owns_peers_ipc_ && bs_) {
@@ -219,6 +278,7 @@ Communicator::~Communicator() {
                 if (peer_scratch_[p]) (void)hipIpcCloseMemHandle(peer_scratch_[p]);
                 if (peer_ag_[p]) (void)hipIpcCloseMemHandle(peer_ag_[p]);
                 if (peer_flags_[p]) (void)hipIpcCloseMemHandle(peer_flags_[p]);
+                if (peer_p2p_[p]) (void)hipIpcCloseMemHandle(peer_p2p_[p]);
             }
         try {
             bs_->barrier();  // every importer closed its mapping
@@ -230,7 +290,25 @@ Communicator::~Communicator() {
     if (scratch_) (void)hipFree(scratch_);
     if (scratch_ag_) (void)hipFree(scratch_ag_);
     if (flags_) (void)hipFree(flags_);
+    if (p2p_) (void)hipFree(p2p_);
     if (err_) (void)hipFree(err_);
+}
+
+P2PEngine* Communicator::P2P() {
+    std::lock_guard<std::mutex> lk(p2p_mu_);
+    if (n_ == 1 || !p2p_) throw std::runtime_error("rdc: point-to-point needs a communicator of 2 or more ranks");
+    if (!p2p_engine_)
+        p2p_engine_.reset(new P2PEngine(rank_, n_, device_, cfg_.p2p_slot_bytes, p2p_, peer_p2p_, p2p_ctl_.get(),
+                                        cfg_.timeout_s));
+    return p2p_engine_.get();
+}
+
+WorkComp* Communicator::ISend(const void* buf, size_t bytes, int dest, hipStream_t after) {
+    return P2P()->ISend(buf, bytes, dest, after);
+}
+
+WorkComp* Communicator::IRecv(void* buf, size_t bytes, int src, hipStream_t after) {
+    return P2P()->IRecv(buf, bytes, src, after);
 }
 
 int Communicator::PickAlgo(int algo) const {

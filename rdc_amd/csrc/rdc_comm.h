@@ -14,6 +14,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <map>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <vector>
@@ -32,9 +33,13 @@ struct CommConfig {
     double timeout_s = 60.0;                 // device-side wait limit
     size_t oneshot_push_max = (size_t)1 << 20;  // auto picks one-shot when (n-1) x bytes <= this
     size_t fuse_bytes = (size_t)256 << 20;      // coalesced allreduce: data bytes per fusion group
+    size_t p2p_slot_bytes = (size_t)4 << 20;    // Send/Recv: piece size (2 slots per ordered rank pair)
 };
 
 struct KernelSet;
+struct P2PCtl;
+class P2PEngine;
+class WorkComp;
 
 class Communicator {
 public:
@@ -65,6 +70,10 @@ public:
     // (pinned) on `stream`; after the caller synchronises, RaiseIfError(*host_word)
     void EnqueueErrorCopy(hipStream_t stream, uint32_t* host_word);
     void RaiseIfError(uint32_t e) const;
+    // point-to-point (rdc_p2p.h): bytes of buf to / from one peer, matched in
+    // order per pair; device copies start after the work queued on `after`
+    WorkComp* ISend(const void* buf, size_t bytes, int dest, hipStream_t after);
+    WorkComp* IRecv(void* buf, size_t bytes, int src, hipStream_t after);
 
     int rank() const { return rank_; }
     int size() const { return n_; }
@@ -78,7 +87,7 @@ public:
     int max_blocks() const;
 
 private:
-    Communicator() {}
+    Communicator();
     void AllocLocal();
     void FillArgsCommon(CollArgs* a) const;
     int PickAlgo(int algo) const;
@@ -118,6 +127,14 @@ private:
     uint64_t pack_tick_ = 0;
     char* image_ = nullptr;         // coalesced staging image (local HBM)
     uint64_t image_bytes_ = 0;
+    // point-to-point: slot region [n senders][kP2PSlots] x p2p_slot_bytes (uncached, IPC-exported),
+    // a control block shared by the group (POSIX shm across processes), engine started on first use
+    P2PEngine* P2P();
+    char* p2p_ = nullptr;
+    char* peer_p2p_[RDC_MAX_RANKS] = {};
+    std::shared_ptr<P2PCtl> p2p_ctl_;
+    std::unique_ptr<P2PEngine> p2p_engine_;
+    std::mutex p2p_mu_;
 };
 
 // op::Reducer<OP,DType> on device: dst = OP(dst, src) element-wise

@@ -20,6 +20,8 @@ hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s);
 hipError_t launch_allgather(const CollArgs& a, int grid, hipStream_t s);
 // coalesced allreduce: units[i].buf = user address; unpack = image -> buffers
 hipError_t launch_pack(const PackUnit* units, int nunits, char* image, int unpack, int grid, hipStream_t s);
+// plain device copy (dst may be IPC-mapped peer memory); never waits
+hipError_t launch_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s);
 hipError_t launch_fill(void* buf, uint64_t count, int dtype, uint64_t seed, int rank, hipStream_t s);
 
 }  // namespace rdc_amd

@@ -83,6 +83,15 @@ __global__ __launch_bounds__(kBlock) void k_pack(const PackUnit* __restrict__ un
     }
 }
 
+// ============================================================ p2p copy ===
+// Point-to-point pieces (rdc_p2p.cpp): a plain copy, 64 KiB per block step;
+// dst may be a peer's IPC-mapped slot (remote stores over xGMI).  Never waits.
+__global__ __launch_bounds__(kBlock) void k_copy(char* __restrict__ dst, const char* __restrict__ src, uint64_t bytes) {
+    constexpr uint64_t kStep = 64 << 10;
+    for (uint64_t off = (uint64_t)blockIdx.x * kStep; off < bytes; off += (uint64_t)gridDim.x * kStep)
+        block_copy(dst + off, src + off, bytes - off < kStep ? bytes - off : kStep);
+}
+
 // ================================================================= fill ===
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -141,6 +150,14 @@ hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s) {
 hipError_t launch_pack(const PackUnit* units, int nunits, char* image, int unpack, int grid, hipStream_t s) {
     if (nunits <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_pack, dim3(grid), dim3(kBlock), 0, s, units, nunits, image, unpack);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    uint64_t grid = (bytes + (64 << 10) - 1) >> 16;
+    if (grid > 128) grid = 128;
+    hipLaunchKernelGGL(k_copy, dim3((unsigned)grid), dim3(kBlock), 0, s, (char*)dst, (const char*)src, bytes);
     return hipGetLastError();
 }
 

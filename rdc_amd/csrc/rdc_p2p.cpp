@@ -1,0 +1,300 @@
+// Point-to-point engine (see rdc_p2p.h).
+#include "rdc_p2p.h"
+
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <stdexcept>
+
+#include "rdc_kernels.h"
+
+namespace rdc_amd {
+
+namespace {
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("rdc p2p: ") + what + ": " + hipGetErrorString(e));
+}
+bool is_host(const void* p) {
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;
+    }
+    return !(a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged);
+}
+}  // namespace
+
+// ---------------------------------------------------------------- WorkComp --
+int WorkComp::Wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return status_.load() == RDC_WS_FINISHED || status_.load() == RDC_WS_ERROR; });
+    return status_.load() == RDC_WS_FINISHED ? 0 : 1;
+}
+
+std::string WorkComp::error() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return err_;
+}
+
+void WorkComp::Finish(int status, const std::string& err) {
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        err_ = err;
+        status_.store(status);
+        cv_.notify_all();
+    }
+    Release();  // the engine's reference
+}
+
+void WorkComp::Release() {
+    if (refs_.fetch_sub(1) == 1) delete this;
+}
+
+// --------------------------------------------------------------- P2PEngine --
+P2PEngine::P2PEngine(int rank, int n, int device, size_t slot_bytes, char* local, char* const* peers, P2PCtl* ctl,
+                     double timeout_s)
+    : rank_(rank), n_(n), device_(device), slot_bytes_(slot_bytes), timeout_s_(timeout_s), local_(local), ctl_(ctl) {
+    for (int p = 0; p < RDC_MAX_RANKS; ++p) peers_[p] = p < n ? peers[p] : nullptr;
+    th_ = std::thread([this] { Loop(); });
+}
+
+P2PEngine::~P2PEngine() {
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+    (void)hipSetDevice(device_);
+    for (int p = 0; p < n_; ++p) {
+        for (Lane* L : {&send_[p], &recv_[p]}) {
+            if (L->stream) (void)hipStreamSynchronize(L->stream);
+            Fail(*L, "rdc p2p: communicator destroyed with the request pending");
+            if (L->stream) (void)hipStreamDestroy(L->stream);
+            if (L->bounce) (void)hipFree(L->bounce);
+        }
+    }
+    for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
+}
+
+WorkComp* P2PEngine::Post(Lane& L, char* buf, size_t bytes, hipStream_t after) {
+    if (bytes && !buf) throw std::invalid_argument("rdc p2p: null buffer");
+    WorkComp* wc = new WorkComp();
+    if (bytes == 0) {
+        wc->Finish(RDC_WS_FINISHED, "");
+        return wc;
+    }
+    Req r;
+    r.wc = wc;
+    r.buf = buf;
+    r.bytes = bytes;
+    r.host = is_host(buf);
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!r.host) {
+            // order the engine's copies after the caller's queued work on `after`
+            (void)hipSetDevice(device_);
+            r.ready = Event();
+            if (hipEventRecord(r.ready, after) != hipSuccess) {
+                (void)hipGetLastError();
+                free_events_.push_back(r.ready);
+                delete wc;
+                throw std::runtime_error("rdc p2p: cannot record the caller's stream");
+            }
+        }
+        if (L.q.empty()) L.last = std::chrono::steady_clock::now();
+        L.q.push_back(std::move(r));
+        ++pending_;
+    }
+    cv_.notify_all();
+    return wc;
+}
+
+WorkComp* P2PEngine::ISend(const void* buf, size_t bytes, int dest, hipStream_t after) {
+    if (dest < 0 || dest >= n_ || dest == rank_) throw std::invalid_argument("rdc p2p: bad destination rank");
+    return Post(send_[dest], const_cast<char*>(static_cast<const char*>(buf)), bytes, after);
+}
+
+WorkComp* P2PEngine::IRecv(void* buf, size_t bytes, int src, hipStream_t after) {
+    if (src < 0 || src >= n_ || src == rank_) throw std::invalid_argument("rdc p2p: bad source rank");
+    return Post(recv_[src], static_cast<char*>(buf), bytes, after);
+}
+
+hipEvent_t P2PEngine::Event() {
+    if (!free_events_.empty()) {
+        hipEvent_t e = free_events_.back();
+        free_events_.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+    return e;
+}
+
+void P2PEngine::Fail(Lane& L, const std::string& err) {
+    for (Req& r : L.q) {
+        for (auto& e : r.inflight) free_events_.push_back(e.first);
+        if (r.ready) free_events_.push_back(r.ready);
+        r.wc->Finish(RDC_WS_ERROR, err);
+        --pending_;
+    }
+    L.q.clear();
+}
+
+// the request's first piece waits for the caller's stream
+void P2PEngine::Ready(Lane& L, Req& r) {
+    if (!L.stream) hip_check(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking), "stream");
+    if (r.ready) {
+        hip_check(hipStreamWaitEvent(L.stream, r.ready, 0), "stream wait");
+        free_events_.push_back(r.ready);  // the wait captured the event's state
+        r.ready = nullptr;
+    }
+}
+
+// retire finished pieces of the front requests in stream order; `word`
+// (posted for a send lane, consumed for a recv lane) publishes the count
+bool P2PEngine::Complete(Lane& L, std::atomic<uint64_t>& word) {
+    bool moved = false;
+    while (!L.q.empty()) {
+        Req& r = L.q.front();
+        while (!r.inflight.empty()) {
+            const hipError_t q = hipEventQuery(r.inflight.front().first);
+            if (q == hipErrorNotReady) break;
+            if (q != hipSuccess) hip_check(q, "copy");
+            free_events_.push_back(r.inflight.front().first);
+            r.done += r.inflight.front().second;
+            r.inflight.pop_front();
+            ++L.seq_done;
+            word.store(L.seq_done, std::memory_order_release);
+            moved = true;
+        }
+        if (r.done < r.bytes) break;
+        r.wc->Finish(RDC_WS_FINISHED, "");
+        L.q.pop_front();
+        --pending_;
+        moved = true;
+    }
+    return moved;
+}
+
+// Sender: piece seq goes to slot (seq-1) % kP2PSlots of the peer's region
+// row for this rank once the peer consumed piece seq - kP2PSlots.
+bool P2PEngine::StepSend(int dest, Lane& L) {
+    bool moved = Complete(L, ctl_->posted[rank_][dest].v);
+    for (Req& r : L.q) {
+        while (r.issued < r.bytes) {
+            const uint64_t seq = L.seq_issued + 1;
+            if (seq > (uint64_t)kP2PSlots &&
+                ctl_->consumed[rank_][dest].v.load(std::memory_order_acquire) < seq - kP2PSlots)
+                return moved;
+            const int s = (int)((seq - 1) % kP2PSlots);
+            const size_t len = std::min(slot_bytes_, r.bytes - r.issued);
+            Ready(L, r);
+            const char* src = r.buf + r.issued;
+            if (r.host) {
+                if (!L.bounce) hip_check(hipMalloc(&L.bounce, slot_bytes_ * kP2PSlots), "hipMalloc bounce");
+                hip_check(hipMemcpyAsync(L.bounce + (size_t)s * slot_bytes_, src, len, hipMemcpyHostToDevice, L.stream),
+                          "H2D");
+                src = L.bounce + (size_t)s * slot_bytes_;
+            }
+            char* dst = peers_[dest] + ((size_t)rank_ * kP2PSlots + s) * slot_bytes_;
+            ctl_->len[rank_][dest][s].v.store(len, std::memory_order_relaxed);  // published by posted's release
+            hip_check(launch_copy(dst, src, len, L.stream), "launch copy");
+            hipEvent_t e = Event();
+            hip_check(hipEventRecord(e, L.stream), "record");
+            r.inflight.emplace_back(e, len);
+            r.issued += len;
+            L.seq_issued = seq;
+            moved = true;
+        }
+    }
+    return moved;
+}
+
+// Receiver: piece seq is readable once posted >= seq; after the copy out,
+// consumed = seq frees the slot for the sender.
+bool P2PEngine::StepRecv(int src, Lane& L) {
+    bool moved = Complete(L, ctl_->consumed[src][rank_].v);
+    for (Req& r : L.q) {
+        while (r.issued < r.bytes) {
+            const uint64_t seq = L.seq_issued + 1;
+            if (ctl_->posted[src][rank_].v.load(std::memory_order_acquire) < seq) return moved;
+            const int s = (int)((seq - 1) % kP2PSlots);
+            const size_t len = std::min(slot_bytes_, r.bytes - r.issued);
+            const size_t sent = ctl_->len[src][rank_][s].v.load(std::memory_order_relaxed);
+            if (sent != len) {
+                Fail(L, "rdc p2p: message size mismatch with rank " + std::to_string(src) + " (piece of " +
+                            std::to_string(sent) + " B sent, " + std::to_string(len) + " B expected)");
+                return true;
+            }
+            Ready(L, r);
+            const char* from = local_ + ((size_t)src * kP2PSlots + s) * slot_bytes_;
+            char* to = r.buf + r.issued;
+            if (r.host)
+                hip_check(hipMemcpyAsync(to, from, len, hipMemcpyDeviceToHost, L.stream), "D2H");
+            else
+                hip_check(launch_copy(to, from, len, L.stream), "launch copy");
+            hipEvent_t e = Event();
+            hip_check(hipEventRecord(e, L.stream), "record");
+            r.inflight.emplace_back(e, len);
+            r.issued += len;
+            L.seq_issued = seq;
+            moved = true;
+        }
+    }
+    return moved;
+}
+
+bool P2PEngine::Progress() {
+    bool moved = false;
+    const auto now = std::chrono::steady_clock::now();
+    for (int p = 0; p < n_; ++p) {
+        if (p == rank_) continue;
+        for (int dir = 0; dir < 2; ++dir) {
+            Lane& L = dir == 0 ? send_[p] : recv_[p];
+            if (L.q.empty()) continue;
+            bool m = false;
+            try {
+                m = dir == 0 ? StepSend(p, L) : StepRecv(p, L);
+            } catch (const std::exception& e) {
+                Fail(L, e.what());
+                m = true;
+            }
+            if (m) {
+                L.last = now;
+                moved = true;
+            } else if (std::chrono::duration<double>(now - L.last).count() > timeout_s_) {
+                Fail(L, std::string("rdc p2p: ") + (dir == 0 ? "send to" : "receive from") + " rank " +
+                            std::to_string(p) + " made no progress for " + std::to_string(timeout_s_) + " s");
+                moved = true;
+            }
+        }
+    }
+    return moved;
+}
+
+void P2PEngine::Loop() {
+    (void)hipSetDevice(device_);
+    std::unique_lock<std::mutex> lk(mu_);
+    int idle = 0;
+    while (!stop_) {
+        if (pending_ == 0) {
+            cv_.wait(lk, [&] { return stop_ || pending_ > 0; });
+            idle = 0;
+            continue;
+        }
+        if (Progress()) {
+            idle = 0;
+            continue;
+        }
+        // nothing moved: back off (yield briefly, then sleep up to 50 us)
+        lk.unlock();
+        if (++idle < 64) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(std::min(50, idle / 64)));
+        lk.lock();
+    }
+}
+
+}  // namespace rdc_amd

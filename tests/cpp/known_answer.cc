@@ -76,6 +76,32 @@ int main(int argc, char* argv[]) {
                     return fail(op == 0 ? "coalesced sum" : "coalesced max", i, rounds[(size_t)k][(size_t)i], want);
             }
     }
+    // test/sendrecv.cc: rank 0 sends "hello world %u " to rank 1, 20 times
+    for (int i = 0; i < 20 && W > 1; ++i) {
+        char str[32];
+        const int len = snprintf(str, sizeof(str), "hello world %u ", (unsigned)i);
+        if (R == 0) {
+            rdc::Send(str, (uint64_t)len, 1);
+        } else if (R == 1) {
+            char s[32] = {0};
+            rdc::Recv(s, (uint64_t)len, 0);
+            if (strncmp(s, str, (size_t)len) != 0) return fail("sendrecv", i, s[0], str[0]);
+        }
+    }
+    // ring of non-blocking exchanges (ISend to next, IRecv from prev)
+    if (W > 1) {
+        std::vector<int> out((size_t)N), in((size_t)N, -1);
+        for (int i = 0; i < N; ++i) out[(size_t)i] = R * 1000003 + i;
+        rdc::comm::ICommunicator* c = rdc::GetCommunicator();
+        rdc::WorkCompletion* ws = c->ISend(out.data(), (uint64_t)N * sizeof(int), (R + 1) % W);
+        rdc::WorkCompletion* wr = c->IRecv(in.data(), (uint64_t)N * sizeof(int), (R - 1 + W) % W);
+        if (!ws->Wait() || !wr->Wait()) return fail("isend/irecv", 0, 0, 0);
+        delete ws;
+        delete wr;
+        const int prev = (R - 1 + W) % W;
+        for (int i = 0; i < N; ++i)
+            if (in[(size_t)i] != prev * 1000003 + i) return fail("isend/irecv ring", i, in[(size_t)i], prev * 1000003 + i);
+    }
     printf("rank %d: known-answer OK (world %d, N %d)\n", R, W, N);
     rdc::Finalize();
     return 0;

@@ -37,16 +37,39 @@ def test_reference_python_callers_are_covered():
     """Every _LIB.Rdc* name the reference's Python package calls for this path
     exists in the C ABI (rdc/core.py, rdc/comm.py)."""
     needed = {"RdcInit", "RdcFinalize", "RdcGetRank", "RdcGetWorldSize", "RdcTrackerPrint",
-              "RdcGetProcessorName", "RdcBroadcast", "RdcAllreduce", "RdcNewCommunicator", "RdcGetCommunicator"}
+              "RdcGetProcessorName", "RdcBroadcast", "RdcAllreduce", "RdcNewCommunicator", "RdcGetCommunicator",
+              # rdc/comm.py:25-76 (point-to-point) and rdc/buffer.py:34-38
+              "RdcISend", "RdcIRecv", "RdcWorkCompletionWait", "RdcWorkCompletionStatus", "RdcDelWorkCompletion",
+              "RdcNewBuffer", "RdcDelBuffer"}
     ref = "/root/reference/rdc"
     if os.path.isdir(ref):  # read as text only
         called = set()
-        for f in ("core.py", "comm.py"):
+        for f in ("core.py", "comm.py", "buffer.py"):
             called |= set(re.findall(r"_LIB\.(Rdc\w+)", open(os.path.join(ref, f)).read()))
-        needed |= called & {"RdcInit", "RdcFinalize", "RdcGetRank", "RdcGetWorldSize", "RdcTrackerPrint",
-                            "RdcGetProcessorName", "RdcBroadcast", "RdcAllreduce", "RdcNewCommunicator",
-                            "RdcGetCommunicator"}
+        # checkpointing (RdcCheckPoint / RdcLoadCheckPoint / RdcVersionNumber) and
+        # RdcEnvGetIntEnv are outside the allreduce path (DESIGN.md §7)
+        out_of_scope = {"RdcCheckPoint", "RdcLoadCheckPoint", "RdcVersionNumber", "RdcEnvGetIntEnv"}
+        assert called - out_of_scope <= set(declared_symbols())
     assert needed <= set(declared_symbols())
+
+
+def test_buffer_and_workcomp_host_side():
+    """rdc.Buffer over ndarray / bytes / bytearray / addr+size (rdc/buffer.py,
+    pytest/buffer.py, pytest/comm.py) and the WorkComp status constants; no GPU."""
+    out = run_py(
+        "import numpy as np, ctypes, rdc_amd\n"
+        "b = rdc_amd.Buffer(b'hello'); assert b.bytes() == b'hello' and len(b) == 5\n"
+        "a = np.random.random_sample(200).astype(np.float32); B = rdc_amd.Buffer(a)\n"
+        "assert np.array_equal(np.array(B), a) and B.size == 800\n"
+        "ba = bytearray(b'abc'); C = rdc_amd.Buffer(ba); ba[0] = 120; assert C.bytes() == b'xbc'\n"
+        "D = rdc_amd.Buffer(addr=a.ctypes.data, size=8); assert np.array_equal(D.to_numpy().view(np.float32), a[:2])\n"
+        "E = rdc_amd.Buffer(b'')\n"
+        "assert (rdc_amd.WS_PENDING, rdc_amd.WS_FINISHED, rdc_amd.WS_ERROR) == (2, 8, 64)\n"
+        "from rdc_amd._lib import _LIB\n"
+        "assert _LIB.RdcWorkCompletionStatus(None) == 64\n"
+        "assert _LIB.RdcIRecv(None, B.handle, 1) is None and b'null communicator' in _LIB.RdcGetLastError()\n"
+        "print('ok')\n")
+    assert "ok" in out
 
 
 def run_py(code, env=None):
