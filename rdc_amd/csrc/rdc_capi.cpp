@@ -90,6 +90,7 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_ONESHOT_BYTES") m.cfg.oneshot_push_max = parse_unit(val);
     else if (k == "RDC_FUSE_BYTES") m.cfg.fuse_bytes = std::max<size_t>(parse_unit(val), 1);
     else if (k == "RDC_BOOTSTRAP_TIMEOUT") m.bootstrap_timeout_s = atof(val);
+    else if (k == "RDC_COALESCE_FUSED") m.cfg.coalesce_fused = atoi(val) != 0;
     else if (k == "RDC_P2P_SLOT_BYTES") m.cfg.p2p_slot_bytes = std::max<size_t>(parse_unit(val) / 4096 * 4096, 4096);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
     // to subsystems outside the device path and are accepted silently
@@ -198,7 +199,7 @@ int RdcInit(int argc, char** argv) {
                                      "RDC_RANK", "rdc_reduce_ring_mincount", "RDC_DEVICE", "RDC_SCRATCH_BYTES",
                                      "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
                                      "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES",
-                                     "RDC_P2P_SLOT_BYTES"};
+                                     "RDC_P2P_SLOT_BYTES", "RDC_COALESCE_FUSED"};
         for (const char* k : keys) env_param(m, k);
         m.env_loaded = true;
         for (int i = 0; i < argc; ++i) {
@@ -522,7 +523,8 @@ int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes
         if (!comms || !devices) throw std::invalid_argument("rdc: null argument");
         // parameters from the environment even without RdcInit
         static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
-                                     "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES", "RDC_P2P_SLOT_BYTES"};
+                                     "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES", "RDC_P2P_SLOT_BYTES",
+                                     "RDC_COALESCE_FUSED"};
         if (!m.inited && !m.env_loaded) {
             for (const char* k : keys) env_param(m, k);
             m.env_loaded = true;

@@ -401,8 +401,10 @@ void Communicator::AllreduceRanges(void* buf, const uint64_t* off, const uint64_
 // The schedule over explicit chunk byte ranges of `buf` (chunk c = [off[c],
 // off[c]+len[c]), folded in the ring order of c).
 void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* off, const uint64_t* len,
-                                uint64_t total, size_t esz, int algo, hipStream_t stream) {
+                                uint64_t total, size_t esz, int algo, hipStream_t stream, const PackUnit* units,
+                                int nunits) {
     algo = PickAlgo(algo, total);
+    if (units && algo != RDC_ALGO_MESH) throw std::logic_error("rdc: unit-table launch needs the mesh schedule");
     if (algo == RDC_ALGO_ONESHOT) {
         const Piece p = PlanOneshotRanges(n_, off, len, total, layout(), cfg_.tile_bytes, max_blocks());
         CollArgs a;
@@ -438,6 +440,8 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
             a.nb_reduce = p.nb_reduce;
             a.nb_gather = p.nb_gather;
             a.kind = RDC_KIND_MESH;
+            a.units = units;
+            a.nunits = nunits;
             hip_check(ks.mesh(a, p.nb_scatter + p.nb_reduce + p.nb_gather, stream), "launch mesh allreduce");
         }
     }
@@ -535,6 +539,11 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
             continue;
         }
         const PackEntry& e = PackTable(bufs + b0, counts + b0, b1 - b0, esz);
+        if (cfg_.coalesce_fused && PickAlgo(algo, e.total) == RDC_ALGO_MESH) {
+            // the mesh roles move the buffers' bytes through the unit table: no image, no pack/unpack
+            LaunchRanges(ks, nullptr, e.off, e.len, e.total, esz, RDC_ALGO_MESH, stream, e.dtable, e.nunits);
+            continue;
+        }
         char* img = Image(e.total);
         const int grid = std::max(1, std::min(e.nunits, 2 * num_cus_));
         hip_check(launch_pack(e.dtable, e.nunits, img, 0, grid, stream), "launch pack");

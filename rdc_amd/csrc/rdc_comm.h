@@ -34,6 +34,7 @@ struct CommConfig {
     size_t oneshot_push_max = (size_t)1 << 20;  // auto picks one-shot when (n-1) x bytes <= this
     size_t fuse_bytes = (size_t)256 << 20;      // coalesced allreduce: data bytes per fusion group
     size_t p2p_slot_bytes = (size_t)4 << 20;    // Send/Recv: piece size (2 slots per ordered rank pair)
+    bool coalesce_fused = true;                 // coalesced mesh reads/writes user buffers directly (no image)
 };
 
 struct KernelSet;
@@ -92,8 +93,9 @@ private:
     void FillArgsCommon(CollArgs* a) const;
     int PickAlgo(int algo) const;
     int PickAlgo(int algo, uint64_t bytes) const;
+    // units != null: coalesced mesh over a device PackUnit table (off/len = packed chunk ranges)
     void LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* off, const uint64_t* len, uint64_t total,
-                      size_t esz, int algo, hipStream_t stream);
+                      size_t esz, int algo, hipStream_t stream, const PackUnit* units = nullptr, int nunits = 0);
     struct PackEntry {
         PackUnit* dtable = nullptr;  // device unit table (user addresses)
         int nunits = 0;

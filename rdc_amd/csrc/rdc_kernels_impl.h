@@ -128,15 +128,12 @@ __device__ __forceinline__ void mesh_fold_elem(const CollArgs& a, char* own, con
         if (p != r) *reinterpret_cast<T*>(a.ag[p] + soff + e) = acc;
 }
 
-// Fold one tile of chunk r: out = ring-order reduction of the n ranks'
-// tile, written to the local user buffer and to every peer's allgather slot.
+// Fold `tlen` bytes: own (this rank's values, overwritten with the result),
+// slot0 (rank q's copy at slot0 + q*slot_bytes) in ring order; the result also
+// goes to every peer's allgather region at byte offset soff.
 template <int OP, typename T, int NMAX>
-__device__ void mesh_reduce_tile(const CollArgs& a, int t, uint64_t tlen) {
+__device__ void mesh_reduce_range(const CollArgs& a, char* own, const char* slot0, uint64_t soff, uint64_t tlen) {
     const int n = a.n, r = a.rank;
-    const uint64_t toff = (uint64_t)t * a.tile_bytes;
-    char* own = a.user + a.off[r] + toff;
-    const char* slot0 = a.rs[r] + a.mis[r] + toff;     // + q*slot_bytes
-    const uint64_t soff = (uint64_t)r * a.slot_bytes + a.mis[r] + toff;  // in peers' ag regions
     const unsigned tid = threadIdx.x;
     if ((((uintptr_t)own ^ (uintptr_t)slot0) & 15) != 0) {
         // this rank's buffer is not 16-B aligned: exact, element by element
@@ -188,6 +185,50 @@ __device__ void mesh_reduce_tile(const CollArgs& a, int t, uint64_t tlen) {
     }
 }
 
+// Fold one tile of chunk r: out = ring-order reduction of the n ranks'
+// tile, written to the local user buffer and to every peer's allgather slot.
+template <int OP, typename T, int NMAX>
+__device__ __forceinline__ void mesh_reduce_tile(const CollArgs& a, int t, uint64_t tlen) {
+    const int r = a.rank;
+    const uint64_t toff = (uint64_t)t * a.tile_bytes;
+    mesh_reduce_range<OP, T, NMAX>(a, a.user + a.off[r] + toff, a.rs[r] + a.mis[r] + toff,
+                                   (uint64_t)r * a.slot_bytes + a.mis[r] + toff, tlen);
+}
+
+// ---- coalesced mesh: packed chunk-major offsets -> user buffers.  The unit
+// table (rdc_plan.h PlanCoalesced) is sorted by packed offset; a tile covers a
+// run of units (gaps between segments are padding nobody reads).  Every role
+// works on the unit pieces of its tile directly, so no staging image exists.
+__device__ __forceinline__ int unit_first(const PackUnit* u, int nunits, uint64_t pos) {
+    __shared__ int s_first;
+    if (threadIdx.x == 0) {  // first unit whose range ends after pos
+        int lo = 0, hi = nunits;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (u[mid].packed + u[mid].len <= pos) lo = mid + 1;
+            else hi = mid;
+        }
+        s_first = lo;
+    }
+    __syncthreads();
+    const int f = s_first;
+    __syncthreads();
+    return f;
+}
+
+// f(user pointer, packed offset, bytes) for every unit piece of packed [p0, p1)
+template <typename F>
+__device__ __forceinline__ void for_unit_pieces(const CollArgs& a, uint64_t p0, uint64_t p1, F&& f) {
+    const PackUnit* u = static_cast<const PackUnit*>(a.units);
+    for (int i = unit_first(u, a.nunits, p0); i < a.nunits; ++i) {
+        const uint64_t up = u[i].packed, ul = u[i].len;
+        if (up >= p1) break;
+        const uint64_t lo = up > p0 ? up : p0;
+        const uint64_t hi = up + ul < p1 ? up + ul : p1;
+        if (lo < hi) f(reinterpret_cast<char*>(u[i].buf) + (lo - up), lo, hi - lo);
+    }
+}
+
 template <int OP, typename T, int NMAX>
 __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
     const int n = a.n, r = a.rank;
@@ -212,7 +253,13 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
             const uint64_t toff = (uint64_t)t * a.tile_bytes;
             uint64_t tlen = a.len[c] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-            block_copy(a.rs[c] + (uint64_t)r * a.slot_bytes + a.mis[c] + toff, a.user + a.off[c] + toff, tlen);
+            char* dst = a.rs[c] + (uint64_t)r * a.slot_bytes + a.mis[c];
+            if (a.units)
+                for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
+                    block_copy(dst + (p - a.off[c]), usr, l);
+                });
+            else
+                block_copy(dst + toff, a.user + a.off[c] + toff, tlen);
             block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, seq);
         }
         return;
@@ -230,7 +277,13 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
             const uint64_t toff = (uint64_t)t * a.tile_bytes;
             uint64_t tlen = a.len[r] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-            mesh_reduce_tile<OP, T, NMAX>(a, t, tlen);
+            if (a.units)
+                for_unit_pieces(a, a.off[r] + toff, a.off[r] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
+                    const uint64_t co = a.mis[r] + (p - a.off[r]);
+                    mesh_reduce_range<OP, T, NMAX>(a, usr, a.rs[r] + co, (uint64_t)r * a.slot_bytes + co, l);
+                });
+            else
+                mesh_reduce_tile<OP, T, NMAX>(a, t, tlen);
             if (threadIdx.x < (unsigned)(n - 1)) {
                 const int p = (r + 1 + threadIdx.x) % n;
                 s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
@@ -253,7 +306,13 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[c] - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-        block_copy(a.user + a.off[c] + toff, a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c] + toff, tlen);
+        const char* src = a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c];
+        if (a.units)
+            for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
+                block_copy(usr, src + (p - a.off[c]), l);
+            });
+        else
+            block_copy(a.user + a.off[c] + toff, src + toff, tlen);
     }
 }
 

@@ -409,6 +409,37 @@ def test_group3_coalesced(group3, dtype, op, algo):
                 assert same_bits(got[r][b], want, dtype), (counts, algo, b, r)
 
 
+@pytest.mark.parametrize("fused,tile", [("1", "16K"), ("1", "0"), ("0", "16K")])
+def test_group_coalesced_mesh_unit_table(fused, tile):
+    """The mesh on a coalesced list moves bytes straight between the user
+    buffers and the peers' scratch through the unit table (no staging image);
+    small tiles make tiles start and end inside units and span several.
+    RDC_COALESCE_FUSED=0 keeps the pack / mesh / unpack path.  Bit-exact."""
+    from rdc_amd._lib import _LIB
+    assert _LIB.RdcSetParam(b"RDC_COALESCE_FUSED", fused.encode()) == 0
+    assert _LIB.RdcSetParam(b"RDC_TILE_BYTES", tile.encode()) == 0
+    try:
+        g = make_group(2, 32 << 20)
+    finally:
+        assert _LIB.RdcSetParam(b"RDC_COALESCE_FUSED", b"1") == 0
+        assert _LIB.RdcSetParam(b"RDC_TILE_BYTES", b"0") == 0
+    try:
+        rng = np.random.default_rng(77)
+        for dtype, op, counts in [(6, 2, [300000, 5, 70001, 1 << 20, 33, 0, 4096]),
+                                  (10, 2, [65537, 3, 200003]), (2, 0, [1, 99999, 12345, 7]),
+                                  (7, 2, [40000, 40001, 2])]:
+            sets = [[rand_input(rng, k, dtype) for k in counts] for _ in range(2)]
+            pads = [[(r + b) % 3 for b in range(len(counts))] for r in range(2)]
+            got = run_group_coalesced(g, sets, dtype, op, 2, pads)
+            for b, k in enumerate(counts):
+                want = O.expected_allreduce([sets[r][b] for r in range(2)], dtype, op)
+                for r in range(2):
+                    assert same_bits(got[r][b], want, dtype), (dtype, counts, b, r)
+    finally:
+        for c in g:
+            c.destroy()
+
+
 def test_group_coalesced_fusion_groups_and_cache(group2):
     """Small fuse groups (RDC_FUSE_BYTES) split the list into several fused
     launch sequences; repeated calls with the same buffers reuse the cached
