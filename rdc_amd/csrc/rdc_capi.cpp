@@ -38,6 +38,7 @@ struct Manager {
     int tracker_port = 29571;
     size_t ring_mincount = 1;  // rdc_reduce_ring_mincount (communicator_manager.cc:46)
     double bootstrap_timeout_s = 300.0;
+    size_t host_zc_bytes = (size_t)1 << 20;  // host buffers up to this run zero-copy on pinned memory
     CommConfig cfg;
     std::unique_ptr<Bootstrap> bs;
     std::map<std::string, std::unique_ptr<Communicator>> comms;
@@ -90,6 +91,7 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_ONESHOT_BYTES") m.cfg.oneshot_push_max = parse_unit(val);
     else if (k == "RDC_FUSE_BYTES") m.cfg.fuse_bytes = std::max<size_t>(parse_unit(val), 1);
     else if (k == "RDC_BOOTSTRAP_TIMEOUT") m.bootstrap_timeout_s = atof(val);
+    else if (k == "RDC_HOST_ZC_BYTES") m.host_zc_bytes = parse_unit(val);
     else if (k == "RDC_COALESCE_FUSED") m.cfg.coalesce_fused = atoi(val) != 0;
     else if (k == "RDC_P2P_SLOT_BYTES") m.cfg.p2p_slot_bytes = std::max<size_t>(parse_unit(val) / 4096 * 4096, 4096);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
@@ -199,7 +201,7 @@ int RdcInit(int argc, char** argv) {
                                      "RDC_RANK", "rdc_reduce_ring_mincount", "RDC_DEVICE", "RDC_SCRATCH_BYTES",
                                      "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
                                      "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES",
-                                     "RDC_P2P_SLOT_BYTES", "RDC_COALESCE_FUSED"};
+                                     "RDC_P2P_SLOT_BYTES", "RDC_COALESCE_FUSED", "RDC_HOST_ZC_BYTES"};
         for (const char* k : keys) env_param(m, k);
         m.env_loaded = true;
         for (int i = 0; i < argc; ++i) {
@@ -310,7 +312,7 @@ void allreduce_sync(Manager& m, Communicator* c, void* sendrecv, size_t count, i
     }
     // host-resident buffer: pieces of every chunk through pinned slots, H2D /
     // allreduce / D2H overlapped on three streams
-    if (!m.host) m.host.reset(new HostPath(c->device()));
+    if (!m.host) m.host.reset(new HostPath(c->device(), m.host_zc_bytes));
     m.host->Allreduce(c, sendrecv, count, dtype, op, s);
 }
 

@@ -136,6 +136,9 @@ void Communicator::AllocLocal() {
     hip_check(hipMalloc(&err_, 256), "hipMalloc err");
     hip_check(hipMemset(flags_, 0, flag_bytes_), "memset flags");
     hip_check(hipMemset(err_, 0, 256), "memset err");
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocCoherent), "hipHostMalloc err");
+    memset(err_host_, 0, 64);
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_host_dev_), err_host_, 0), "err device pointer");
     hip_check(hipDeviceSynchronize(), "sync after alloc");
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_) == hipSuccess && cus > 0)
@@ -292,6 +295,7 @@ Communicator::~Communicator() {
     if (flags_) (void)hipFree(flags_);
     if (p2p_) (void)hipFree(p2p_);
     if (err_) (void)hipFree(err_);
+    if (err_host_) (void)hipHostFree(err_host_);
 }
 
 P2PEngine* Communicator::P2P() {
@@ -338,6 +342,7 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
         a->flags[p] = peer_flags_[p];
     }
     a->err = err_;
+    a->err_mirror = err_host_dev_;
     a->done_ctr = err_ + 16;
     a->launch_ctr = err_ + 32;
     a->launch_kind = err_ + 48;
@@ -416,6 +421,9 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         memcpy(a.tiles, p.tiles, sizeof(a.tiles));
         a.tile_bytes = p.tile_bytes;
         a.total_bytes = total;
+        a.notify = notify_;
+        a.notify_val = notify_val_;
+        notify_ = nullptr;
         ++seq_;
         hip_check(ks.oneshot(a, p.nb_scatter, stream), "launch one-shot allreduce");
         return;
@@ -425,6 +433,11 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
     for (const Piece& p : plan) {
         CollArgs a;
         FillArgsCommon(&a);
+        if (&p == &plan.back()) {
+            a.notify = notify_;
+            a.notify_val = notify_val_;
+            notify_ = nullptr;
+        }
         a.user = buf;
         memcpy(a.off, p.off, sizeof(a.off));
         memcpy(a.len, p.len, sizeof(a.len));
@@ -599,15 +612,12 @@ void Communicator::Check(hipStream_t stream) {
     if (err_ == nullptr) return;  // world size 1: nothing was ever launched
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamSynchronize(stream), "stream sync");
-    uint32_t e = 0;
-    hip_check(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost), "read error word");
-    RaiseIfError(e);
+    RaiseIfError(HostErrorWord());
 }
 
-void Communicator::EnqueueErrorCopy(hipStream_t stream, uint32_t* host_word) {
-    *host_word = 0;
-    if (err_ == nullptr) return;
-    hip_check(hipMemcpyAsync(host_word, err_, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "copy error word");
+uint32_t Communicator::HostErrorWord() const {
+    if (err_host_ == nullptr) return RDC_KERR_NONE;
+    return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
 }
 
 void Communicator::RaiseIfError(uint32_t e) const {

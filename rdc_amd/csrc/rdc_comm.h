@@ -67,9 +67,16 @@ public:
     void Allgather(void* const* bufs, const uint64_t* sizes, hipStream_t stream);
     // waits for `stream`, then reads the device error word; throws on error
     void Check(hipStream_t stream);
-    // split form of Check: enqueue a copy of the error word into `host_word`
-    // (pinned) on `stream`; after the caller synchronises, RaiseIfError(*host_word)
-    void EnqueueErrorCopy(hipStream_t stream, uint32_t* host_word);
+    // split form of Check: after the caller synchronised the stream of its
+    // launches, RaiseIfError(HostErrorWord()) (the last block of every launch
+    // mirrors the device error word into pinned host memory)
+    uint32_t HostErrorWord() const;
+    // the next allreduce's final launch stores `val` into the pinned word at
+    // device address `dev_word` when it completes (one call only)
+    void SetHostNotify(uint32_t* dev_word, uint32_t val) {
+        notify_ = dev_word;
+        notify_val_ = val;
+    }
     void RaiseIfError(uint32_t e) const;
     // point-to-point (rdc_p2p.h): bytes of buf to / from one peer, matched in
     // order per pair; device copies start after the work queued on `after`
@@ -116,6 +123,10 @@ private:
     char* scratch_ag_ = nullptr;    // AG region
     uint32_t* flags_ = nullptr;
     uint32_t* err_ = nullptr;
+    uint32_t* err_host_ = nullptr;  // pinned mirror of *err_ (kernel-written)
+    uint32_t* err_host_dev_ = nullptr;
+    uint32_t* notify_ = nullptr;    // SetHostNotify
+    uint32_t notify_val_ = 0;
     size_t slot_bytes_ = 0, region_bytes_ = 0, flag_bytes_ = 0;
     uint32_t max_tiles_ = 0;
     uint32_t seq_ = 0;

@@ -84,6 +84,9 @@ struct CollArgs {
     char* cbuf[RDC_MAX_RANKS];           // allgather: local buffer of rank c's data (off/len index into it)
     int nb_scatter, nb_reduce, nb_gather;  // mesh block roles (allgather: push / -, gather)
     uint32_t* err;                       // local device error word
+    uint32_t* err_mirror;                // host-pinned copy of *err, refreshed by every launch's last block
+    uint32_t* notify;                    // optional pinned word: the last block stores notify_val there when
+    uint32_t notify_val;                 //   the launch is complete (host spins on it instead of a stream sync)
     uint32_t* done_ctr;                  // local per-launch block arrival counter (self-resetting)
     uint32_t* launch_ctr;                // local count of completed launches (device-side seq)
     uint32_t* launch_kind;               // local: kind of the last completed launch

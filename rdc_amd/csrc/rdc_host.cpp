@@ -7,6 +7,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <chrono>
 #include <stdexcept>
 #include <string>
 
@@ -107,7 +108,8 @@ void CopyPool::Run(int n, const std::function<void(int)>& f) {
 }
 
 // ---------------------------------------------------------------- HostPath --
-HostPath::HostPath(int device) : device_(device), pool_(std::max(0, env_int("RDC_HOST_THREADS", 4) - 1)) {
+HostPath::HostPath(int device, size_t zc_max)
+    : device_(device), zc_max_(zc_max), pool_(std::max(0, env_int("RDC_HOST_THREADS", 4) - 1)) {
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "stream");
     hip_check(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking), "stream");
@@ -214,23 +216,58 @@ void HostPath::DrainLoop() {
     }
 }
 
-// Small buffers are latency-bound: copy into pinned memory, H2D, allreduce,
-// D2H and the error word all on the communicator's stream, ONE sync.
+// Small buffers are latency-bound.  Up to zc_max bytes the collective runs
+// zero-copy on the pinned staging buffer itself (the kernel reads and writes
+// host memory over PCIe): memcpy in, ONE kernel, one sync, memcpy out.  Larger
+// ones: H2D, allreduce, D2H on the communicator's stream, one sync.  The
+// error word needs no copy (the kernel mirrors it into pinned memory).
 void HostPath::AllreduceSmall(Communicator* c, char* h, size_t count, size_t S, int dtype, int op,
                               hipStream_t comm_stream) {
     if (!pin_small_) {
-        hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_small_), kSmall + 64, hipHostMallocDefault),
+        hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_small_), kSmall + 64, hipHostMallocCoherent),
                   "hipHostMalloc");
+        hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_small_dev_), pin_small_, 0),
+                  "hipHostGetDevicePointer");
+        notify_host_ = reinterpret_cast<uint32_t*>(pin_small_ + kSmall);
+        *notify_host_ = 0;
+        hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&notify_dev_), notify_host_, 0),
+                  "hipHostGetDevicePointer");
         hip_check(hipMalloc(reinterpret_cast<void**>(&dev_small_), kSmall), "hipMalloc");
     }
-    uint32_t* err_word = reinterpret_cast<uint32_t*>(pin_small_ + kSmall);
     memcpy(pin_small_, h, S);
-    hip_check(hipMemcpyAsync(dev_small_, pin_small_, S, hipMemcpyHostToDevice, comm_stream), "H2D");
-    c->Allreduce(dev_small_, count, dtype, op, comm_stream);
-    hip_check(hipMemcpyAsync(pin_small_, dev_small_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
-    c->EnqueueErrorCopy(comm_stream, err_word);
+    if (S <= zc_max_) {
+        // the launch's last block stores the token into pinned memory: spin on
+        // it (5 us cheaper than a stream sync on MI355X, tools/sync_latency.hip)
+        const uint32_t token = ++notify_token_;
+        c->SetHostNotify(notify_dev_, token);
+        try {
+            c->Allreduce(pin_small_dev_, count, dtype, op, comm_stream);
+        } catch (...) {
+            c->SetHostNotify(nullptr, 0);
+            throw;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        const double limit = c->config().timeout_s * 2 + 10;
+        uint32_t spins = 0;
+        while (__atomic_load_n(notify_host_, __ATOMIC_ACQUIRE) != token) {
+            __builtin_ia32_pause();
+            if ((++spins & 4095) == 0 &&
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+                hip_check(hipStreamSynchronize(comm_stream), "sync");  // surfaces a launch failure
+                if (__atomic_load_n(notify_host_, __ATOMIC_ACQUIRE) != token)
+                    throw std::runtime_error("rdc host path: collective did not complete");
+            }
+        }
+        c->RaiseIfError(c->HostErrorWord());
+        memcpy(h, pin_small_, S);
+        return;
+    } else {
+        hip_check(hipMemcpyAsync(dev_small_, pin_small_, S, hipMemcpyHostToDevice, comm_stream), "H2D");
+        c->Allreduce(dev_small_, count, dtype, op, comm_stream);
+        hip_check(hipMemcpyAsync(pin_small_, dev_small_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
+    }
     hip_check(hipStreamSynchronize(comm_stream), "sync");
-    c->RaiseIfError(*err_word);
+    c->RaiseIfError(c->HostErrorWord());
     memcpy(h, pin_small_, S);
 }
 

@@ -49,7 +49,8 @@ private:
 
 class HostPath {
 public:
-    explicit HostPath(int device);
+    // zc_max: buffers up to this many bytes run zero-copy on pinned memory
+    HostPath(int device, size_t zc_max);
     ~HostPath();
     // in place; synchronous (returns after the result is back in `host`)
     void Allreduce(Communicator* c, void* host, size_t count, int dtype, int op, hipStream_t comm_stream);
@@ -73,6 +74,11 @@ private:
     int device_;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
     char* pin_small_ = nullptr;      // kSmall bytes + the error word
+    char* pin_small_dev_ = nullptr;  // its device address
+    uint32_t* notify_host_ = nullptr;  // completion word (after the kSmall bytes)
+    uint32_t* notify_dev_ = nullptr;
+    uint32_t notify_token_ = 0;
+    size_t zc_max_ = 0;
     char* dev_small_ = nullptr;
     hipEvent_t in_done_[kSlots] = {};
     std::vector<hipEvent_t> ar_done_;  // one per piece of the current call

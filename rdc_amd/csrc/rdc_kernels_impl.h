@@ -563,7 +563,9 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
 __device__ __forceinline__ void launch_done(const CollArgs& a, uint32_t seq) {
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
+        // system scope: a launch may write host memory (zero-copy host path),
+        // which must be visible before the last block's notify store
+        __threadfence_system();
         const uint32_t prev = atomicAdd(a.done_ctr, 1u);
         if (prev == gridDim.x - 1) {
             __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -573,6 +575,10 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint32_t seq) {
                 if (p != a.rank) flag_store(done_word(a, p, a.rank), seq);
             __hip_atomic_store(a.launch_kind, (uint32_t)a.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.launch_ctr, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the host reads the (sticky) error word here after a stream sync: no copy needed
+            __hip_atomic_store(a.err_mirror, __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (a.notify) __hip_atomic_store(a.notify, a.notify_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
