@@ -1,6 +1,8 @@
 // Point-to-point engine (see rdc_p2p.h).
 #include "rdc_p2p.h"
 
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -12,6 +14,23 @@
 namespace rdc_amd {
 
 namespace {
+// RDC_P2P_TRACE=1: timeline of the first pieces on stderr (diagnostics)
+double trace_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+bool trace_on() {
+    static const bool on = getenv("RDC_P2P_TRACE") != nullptr;
+    return on;
+}
+#define P2P_TRACE(...)                                          \
+    do {                                                        \
+        if (trace_on()) {                                       \
+            fprintf(stderr, "[p2p %.1f] ", trace_us());         \
+            fprintf(stderr, __VA_ARGS__);                       \
+            fputc('\n', stderr);                               \
+        }                                                       \
+    } while (0)
+
 void hip_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string("rdc p2p: ") + what + ": " + hipGetErrorString(e));
 }
@@ -28,6 +47,14 @@ bool is_host(const void* p) {
 
 // ---------------------------------------------------------------- WorkComp --
 int WorkComp::Wait() {
+    for (int i = 0; i < 20000; ++i) {  // short transfers finish within microseconds: spin first
+        const int s = status_.load(std::memory_order_acquire);
+        if (s == RDC_WS_FINISHED || s == RDC_WS_ERROR) {
+            std::lock_guard<std::mutex> lk(mu_);  // Finish() has released the lock: err_ is final
+            return s == RDC_WS_FINISHED ? 0 : 1;
+        }
+        __builtin_ia32_pause();
+    }
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [&] { return status_.load() == RDC_WS_FINISHED || status_.load() == RDC_WS_ERROR; });
     return status_.load() == RDC_WS_FINISHED ? 0 : 1;
@@ -91,6 +118,7 @@ WorkComp* P2PEngine::Post(Lane& L, char* buf, size_t bytes, hipStream_t after) {
     r.buf = buf;
     r.bytes = bytes;
     r.host = is_host(buf);
+    P2P_TRACE("post %p %zu B host=%d", (void*)buf, bytes, (int)r.host);
     {
         std::lock_guard<std::mutex> lk(mu_);
         if (!r.host) {
@@ -109,6 +137,7 @@ WorkComp* P2PEngine::Post(Lane& L, char* buf, size_t bytes, hipStream_t after) {
         ++pending_;
     }
     cv_.notify_all();
+    P2P_TRACE("posted");
     return wc;
 }
 
@@ -168,6 +197,7 @@ bool P2PEngine::Complete(Lane& L, std::atomic<uint64_t>& word) {
             r.inflight.pop_front();
             ++L.seq_done;
             word.store(L.seq_done, std::memory_order_release);
+            P2P_TRACE("piece %llu complete", (unsigned long long)L.seq_done);
             moved = true;
         }
         if (r.done < r.bytes) break;
@@ -202,6 +232,7 @@ bool P2PEngine::StepSend(int dest, Lane& L) {
             char* dst = peers_[dest] + ((size_t)rank_ * kP2PSlots + s) * slot_bytes_;
             ctl_->len[rank_][dest][s].v.store(len, std::memory_order_relaxed);  // published by posted's release
             hip_check(launch_copy(dst, src, len, L.stream), "launch copy");
+            P2P_TRACE("send piece %llu launched", (unsigned long long)seq);
             hipEvent_t e = Event();
             hip_check(hipEventRecord(e, L.stream), "record");
             r.inflight.emplace_back(e, len);
@@ -236,6 +267,7 @@ bool P2PEngine::StepRecv(int src, Lane& L) {
                 hip_check(hipMemcpyAsync(to, from, len, hipMemcpyDeviceToHost, L.stream), "D2H");
             else
                 hip_check(launch_copy(to, from, len, L.stream), "launch copy");
+            P2P_TRACE("recv piece %llu launched", (unsigned long long)seq);
             hipEvent_t e = Event();
             hip_check(hipEventRecord(e, L.stream), "record");
             r.inflight.emplace_back(e, len);
@@ -289,10 +321,14 @@ void P2PEngine::Loop() {
             idle = 0;
             continue;
         }
-        // nothing moved: back off (yield briefly, then sleep up to 50 us)
+        // nothing moved: spin (a hand-off is a few microseconds away) for
+        // ~10 ms of idle polls, then back off to sleeps of up to 50 us
         lk.unlock();
-        if (++idle < 64) std::this_thread::yield();
-        else std::this_thread::sleep_for(std::chrono::microseconds(std::min(50, idle / 64)));
+        if (++idle < 8192) {
+            for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+        } else {
+            std::this_thread::sleep_for(std::chrono::microseconds(std::min(50, (idle - 8192) / 64 + 1)));
+        }
         lk.lock();
     }
 }
