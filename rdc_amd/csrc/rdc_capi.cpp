@@ -161,7 +161,9 @@ bool is_device_pointer(const void* p) {
 
 hipStream_t manager_stream(Manager& m, int device) {
     if (!m.stream) {
-        if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking) != hipSuccess)
+        // a blocking stream: synchronous calls on device memory are ordered
+        // after the work the caller queued on the null (default) stream
+        if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&m.stream, hipStreamDefault) != hipSuccess)
             throw std::runtime_error("rdc: cannot create stream");
     }
     return m.stream;
@@ -306,8 +308,16 @@ void allreduce_sync(Manager& m, Communicator* c, void* sendrecv, size_t count, i
     if (c->size() == 1 || count == 0) return;
     hipStream_t s = manager_stream(m, c->device());
     if (is_device_pointer(sendrecv)) {
-        c->Allreduce(sendrecv, count, dtype, op, s);
-        c->Check(s);
+        // the manager's stream is ordered after the caller's null-stream
+        // work; completion is the launch's own token (no stream sync)
+        const uint32_t token = c->ArmNotify();
+        try {
+            c->Allreduce(sendrecv, count, dtype, op, s);
+        } catch (...) {
+            c->WaitNotify(token, s);  // disarms
+            throw;
+        }
+        c->WaitNotify(token, s);
         return;
     }
     // host-resident buffer: pieces of every chunk through pinned slots, H2D /

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <stdexcept>
 #include <string>
 
@@ -612,6 +613,36 @@ void Communicator::Check(hipStream_t stream) {
     if (err_ == nullptr) return;  // world size 1: nothing was ever launched
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamSynchronize(stream), "stream sync");
+    RaiseIfError(HostErrorWord());
+}
+
+// pinned words: err_host_[0] = error mirror, err_host_[4] = notify token
+uint32_t Communicator::ArmNotify() {
+    if (err_host_dev_ == nullptr) return 0;
+    notify_ = err_host_dev_ + 4;
+    notify_val_ = ++notify_token_;
+    return notify_val_;
+}
+
+void Communicator::WaitNotify(uint32_t token, hipStream_t stream) {
+    if (err_host_ == nullptr) return;
+    if (notify_ != nullptr) {  // nothing was launched (empty buffer, world size 1, or an error before launch)
+        notify_ = nullptr;
+        return;
+    }
+    const uint32_t* w = err_host_ + 4;
+    const auto t0 = std::chrono::steady_clock::now();
+    const double limit = cfg_.timeout_s * 2 + 10;  // the kernels themselves give up after timeout_s
+    uint32_t spins = 0;
+    while (__atomic_load_n(w, __ATOMIC_ACQUIRE) != token) {
+        __builtin_ia32_pause();
+        if ((++spins & 4095) == 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+            hip_check(hipStreamSynchronize(stream), "stream sync");  // surfaces a launch failure
+            if (__atomic_load_n(w, __ATOMIC_ACQUIRE) != token)
+                throw std::runtime_error("rdc: collective did not complete on rank " + std::to_string(rank_));
+        }
+    }
     RaiseIfError(HostErrorWord());
 }
 

@@ -71,12 +71,14 @@ public:
     // launches, RaiseIfError(HostErrorWord()) (the last block of every launch
     // mirrors the device error word into pinned host memory)
     uint32_t HostErrorWord() const;
-    // the next allreduce's final launch stores `val` into the pinned word at
-    // device address `dev_word` when it completes (one call only)
-    void SetHostNotify(uint32_t* dev_word, uint32_t val) {
-        notify_ = dev_word;
-        notify_val_ = val;
-    }
+    // Synchronous callers: ArmNotify() before ONE Allreduce / AllreduceRanges,
+    // WaitNotify(token, stream) after it.  The call's final launch stores the
+    // token into pinned host memory after a system-scope fence; the host spins
+    // on it (a stream sync costs ~5 us more per call, tools/sync_latency.hip),
+    // then raises a device-side error like Check.  A call that launched
+    // nothing returns at once.
+    uint32_t ArmNotify();
+    void WaitNotify(uint32_t token, hipStream_t stream);
     void RaiseIfError(uint32_t e) const;
     // point-to-point (rdc_p2p.h): bytes of buf to / from one peer, matched in
     // order per pair; device copies start after the work queued on `after`
@@ -125,8 +127,9 @@ private:
     uint32_t* err_ = nullptr;
     uint32_t* err_host_ = nullptr;  // pinned mirror of *err_ (kernel-written)
     uint32_t* err_host_dev_ = nullptr;
-    uint32_t* notify_ = nullptr;    // SetHostNotify
+    uint32_t* notify_ = nullptr;    // armed: device address of the pinned notify word
     uint32_t notify_val_ = 0;
+    uint32_t notify_token_ = 0;
     size_t slot_bytes_ = 0, region_bytes_ = 0, flag_bytes_ = 0;
     uint32_t max_tiles_ = 0;
     uint32_t seq_ = 0;

@@ -228,44 +228,26 @@ void HostPath::AllreduceSmall(Communicator* c, char* h, size_t count, size_t S, 
                   "hipHostMalloc");
         hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_small_dev_), pin_small_, 0),
                   "hipHostGetDevicePointer");
-        notify_host_ = reinterpret_cast<uint32_t*>(pin_small_ + kSmall);
-        *notify_host_ = 0;
-        hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&notify_dev_), notify_host_, 0),
-                  "hipHostGetDevicePointer");
         hip_check(hipMalloc(reinterpret_cast<void**>(&dev_small_), kSmall), "hipMalloc");
     }
     memcpy(pin_small_, h, S);
     if (S <= zc_max_) {
-        // the launch's last block stores the token into pinned memory: spin on
-        // it (5 us cheaper than a stream sync on MI355X, tools/sync_latency.hip)
-        const uint32_t token = ++notify_token_;
-        c->SetHostNotify(notify_dev_, token);
+        // the launch's last block stores a token into pinned memory: spin on
+        // it instead of a stream sync (Communicator::ArmNotify / WaitNotify)
+        const uint32_t token = c->ArmNotify();
         try {
             c->Allreduce(pin_small_dev_, count, dtype, op, comm_stream);
         } catch (...) {
-            c->SetHostNotify(nullptr, 0);
+            c->WaitNotify(token, comm_stream);  // disarms
             throw;
         }
-        const auto t0 = std::chrono::steady_clock::now();
-        const double limit = c->config().timeout_s * 2 + 10;
-        uint32_t spins = 0;
-        while (__atomic_load_n(notify_host_, __ATOMIC_ACQUIRE) != token) {
-            __builtin_ia32_pause();
-            if ((++spins & 4095) == 0 &&
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
-                hip_check(hipStreamSynchronize(comm_stream), "sync");  // surfaces a launch failure
-                if (__atomic_load_n(notify_host_, __ATOMIC_ACQUIRE) != token)
-                    throw std::runtime_error("rdc host path: collective did not complete");
-            }
-        }
-        c->RaiseIfError(c->HostErrorWord());
+        c->WaitNotify(token, comm_stream);
         memcpy(h, pin_small_, S);
         return;
-    } else {
-        hip_check(hipMemcpyAsync(dev_small_, pin_small_, S, hipMemcpyHostToDevice, comm_stream), "H2D");
-        c->Allreduce(dev_small_, count, dtype, op, comm_stream);
-        hip_check(hipMemcpyAsync(pin_small_, dev_small_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
     }
+    hip_check(hipMemcpyAsync(dev_small_, pin_small_, S, hipMemcpyHostToDevice, comm_stream), "H2D");
+    c->Allreduce(dev_small_, count, dtype, op, comm_stream);
+    hip_check(hipMemcpyAsync(pin_small_, dev_small_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
     hip_check(hipStreamSynchronize(comm_stream), "sync");
     c->RaiseIfError(c->HostErrorWord());
     memcpy(h, pin_small_, S);

@@ -75,9 +75,6 @@ private:
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
     char* pin_small_ = nullptr;      // kSmall bytes + the error word
     char* pin_small_dev_ = nullptr;  // its device address
-    uint32_t* notify_host_ = nullptr;  // completion word (after the kSmall bytes)
-    uint32_t* notify_dev_ = nullptr;
-    uint32_t notify_token_ = 0;
     size_t zc_max_ = 0;
     char* dev_small_ = nullptr;
     hipEvent_t in_done_[kSlots] = {};
