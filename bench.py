@@ -94,6 +94,29 @@ def cpu_baseline(nbytes_workload, seconds):
     }
 
 
+def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
+    """Measured link rates (outside the timed region, every rank idle): the
+    copy kernel the collectives use pushes nbytes from each GPU into
+    (a) rank+1 only - one link, one direction, every link busy in a ring;
+    (b) every peer at once - all n-1 links out of each GPU (the mesh's egress).
+    Slowest rank's rate.  On a 1-GPU box the ranks share one HBM."""
+    out = {}
+    for mode, key in ((0, "one_link_one_direction_GBps"), (1, "all_links_egress_GBps")):
+        ms, used = ctypes.c_double(), ctypes.c_size_t()
+        rc = lib.RdcCommProbe(comm.handle, mode, nbytes, reps, sp, ctypes.byref(ms), ctypes.byref(used))
+        if rc != 0:
+            return {"error": lib.RdcGetLastError().decode()}
+        per_target = used.value
+        t = torch.tensor([ms.value], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ntarget = 1 if mode == 0 else int(os.environ.get("WORLD_SIZE", "1")) - 1
+        out[key] = round(per_target * ntarget / (float(t[0]) * 1e-3) / 1e9, 2)
+        dist.barrier()
+    out["bytes_per_target"] = per_target
+    out["kernel"] = "k_push (block_copy, 16-B non-temporal remote stores)"
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -170,6 +193,7 @@ def main():
     if world > 1:
         comm.check(sp)
         dist.barrier()
+        probe = xgmi_probe(_LIB, comm, sp, dist, torch)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -230,7 +254,12 @@ def main():
                 "frac": round(busbw / peak, 4), "traffic": None,
                 "kernel": "k_%s<Sum,%s>" % (algo_name, args.dtype),
                 "algorithmic_bytes_per_launch": int(2 * (world - 1) * S // world), "kernel_avg_ms": round(kern_ms, 4),
-                "frac_of_bidir_ring_roofline": round(busbw / BIDIR_RING_GBPS, 4)}
+                "frac_of_bidir_ring_roofline": round(busbw / BIDIR_RING_GBPS, 4),
+                "xgmi_probe": probe}
+        if isinstance(probe, dict) and probe.get("all_links_egress_GBps"):
+            meas = probe["one_link_one_direction_GBps"] if algo_name == "ring" else probe["all_links_egress_GBps"]
+            roof["peak_measured"] = meas
+            roof["frac_of_measured"] = round(busbw / meas, 4)
         workload = "in-place allreduce(sum) of a %d MiB %s buffer per GPU, %s schedule" % (S >> 20, args.dtype,
                                                                                         algo_name)
         if args.buckets > 1:

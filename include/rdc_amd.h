@@ -157,6 +157,17 @@ int RdcCommDevice(void* comm);
 /* 0 uncached, 1 fine-grained, 2 coarse-grained scratch */
 int RdcCommAllocKind(void* comm);
 
+/* xGMI link probe (diagnostics, bench.py at N > 1): push `bytes` per target
+ * from this rank's scratch into peers' scratch `reps` times on `stream`, all
+ * targets at once, with the copy kernel the collectives use for remote
+ * stores.  mode 0: rank+1 only (one link, one direction); mode 1: every peer
+ * (all n-1 links out of this GPU).  *ms_out = average ms per round;
+ * *bytes_out (may be NULL) = bytes per target actually pushed (clamped to
+ * the scratch slot).  Call it
+ * between collectives with every rank idle (e.g. after a barrier): it
+ * overwrites scratch, which every collective rewrites before reading. */
+int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, double* ms_out, size_t* bytes_out);
+
 /* Single process driving n ranks (devices[i] = HIP device of rank i; devices
  * may repeat).  comms[i] receives rank i's handle.  scratch_bytes 0 = default. */
 int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes);

@@ -55,6 +55,7 @@ def _load():
         "RdcCommAllreduceEx": (i, [vp, vp, sz, i, i, i, vp]),
         "RdcCommBroadcast": (i, [vp, vp, sz, i, vp]),
         "RdcCommCheck": (i, [vp, vp]),
+        "RdcCommProbe": (i, [vp, i, sz, i, vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]),
         "RdcCommRank": (i, [vp]),
         "RdcCommSize": (i, [vp]),
         "RdcCommDevice": (i, [vp]),

@@ -523,6 +523,14 @@ int RdcCommCheck(void* comm, void* stream) {
     return guard([&] { as_comm(comm)->Check(static_cast<hipStream_t>(stream)); });
 }
 
+int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, double* ms_out, size_t* bytes_out) {
+    return guard([&] {
+        if (!ms_out) throw std::invalid_argument("rdc: null argument");
+        *ms_out = as_comm(comm)->Probe(mode, &bytes, reps, static_cast<hipStream_t>(stream));
+        if (bytes_out) *bytes_out = bytes;
+    });
+}
+
 int RdcCommRank(void* comm) { return comm ? static_cast<Communicator*>(comm)->rank() : -1; }
 int RdcCommSize(void* comm) { return comm ? static_cast<Communicator*>(comm)->size() : -1; }
 int RdcCommDevice(void* comm) { return comm ? static_cast<Communicator*>(comm)->device() : -1; }

@@ -587,6 +587,41 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
     }
 }
 
+double Communicator::Probe(int mode, size_t* bytes_io, int reps, hipStream_t stream) {
+    size_t bytes = *bytes_io;
+    if (n_ == 1) throw std::invalid_argument("rdc: probe needs 2 or more ranks");
+    if (mode != 0 && mode != 1) throw std::invalid_argument("rdc: probe mode is 0 (next rank) or 1 (all peers)");
+    bytes = std::min(bytes, region_bytes_ - (size_t)RDC_SLOT_ALIGN);  // source: my own AG region
+    if (mode == 1) bytes = std::min(bytes, slot_bytes_ - (size_t)RDC_SLOT_ALIGN);
+    bytes &= ~(size_t)255;
+    if (bytes == 0 || reps <= 0) throw std::invalid_argument("rdc: probe needs bytes and reps");
+    *bytes_io = bytes;
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    PushTargets t;
+    memset(&t, 0, sizeof(t));
+    int nd = 0;
+    if (mode == 0) {
+        t.dst[nd++] = peer_scratch_[(rank_ + 1) % n_];  // the whole RS region of the next rank
+    } else {
+        for (int k = 1; k < n_; ++k)  // my slot in every peer's RS region
+            t.dst[nd++] = peer_scratch_[(rank_ + k) % n_] + (size_t)rank_ * slot_bytes_;
+    }
+    hipEvent_t e0, e1;
+    hip_check(hipEventCreate(&e0), "event");
+    hip_check(hipEventCreate(&e1), "event");
+    const int grid = 2 * num_cus_;
+    hip_check(launch_push(t, nd, scratch_ag_, bytes, grid, stream), "launch push");  // warm
+    hip_check(hipEventRecord(e0, stream), "record");
+    for (int i = 0; i < reps; ++i) hip_check(launch_push(t, nd, scratch_ag_, bytes, grid, stream), "launch push");
+    hip_check(hipEventRecord(e1, stream), "record");
+    hip_check(hipEventSynchronize(e1), "sync");
+    float ms = 0;
+    hip_check(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return ms / reps;
+}
+
 void Communicator::Allgather(void* const* bufs, const uint64_t* sizes, hipStream_t stream) {
     if (n_ == 1) return;
     for (int c = 0; c < n_; ++c)

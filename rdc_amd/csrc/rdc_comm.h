@@ -85,6 +85,13 @@ public:
     WorkComp* ISend(const void* buf, size_t bytes, int dest, hipStream_t after);
     WorkComp* IRecv(void* buf, size_t bytes, int src, hipStream_t after);
 
+    // xGMI probe (diagnostics; no collective may be in flight on any rank):
+    // push `bytes` into each target peer's scratch (mode 0: rank+1 only, one
+    // link one direction; mode 1: every peer at once) `reps` times on
+    // `stream`; returns the average ms per push round (HIP events).
+    // Overwrites scratch contents only, which every collective rewrites.
+    double Probe(int mode, size_t* bytes, int reps, hipStream_t stream);  // *bytes: asked in, used out
+
     int rank() const { return rank_; }
     int size() const { return n_; }
     int device() const { return device_; }

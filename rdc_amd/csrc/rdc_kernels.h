@@ -22,6 +22,11 @@ hipError_t launch_allgather(const CollArgs& a, int grid, hipStream_t s);
 hipError_t launch_pack(const PackUnit* units, int nunits, char* image, int unpack, int grid, hipStream_t s);
 // plain device copy (dst may be IPC-mapped peer memory); never waits
 hipError_t launch_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s);
+// xGMI probe: block b pushes its share of `bytes` from src into dsts[b % ndst]
+struct PushTargets {
+    char* dst[RDC_MAX_RANKS];
+};
+hipError_t launch_push(const PushTargets& t, int ndst, const void* src, uint64_t bytes, int grid, hipStream_t s);
 hipError_t launch_fill(void* buf, uint64_t count, int dtype, uint64_t seed, int rank, hipStream_t s);
 
 }  // namespace rdc_amd

@@ -92,6 +92,20 @@ __global__ __launch_bounds__(kBlock) void k_copy(char* __restrict__ dst, const c
         block_copy(dst + off, src + off, bytes - off < kStep ? bytes - off : kStep);
 }
 
+// ================================================================ probe ===
+// Link probe (Communicator::Probe): the blocks are split evenly over the ndst
+// targets; each target receives the same `bytes` from src with remote
+// stores (16-B non-temporal lanes), all targets concurrently.
+__global__ __launch_bounds__(kBlock) void k_push(PushTargets t, int ndst, const char* __restrict__ src,
+                                                 uint64_t bytes) {
+    const int per = gridDim.x / ndst;
+    const int d = blockIdx.x % ndst, b = blockIdx.x / ndst;
+    if (b >= per) return;
+    constexpr uint64_t kStep = 64 << 10;
+    for (uint64_t off = (uint64_t)b * kStep; off < bytes; off += (uint64_t)per * kStep)
+        block_copy(t.dst[d] + off, src + off, bytes - off < kStep ? bytes - off : kStep);
+}
+
 // ================================================================= fill ===
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -158,6 +172,14 @@ hipError_t launch_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s
     uint64_t grid = (bytes + (64 << 10) - 1) >> 16;
     if (grid > 128) grid = 128;
     hipLaunchKernelGGL(k_copy, dim3((unsigned)grid), dim3(kBlock), 0, s, (char*)dst, (const char*)src, bytes);
+    return hipGetLastError();
+}
+
+hipError_t launch_push(const PushTargets& t, int ndst, const void* src, uint64_t bytes, int grid, hipStream_t s) {
+    if (ndst <= 0 || bytes == 0) return hipSuccess;
+    grid = (grid / ndst) * ndst;
+    if (grid < ndst) grid = ndst;
+    hipLaunchKernelGGL(k_push, dim3((unsigned)grid), dim3(kBlock), 0, s, t, ndst, (const char*)src, bytes);
     return hipGetLastError();
 }
 

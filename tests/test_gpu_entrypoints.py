@@ -58,6 +58,9 @@ def test_bench_torchrun_two_ranks():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["roofline"]["bound"] == "xgmi"
     assert out["config"]["bytes_per_gpu"] == 64 << 20
+    probe = out["roofline"]["xgmi_probe"]
+    assert probe["one_link_one_direction_GBps"] > 0 and probe["all_links_egress_GBps"] > 0, probe
+    assert out["roofline"]["frac_of_measured"] > 0
 
 
 def test_launcher_cpp_known_answer(known_answer_exe):
