@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--unfused", action="store_true", help="buckets as separate allreduce calls (no coalescing)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run oracle spot check")
+    ap.add_argument("--ring-steps", type=int, default=5,
+                    help="N>1: also time the reference's ring schedule this many steps after the timed region")
     return ap.parse_args()
 
 
@@ -92,6 +94,29 @@ def cpu_baseline(nbytes_workload, seconds):
                   "(value = buffer bytes / time, same unit as the GPU line; HBM-equivalent traffic 3x)"
                   % (n * 4 >> 20, reps, el),
     }
+
+
+def time_ring(lib, comm, buf, count, dt_enum, sp, dist, torch, steps):
+    """ms per in-place allreduce with the reference's ring schedule (k_ring),
+    max over ranks, after 2 warm-up launches."""
+    from rdc_amd._lib import check_call
+
+    def one():
+        check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), count, dt_enum, 2, 1, sp))
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize()
+    comm.check(sp)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    comm.check(sp)
+    return float(t[0]) * 1e3
 
 
 def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
@@ -214,6 +239,12 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall, kern_ms = float(tt[0]), float(tt[1])
 
+    # the reference's own schedule on the same buffer, after the timed region
+    # (informational: same bits, one link direction per GPU)
+    ring_cmp = None
+    if world > 1 and args.buckets == 1 and args.algo == "auto" and args.ring_steps > 0:
+        ring_cmp = time_ring(_LIB, comm, buf, count, dt_enum, sp, dist, torch, args.ring_steps)
+
     # spot check (outside the timed region): N=1 reduce result vs oracle on a slice
     check = None
     if world == 1 and not args.no_check:
@@ -287,6 +318,12 @@ def main():
     }
     if world > 1:
         out["busbw_GBps"] = round(algbw * 2 * (world - 1) / world, 2)
+    if ring_cmp is not None:
+        rb = S / (ring_cmp * 1e-3) / 1e9 * 2 * (world - 1) / world
+        out["ring_schedule"] = {"ms_per_step": round(ring_cmp, 4), "busbw_GBps": round(rb, 2),
+                                "frac_of_one_link_peak": round(rb / XGMI_LINK_DIR_GBPS, 4),
+                                "note": "reference ring schedule (k_ring) on the same buffer, timed after the "
+                                        "main region; bit-identical result"}
     if check is not None:
         out["oracle_check"] = check
     print(json.dumps(out), flush=True)
