@@ -35,6 +35,7 @@ struct CommConfig {
     size_t fuse_bytes = (size_t)256 << 20;      // coalesced allreduce: data bytes per fusion group
     size_t p2p_slot_bytes = (size_t)4 << 20;    // Send/Recv: piece size (2 slots per ordered rank pair)
     bool coalesce_fused = true;                 // coalesced mesh reads/writes user buffers directly (no image)
+    size_t fuse_bytes_direct = (size_t)16 << 30;  // ... in groups of up to this many data bytes
 };
 
 struct KernelSet;
@@ -122,6 +123,8 @@ private:
     static constexpr size_t kPackCacheMax = 64;
     const PackEntry& PackTable(void* const* bufs, const size_t* counts, int nbuf, size_t esz);
     char* Image(uint64_t bytes);
+    void CoalescedStaged(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, int dtype, int op,
+                         size_t esz, int algo, hipStream_t stream);
 
     std::string name_;
     int rank_ = 0, n_ = 1, device_ = 0;
