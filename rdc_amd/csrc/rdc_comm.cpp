@@ -77,6 +77,7 @@ struct PeerInfo {
     uint64_t max_tiles;
     uint64_t p2p_slot_bytes;
     char host[64];
+    char pci[32];  // physical GPU (ranks may share one: tests, emulation)
 };
 
 // The point-to-point control block (rdc_p2p.h) in POSIX shared memory: rank 0
@@ -183,6 +184,10 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     mine.slot_bytes = c->slot_bytes_;
     mine.max_tiles = c->max_tiles_;
     gethostname(mine.host, sizeof(mine.host) - 1);
+    if (hipDeviceGetPCIBusId(mine.pci, sizeof(mine.pci) - 1, device) != hipSuccess) {
+        (void)hipGetLastError();
+        snprintf(mine.pci, sizeof(mine.pci), "device-%d", device);
+    }
     std::vector<PeerInfo> all((size_t)c->n_);
     dbg("[rdc %d] %s\n", c->rank_, "handles exported");
     bs->allgather(&mine, sizeof(mine), all.data());
@@ -195,6 +200,8 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
             throw std::runtime_error("rdc: xGMI path needs every rank on one node (rank " + std::to_string(p) +
                                      " is on " + all[(size_t)p].host + ")");
     }
+    for (int p = 0; p < c->n_; ++p)
+        if (p != c->rank_ && strncmp(all[(size_t)p].pci, mine.pci, sizeof(mine.pci)) == 0) c->shared_gpu_ = true;
     // direct peer access between distinct devices (xGMI); IPC mapping with
     // hipIpcMemLazyEnablePeerAccess covers the rest.
     for (int p = 0; p < c->n_; ++p) {
@@ -246,6 +253,10 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
         c->AllocLocal();
         cs.push_back(std::move(c));
     }
+    bool shared = false;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < i; ++j) shared |= devices[i] == devices[j];
+    for (auto& c : cs) c->shared_gpu_ = shared;
     std::shared_ptr<P2PCtl> ctl = std::make_shared<P2PCtl>();  // value-initialised: all words 0
     for (int i = 0; i < n; ++i) {
         cs[(size_t)i]->p2p_ctl_ = ctl;
@@ -362,6 +373,16 @@ Layout Communicator::layout() const {
 
 int Communicator::max_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_blocks : num_cus_; }
 
+// The mesh keeps more remote stores in flight with two blocks per CU (k_mesh:
+// 100 VGPRs, 4 blocks per CU fit): 1 GiB on 2 ranks 1.86 -> 1.65-1.69 ms at
+// 384-512 blocks (tools/mesh_sweep*.sh).  Only when no other rank shares this
+// GPU: several ranks' oversubscribed launches on one GPU could keep a waiting
+// role's partner blocks from being dispatched.
+int Communicator::mesh_blocks() const {
+    if (cfg_.max_blocks > 0) return cfg_.max_blocks;
+    return shared_gpu_ ? num_cus_ : 2 * num_cus_;
+}
+
 void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStream_t stream, int algo) {
     KernelSet ks;
     if (!get_kernels(dtype, op, &ks))
@@ -430,7 +451,8 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         return;
     }
     const std::vector<Piece> plan =
-        PlanAllreduceRanges(n_, off, len, esz, layout(), algo, cfg_.tile_bytes, max_blocks());
+        PlanAllreduceRanges(n_, off, len, esz, layout(), algo, cfg_.tile_bytes,
+                            algo == RDC_ALGO_MESH ? mesh_blocks() : max_blocks());
     for (const Piece& p : plan) {
         CollArgs a;
         FillArgsCommon(&a);

@@ -103,6 +103,8 @@ public:
     const CommConfig& config() const { return cfg_; }
     Layout layout() const;
     int max_blocks() const;
+    int mesh_blocks() const;        // grid of a mesh launch
+    bool shared_gpu() const { return shared_gpu_; }
 
 private:
     Communicator();
@@ -145,6 +147,7 @@ private:
     uint32_t seq_ = 0;
     int alloc_kind_ = 0;
     int num_cus_ = 256;
+    bool shared_gpu_ = false;       // another rank of this communicator runs on the same physical GPU
     int wall_khz_ = 100000;         // wall_clock64() rate
     char* peer_scratch_[RDC_MAX_RANKS] = {};
     char* peer_ag_[RDC_MAX_RANKS] = {};

@@ -1,0 +1,11 @@
+# mesh (and ring) 1 GiB fp32, 2 ranks as processes on ONE GPU: grid size sweep
+cd $GRAFT_REPO_ROOT
+port=29850
+for nb in 384 512 768 1024; do
+  for algo in mesh ring; do
+    port=$((port+3))
+    RDC_NBLOCKS=$nb timeout -k 10 120 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+       --master-addr 127.0.0.1 --master-port $port bench.py --gpus 2 --steps 10 --warmup 3 --ring-steps 0 --algo $algo 2>&1 | grep '^{' \
+       | python -c "import sys,json; d=json.loads(sys.stdin.read()); print('nblocks=$nb $algo %.3f ms/step' % d['ms_per_step'])" || exit 1
+  done
+done
