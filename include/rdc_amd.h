@@ -41,7 +41,8 @@ extern "C" {
  * Keys: RDC_RANK, RDC_WORLD_SIZE|rdc_world_size, RDC_TRACKER_URI,
  * RDC_TRACKER_PORT, rdc_reduce_ring_mincount, RDC_DEVICE, RDC_SCRATCH_BYTES,
  * RDC_ALGO (mesh|ring|oneshot), RDC_NBLOCKS, RDC_TILE_BYTES, RDC_TIMEOUT, RDC_ONESHOT_BYTES,
- * RDC_FUSE_BYTES.
+ * RDC_FUSE_BYTES, RDC_FUSE_BYTES_DIRECT, RDC_COALESCE_FUSED, RDC_HOST_ZC_BYTES,
+ * RDC_BCAST_SPLIT_BYTES, RDC_P2P_SLOT_BYTES.
  * Falls back to torchrun's RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT
  * (tracker port = MASTER_PORT+1).  Does not touch the GPU. */
 int RdcInit(int argc, char** argv);
@@ -85,9 +86,12 @@ int RdcAllgather(void** bufs, const size_t* sizes);
 int RdcAllgatherOn(void* comm, void** bufs, const size_t* sizes);
 
 /* Coalesced (bucketed) allreduce: the result of one RdcAllreduce per buffer,
- * in order, bit-identical, but the buffers move in fused launches (groups of
- * up to RDC_FUSE_BYTES, default 256 MiB, packed chunk-major into one HBM
- * staging image; BASELINE cfg5 / test/mallreduce.cc's back-to-back shape).
+ * in order, bit-identical, but the buffers move in fused launches (BASELINE
+ * cfg5 / test/mallreduce.cc's back-to-back shape).  With the mesh schedule the
+ * launches read and write the buffers in place through a cached unit table
+ * (groups of up to RDC_FUSE_BYTES_DIRECT, default 16 GiB); one-shot / ring
+ * lists are packed chunk-major into an HBM staging image in groups of
+ * RDC_FUSE_BYTES (default 256 MiB).
  * bufs[b] holds counts[b] elements of `dtype`; all host or all device memory;
  * synchronous.  RdcAllreduceCoalesced uses the "main" communicator. */
 int RdcAllreduceCoalesced(void** bufs, const size_t* counts, int nbuf, int dtype, int op);

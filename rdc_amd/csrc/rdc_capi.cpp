@@ -93,6 +93,7 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_BOOTSTRAP_TIMEOUT") m.bootstrap_timeout_s = atof(val);
     else if (k == "RDC_HOST_ZC_BYTES") m.host_zc_bytes = parse_unit(val);
     else if (k == "RDC_COALESCE_FUSED") m.cfg.coalesce_fused = atoi(val) != 0;
+    else if (k == "RDC_BCAST_SPLIT_BYTES") m.cfg.bcast_split_bytes = parse_unit(val);
     else if (k == "RDC_FUSE_BYTES_DIRECT") m.cfg.fuse_bytes_direct = std::max<size_t>(parse_unit(val), 1);
     else if (k == "RDC_P2P_SLOT_BYTES") m.cfg.p2p_slot_bytes = std::max<size_t>(parse_unit(val) / 4096 * 4096, 4096);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
@@ -205,7 +206,7 @@ int RdcInit(int argc, char** argv) {
                                      "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
                                      "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES",
                                      "RDC_P2P_SLOT_BYTES", "RDC_COALESCE_FUSED", "RDC_HOST_ZC_BYTES",
-                                     "RDC_FUSE_BYTES_DIRECT"};
+                                     "RDC_FUSE_BYTES_DIRECT", "RDC_BCAST_SPLIT_BYTES"};
         for (const char* k : keys) env_param(m, k);
         m.env_loaded = true;
         for (int i = 0; i < argc; ++i) {
@@ -546,7 +547,8 @@ int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes
         // parameters from the environment even without RdcInit
         static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
                                      "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES", "RDC_P2P_SLOT_BYTES",
-                                     "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT"};
+                                     "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT",
+                                     "RDC_BCAST_SPLIT_BYTES"};
         if (!m.inited && !m.env_loaded) {
             for (const char* k : keys) env_param(m, k);
             m.env_loaded = true;

@@ -631,6 +631,8 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
         a.mis[0] = p.mis[0];
         a.tiles[0] = p.tiles[0];
         a.tile_bytes = p.tile_bytes;
+        // large pieces: root -> one forwarder per tile -> the other ranks (k_bcast)
+        a.bcast_split = (n_ >= 3 && p.len[0] >= cfg_.bcast_split_bytes && p.tiles[0] >= n_ - 1) ? 1 : 0;
         ++seq_;
         hip_check(launch_bcast(a, p.nb_scatter, stream), "launch broadcast");
     }

@@ -36,6 +36,7 @@ struct CommConfig {
     size_t p2p_slot_bytes = (size_t)4 << 20;    // Send/Recv: piece size (2 slots per ordered rank pair)
     bool coalesce_fused = true;                 // coalesced mesh reads/writes user buffers directly (no image)
     size_t fuse_bytes_direct = (size_t)16 << 30;  // ... in groups of up to this many data bytes
+    size_t bcast_split_bytes = (size_t)1 << 20;   // broadcast pieces from this size: root -> forwarders -> ranks
 };
 
 struct KernelSet;

@@ -91,7 +91,8 @@ struct CollArgs {
     uint32_t* launch_ctr;                // local count of completed launches (device-side seq)
     uint32_t* launch_kind;               // local: kind of the last completed launch
     int kind;                            // this launch's RDC_KIND_*
-    uint64_t half_bytes;                 // one-shot: offset of the slot half used by odd seq
+    int bcast_split;                     // broadcast: root -> forwarder per tile -> other ranks (n >= 3)
+    uint64_t half_bytes;                // one-shot: offset of the slot half used by odd seq
     uint64_t total_bytes;                // one-shot: whole buffer bytes
     const void* units;                   // coalesced mesh: device PackUnit table (off/len are packed
     int nunits;                          //   offsets; user bytes reached through the units), else null

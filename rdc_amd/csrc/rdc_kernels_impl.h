@@ -517,20 +517,38 @@ __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
 
 // ============================================================ broadcast ===
 // piece = [off[0], off[0]+len[0]) of the user buffer; tiles[0] tiles.
+// direct (bcast_split == 0): the root pushes every tile to all n-1 peers - one
+//   hop, but the root's egress is (n-1) x S: for small pieces.
+// split (n >= 3): tile t goes from the root to ONE forwarder, the
+//   (t mod (n-1))-th rank after the root, which lands it and pushes it on to
+//   the other n-2 non-root ranks.  Two hops, but every link out of the root
+//   carries S/(n-1) and every forwarder link S/(n-1): up to (n-1)/2 x the
+//   direct rate when the links are the bound (8 GPUs: 3.5x).
+// Either way a rank's flag (n+root, t) has one writer per launch: the root
+// (direct, or the forwarder's own flag) or the tile's forwarder.
+__device__ __forceinline__ int bcast_forwarder(int n, int root, int t) { return (root + 1 + t % (n - 1)) % n; }
+
 __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
     const int n = a.n, r = a.rank, root = a.root;
+    const bool split = a.bcast_split != 0 && n >= 3;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
-    if (r == root && blockIdx.x < a.tiles[0]) {
+    __shared__ int s_cnt;
+    if (blockIdx.x < a.tiles[0] && (r == root || split)) {
         // A broadcast's receivers never report back, so before overwriting a
-        // peer's allgather region the root waits until that peer finished
-        // its previous launch (done word >= seq-1).  Allreduce launches need
-        // no such gate: their peer writes depend on data the target only
-        // sends once it has entered the same launch.
-        if (threadIdx.x < (unsigned)(n - 1))
-            s_flags[threadIdx.x] = done_word(a, r, (root + 1 + threadIdx.x) % n);
+        // peer's allgather region a writer waits until that peer finished
+        // its previous launch (done word >= seq-1): the root for every peer,
+        // a forwarder (split) for the other non-root ranks.  Allreduce
+        // launches need no such gate: their peer writes depend on data the
+        // target only sends once it has entered the same launch.
+        if (threadIdx.x == 0) {
+            int k = 0;
+            for (int q = 0; q < n; ++q)
+                if (q != r && q != root) s_flags[k++] = done_word(a, r, q);
+            s_cnt = k;
+        }
         __syncthreads();
-        if (!block_wait(s_flags, n - 1, seq - 1, ab, RDC_KERR_TIMEOUT_BCAST)) return;
+        if (!block_wait(s_flags, s_cnt, seq - 1, ab, RDC_KERR_TIMEOUT_BCAST)) return;
     }
     for (int t = blockIdx.x; t < a.tiles[0]; t += gridDim.x) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
@@ -538,18 +556,36 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
         char* mine = a.user + a.off[0] + toff;
         const uint64_t soff = a.mis[0] + toff;
+        const uint64_t frow = (uint64_t)(n + root) * a.max_tiles + t;
         if (r == root) {
-            for (int k = 1; k < n; ++k) block_copy(a.ag[(root + k) % n] + soff, mine, tlen);
-            if (threadIdx.x < (unsigned)(n - 1))
-                s_flags[threadIdx.x] =
-                    a.flags[(root + 1 + threadIdx.x) % n] + (uint64_t)(n + root) * a.max_tiles + t;
-            block_publish(s_flags, n - 1, seq);
+            if (split) {
+                const int f = bcast_forwarder(n, root, t);
+                block_copy(a.ag[f] + soff, mine, tlen);
+                block_publish1(a.flags[f] + frow, seq);
+            } else {
+                for (int k = 1; k < n; ++k) block_copy(a.ag[(root + k) % n] + soff, mine, tlen);
+                if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.flags[(root + 1 + threadIdx.x) % n] + frow;
+                block_publish(s_flags, n - 1, seq);
+            }
             __syncthreads();
         } else {
-            if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + root) * a.max_tiles + t;
+            if (threadIdx.x == 0) s_flags[0] = a.flags[r] + frow;
             __syncthreads();
             if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_BCAST)) return;
-            block_copy(mine, a.ag[r] + soff, tlen);
+            const char* land = a.ag[r] + soff;
+            if (split && bcast_forwarder(n, root, t) == r) {
+                for (int k = 1; k < n; ++k) {
+                    const int q = (r + k) % n;
+                    if (q != root) block_copy(a.ag[q] + soff, land, tlen);
+                }
+                if (threadIdx.x == 0) {
+                    int k = 0;
+                    for (int q = 0; q < n; ++q)
+                        if (q != r && q != root) s_flags[k++] = a.flags[q] + frow;
+                }
+                block_publish(s_flags, n - 2, seq);  // its barrier orders thread 0's list before use
+            }
+            block_copy(mine, land, tlen);
             __syncthreads();
         }
     }

@@ -156,7 +156,7 @@ def test_group_broadcast(group3):
     from rdc_amd._lib import _LIB
     rng = np.random.default_rng(3)
     for root in range(3):
-        for nbytes in (1, 100, 1 << 20 | 3):
+        for nbytes in (1, 100, 1 << 20 | 3, (5 << 20) + 7):
             data = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(3)]
             bufs = [to_dev(d, 1 + r) for r, d in enumerate(data)]
             streams = group3.streams
@@ -267,6 +267,7 @@ def test_mp_allreduce(world):
         {"count": 77777, "dtype": 1, "op": 3, "comm": "second"},
         {"count": 70000, "dtype": 11, "op": 2, "reps": 3},
         {"count": 123457, "dtype": 0, "kind": "broadcast", "root": world - 1},
+        {"count": (3 << 20) + 5, "dtype": 0, "kind": "broadcast", "root": 1},   # forwarded (n >= 3)
         {"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"},
         {"count": 25000003, "dtype": 6, "op": 2, "kind": "host_allreduce", "reps": 2},   # 7 pipelined pieces
         {"count": 3000001, "dtype": 10, "op": 0, "kind": "host_allreduce"},

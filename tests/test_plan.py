@@ -168,3 +168,14 @@ def test_fuse_groups():
     assert fuse_groups([256] * 8, f32, 4096) == [0, 4, 8]           # 1 KiB each, 4 KiB groups
     assert fuse_groups([256, 10000, 256], f32, 4096) == [0, 1, 2, 3]  # an oversized buffer is alone
     assert fuse_groups([(1 << 20) // 4] * 1024, f32, 0) == list(range(0, 1025, 256))  # cfg5: 4 x 256 MiB
+
+
+def test_mixed_plan_is_deterministic():
+    """The randomized GPU chain (tests/test_gpu_mixed.py) is the same on every
+    rank and in the parent: seeded plan, oracle expectation of the right size."""
+    from tests.mixed_plan import expected, make_plan, output_bytes
+    a, b = make_plan(11, 40, 3), make_plan(11, 40, 3)
+    assert a == b and len(a) == 40
+    assert {op["kind"] for op in a} >= {"allreduce", "bcast", "allgather", "coalesced"}
+    small = make_plan(5, 6, 2)
+    assert expected(small, 2).size == output_bytes(small)
