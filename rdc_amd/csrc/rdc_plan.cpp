@@ -37,12 +37,21 @@ void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blo
     size_t t = cfg_tile;
     if (t == 0) {
         // ring: each block walks 2(n-1) hand-offs per tile, so one tile per
-        // block.  mesh: ~4 tiles per reduce block, so the scatter, reduce and
-        // gather roles overlap (with one tile each they run as three
-        // back-to-back phases: 0.22 vs 0.13 ms for 64 MB, tools/group_perf.py).
+        // block.  mesh: ~2 tiles per reduce block, at least 64 KiB — every
+        // tile costs a flag hand-off per role, and the tile sweep on one GPU
+        // (tools/tile_sweep.sh, profiles/r01/mesh_tile_sweep_group2.log)
+        // found 4 tiles per reduce block too fine below 64 MB (16 MB:
+        // 0.115 ms at 22 KiB tiles vs 0.071-0.075 ms at 64-128 KiB), and
+        // 16 KiB floors slow at 4 MB (0.044 vs 0.034 ms at 64 KiB).
         const size_t G = (size_t)std::max(1, max_blocks);
-        const size_t want = algo == RDC_ALGO_RING ? chunk_bytes / G : chunk_bytes / (4 * std::max<size_t>(1, G * 3 / 8));
-        t = std::min<size_t>(std::max<size_t>(want, RDC_MIN_TILE), (size_t)1 << 20);
+        size_t want, lo = RDC_MIN_TILE;
+        if (algo == RDC_ALGO_RING) {
+            want = chunk_bytes / G;
+        } else {
+            want = chunk_bytes / (2 * std::max<size_t>(1, G * 3 / 8));
+            lo = (size_t)64 << 10;
+        }
+        t = std::min<size_t>(std::max<size_t>(want, lo), (size_t)1 << 20);
     }
     t = std::max<size_t>(round_up(t, RDC_SLOT_ALIGN), RDC_MIN_TILE);
     p->tile_bytes = t;
