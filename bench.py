@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--unfused", action="store_true", help="buckets as separate allreduce calls (no coalescing)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run oracle spot check")
+    ap.add_argument("--extra-steps", type=int, default=5,
+                    help="N>1: also time cfg4 (fp16) and cfg5 (1024 buckets) this many steps after the timed region")
     ap.add_argument("--ring-steps", type=int, default=5,
                     help="N>1: also time the reference's ring schedule this many steps after the timed region")
     return ap.parse_args()
@@ -117,6 +119,59 @@ def time_ring(lib, comm, buf, count, dt_enum, sp, dist, torch, steps):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     comm.check(sp)
     return float(t[0]) * 1e3
+
+
+def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps):
+    """The other BASELINE.json multi-GPU configs on the same communicator,
+    after the timed region (informational): cfg4 = fp16 allreduce of a buffer
+    of S bytes, cfg5 = 1024 buckets of S/1024 bytes fp32 in one coalesced
+    call.  ms per step = max over ranks of the wall time of `steps` calls."""
+    from rdc_amd._lib import check_call
+    out = {}
+
+    def timed(one):
+        for _ in range(2):
+            one()
+        torch.cuda.synchronize()
+        comm.check(sp)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        comm.check(sp)
+        return float(t[0]) * 1e3
+
+    def entry(ms, nbytes, what):
+        bb = nbytes / (ms * 1e-3) / 1e9 * 2 * (world - 1) / world
+        return {"workload": what, "bytes_per_gpu": nbytes, "ms_per_step": round(ms, 4), "busbw_GBps": round(bb, 2),
+                "steps": steps}
+
+    try:
+        h = torch.empty(S // 2, dtype=torch.float16, device="cuda")
+        import rdc_amd
+        rdc_amd.fill_(h, 0x5EED0000, rank)
+        ms = timed(lambda: check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(h.data_ptr()), h.numel(),
+                                                             10, 2, 0, sp)))
+        out["cfg4_fp16"] = entry(ms, S, "in-place allreduce(sum) of a %d MiB float16 buffer (packed half "
+                                        "reduce kernel)" % (S >> 20))
+        del h
+        K = 1024
+        per = S // 4 // K
+        bks = [torch.empty(per, dtype=torch.float32, device="cuda") for _ in range(K)]
+        for b, t in enumerate(bks):
+            rdc_amd.fill_(t, 0x5EED0000 + b, rank)
+        ptrs = (ctypes.c_void_p * K)(*[t.data_ptr() for t in bks])
+        cnts = (ctypes.c_size_t * K)(*([per] * K))
+        ms = timed(lambda: check_call(lib.RdcCommAllreduceCoalesced(comm.handle, ptrs, cnts, K, 6, 2, 0, sp)))
+        out["cfg5_buckets"] = entry(ms, per * 4 * K, "%d x %d KiB float32 buckets, one coalesced call "
+                                                     "(test/mallreduce.cc shape)" % (K, per * 4 >> 10))
+    except Exception as e:  # informational: never costs the main line
+        out["error"] = str(e)
+    return out
 
 
 def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
@@ -244,6 +299,11 @@ def main():
     ring_cmp = None
     if world > 1 and args.buckets == 1 and args.algo == "auto" and args.ring_steps > 0:
         ring_cmp = time_ring(_LIB, comm, buf, count, dt_enum, sp, dist, torch, args.ring_steps)
+    extra = None
+    if world > 1 and args.buckets == 1 and args.algo == "auto" and args.extra_steps > 0 and args.dtype == "float32":
+        del buf  # room for the other configs' buffers
+        torch.cuda.empty_cache()
+        extra = time_extra_configs(_LIB, comm, S, world, rank, sp, dist, torch, args.extra_steps)
 
     # spot check (outside the timed region): N=1 reduce result vs oracle on a slice
     check = None
@@ -324,6 +384,8 @@ def main():
                                 "frac_of_one_link_peak": round(rb / XGMI_LINK_DIR_GBPS, 4),
                                 "note": "reference ring schedule (k_ring) on the same buffer, timed after the "
                                         "main region; bit-identical result"}
+    if extra is not None:
+        out["extra_configs"] = extra
     if check is not None:
         out["oracle_check"] = check
     print(json.dumps(out), flush=True)
