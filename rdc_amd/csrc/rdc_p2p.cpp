@@ -310,13 +310,24 @@ bool P2PEngine::Progress() {
 void P2PEngine::Loop() {
     (void)hipSetDevice(device_);
     std::unique_lock<std::mutex> lk(mu_);
-    int idle = 0;
+    int idle = 0, quiet = 0;
     while (!stop_) {
         if (pending_ == 0) {
+            // stay hot for ~2 ms after the last request: the next message of
+            // an exchange usually follows within microseconds, and a wake
+            // from the condition variable costs 5-10 us
+            if (quiet < 4096) {
+                ++quiet;
+                lk.unlock();
+                for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+                lk.lock();
+                continue;
+            }
             cv_.wait(lk, [&] { return stop_ || pending_ > 0; });
-            idle = 0;
+            idle = quiet = 0;
             continue;
         }
+        quiet = 0;
         if (Progress()) {
             idle = 0;
             continue;
