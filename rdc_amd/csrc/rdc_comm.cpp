@@ -110,7 +110,17 @@ std::shared_ptr<P2PCtl> map_p2p_ctl(Bootstrap* bs) {
     void* p = mmap(nullptr, sizeof(P2PCtl), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);
     if (p == MAP_FAILED) throw std::runtime_error(std::string("rdc: cannot map shared memory: ") + strerror(errno));
-    std::shared_ptr<P2PCtl> ctl(static_cast<P2PCtl*>(p), [](P2PCtl* q) { munmap(q, sizeof(P2PCtl)); });
+    // registered for device access: the p2p copy kernels publish posted /
+    // consumed themselves (rdc_p2p.h)
+    if (hipHostRegister(p, sizeof(P2PCtl), hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        munmap(p, sizeof(P2PCtl));
+        throw std::runtime_error("rdc: cannot register the p2p control block for device access");
+    }
+    std::shared_ptr<P2PCtl> ctl(static_cast<P2PCtl*>(p), [](P2PCtl* q) {
+        (void)hipHostUnregister(q);
+        munmap(q, sizeof(P2PCtl));
+    });
     bs->barrier();
     if (bs->rank() == 0) shm_unlink(name);
     return ctl;
@@ -257,7 +267,16 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < i; ++j) shared |= devices[i] == devices[j];
     for (auto& c : cs) c->shared_gpu_ = shared;
-    std::shared_ptr<P2PCtl> ctl = std::make_shared<P2PCtl>();  // value-initialised: all words 0
+    P2PCtl* raw = new P2PCtl();  // value-initialised: all words 0
+    if (hipHostRegister(raw, sizeof(P2PCtl), hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        delete raw;
+        throw std::runtime_error("rdc: cannot register the p2p control block for device access");
+    }
+    std::shared_ptr<P2PCtl> ctl(raw, [](P2PCtl* q) {
+        (void)hipHostUnregister(q);
+        delete q;
+    });
     for (int i = 0; i < n; ++i) {
         cs[(size_t)i]->p2p_ctl_ = ctl;
         for (int j = 0; j < n; ++j) {

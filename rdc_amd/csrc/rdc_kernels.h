@@ -20,8 +20,12 @@ hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s);
 hipError_t launch_allgather(const CollArgs& a, int grid, hipStream_t s);
 // coalesced allreduce: units[i].buf = user address; unpack = image -> buffers
 hipError_t launch_pack(const PackUnit* units, int nunits, char* image, int unpack, int grid, hipStream_t s);
-// plain device copy (dst may be IPC-mapped peer memory); never waits
-hipError_t launch_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s);
+// plain device copy (dst may be IPC-mapped peer memory); never waits.
+// With `word` (host-mapped): the last block to finish stores `value` there
+// (system-scope release, after every block's system fence); `arrive` is a
+// zeroed device counter owned by the stream (reset by that last block).
+hipError_t launch_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s, uint32_t* arrive = nullptr,
+                       uint64_t* word = nullptr, uint64_t value = 0);
 // xGMI probe: block b pushes its share of `bytes` from src into dsts[b % ndst]
 struct PushTargets {
     char* dst[RDC_MAX_RANKS];

@@ -86,10 +86,24 @@ __global__ __launch_bounds__(kBlock) void k_pack(const PackUnit* __restrict__ un
 // ============================================================ p2p copy ===
 // Point-to-point pieces (rdc_p2p.cpp): a plain copy, 64 KiB per block step;
 // dst may be a peer's IPC-mapped slot (remote stores over xGMI).  Never waits.
-__global__ __launch_bounds__(kBlock) void k_copy(char* __restrict__ dst, const char* __restrict__ src, uint64_t bytes) {
+// The last block publishes the piece's sequence number into the host-mapped
+// control block, so neither side's host needs to observe the kernel first.
+__global__ __launch_bounds__(kBlock) void k_copy(char* __restrict__ dst, const char* __restrict__ src, uint64_t bytes,
+                                                 uint32_t* arrive, uint64_t* word, uint64_t value) {
     constexpr uint64_t kStep = 64 << 10;
     for (uint64_t off = (uint64_t)blockIdx.x * kStep; off < bytes; off += (uint64_t)gridDim.x * kStep)
         block_copy(dst + off, src + off, bytes - off < kStep ? bytes - off : kStep);
+    if (word == nullptr) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        if (atomicAdd(arrive, 1u) == gridDim.x - 1) {
+            __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // ================================================================ probe ===
@@ -167,11 +181,14 @@ hipError_t launch_pack(const PackUnit* units, int nunits, char* image, int unpac
     return hipGetLastError();
 }
 
-hipError_t launch_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s) {
-    if (bytes == 0) return hipSuccess;
+hipError_t launch_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s, uint32_t* arrive, uint64_t* word,
+                       uint64_t value) {
+    if (bytes == 0 && word == nullptr) return hipSuccess;
     uint64_t grid = (bytes + (64 << 10) - 1) >> 16;
     if (grid > 128) grid = 128;
-    hipLaunchKernelGGL(k_copy, dim3((unsigned)grid), dim3(kBlock), 0, s, (char*)dst, (const char*)src, bytes);
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(k_copy, dim3((unsigned)grid), dim3(kBlock), 0, s, (char*)dst, (const char*)src, bytes, arrive,
+                       word, value);
     return hipGetLastError();
 }
 

@@ -84,6 +84,13 @@ P2PEngine::P2PEngine(int rank, int n, int device, size_t slot_bytes, char* local
                      double timeout_s)
     : rank_(rank), n_(n), device_(device), slot_bytes_(slot_bytes), timeout_s_(timeout_s), local_(local), ctl_(ctl) {
     for (int p = 0; p < RDC_MAX_RANKS; ++p) peers_[p] = p < n ? peers[p] : nullptr;
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    void* d = nullptr;
+    hip_check(hipHostGetDevicePointer(&d, ctl_, 0), "control block device address");
+    ctl_dev_ = static_cast<char*>(d);
+    hip_check(hipMalloc(&arrive_, 2 * RDC_MAX_RANKS * sizeof(uint32_t)), "hipMalloc arrival counters");
+    hip_check(hipMemset(arrive_, 0, 2 * RDC_MAX_RANKS * sizeof(uint32_t)), "memset arrival counters");
+    hip_check(hipDeviceSynchronize(), "sync");
     th_ = std::thread([this] { Loop(); });
 }
 
@@ -104,6 +111,11 @@ P2PEngine::~P2PEngine() {
         }
     }
     for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
+    if (arrive_) (void)hipFree(arrive_);
+}
+
+uint64_t* P2PEngine::DevWord(const std::atomic<uint64_t>& w) const {
+    return reinterpret_cast<uint64_t*>(ctl_dev_ + (reinterpret_cast<const char*>(&w) - reinterpret_cast<const char*>(ctl_)));
 }
 
 WorkComp* P2PEngine::Post(Lane& L, char* buf, size_t bytes, hipStream_t after) {
@@ -164,7 +176,6 @@ hipEvent_t P2PEngine::Event() {
 
 void P2PEngine::Fail(Lane& L, const std::string& err) {
     for (Req& r : L.q) {
-        for (auto& e : r.inflight) free_events_.push_back(e.first);
         if (r.ready) free_events_.push_back(r.ready);
         r.wc->Finish(RDC_WS_ERROR, err);
         --pending_;
@@ -182,21 +193,17 @@ void P2PEngine::Ready(Lane& L, Req& r) {
     }
 }
 
-// retire finished pieces of the front requests in stream order; `word`
-// (posted for a send lane, consumed for a recv lane) publishes the count
-bool P2PEngine::Complete(Lane& L, std::atomic<uint64_t>& word) {
+// retire finished pieces of the front requests: `word` (posted for a send
+// lane, consumed for a recv lane) is advanced by the copy kernels themselves
+bool P2PEngine::Complete(Lane& L, const std::atomic<uint64_t>& word) {
     bool moved = false;
+    const uint64_t now = word.load(std::memory_order_acquire);
     while (!L.q.empty()) {
         Req& r = L.q.front();
-        while (!r.inflight.empty()) {
-            const hipError_t q = hipEventQuery(r.inflight.front().first);
-            if (q == hipErrorNotReady) break;
-            if (q != hipSuccess) hip_check(q, "copy");
-            free_events_.push_back(r.inflight.front().first);
+        while (!r.inflight.empty() && r.inflight.front().first <= now) {
             r.done += r.inflight.front().second;
             r.inflight.pop_front();
             ++L.seq_done;
-            word.store(L.seq_done, std::memory_order_release);
             P2P_TRACE("piece %llu complete", (unsigned long long)L.seq_done);
             moved = true;
         }
@@ -231,11 +238,10 @@ bool P2PEngine::StepSend(int dest, Lane& L) {
             }
             char* dst = peers_[dest] + ((size_t)rank_ * kP2PSlots + s) * slot_bytes_;
             ctl_->len[rank_][dest][s].v.store(len, std::memory_order_relaxed);  // published by posted's release
-            hip_check(launch_copy(dst, src, len, L.stream), "launch copy");
+            hip_check(launch_copy(dst, src, len, L.stream, arrive_ + dest, DevWord(ctl_->posted[rank_][dest].v), seq),
+                      "launch copy");
             P2P_TRACE("send piece %llu launched", (unsigned long long)seq);
-            hipEvent_t e = Event();
-            hip_check(hipEventRecord(e, L.stream), "record");
-            r.inflight.emplace_back(e, len);
+            r.inflight.emplace_back(seq, len);
             r.issued += len;
             L.seq_issued = seq;
             moved = true;
@@ -263,14 +269,17 @@ bool P2PEngine::StepRecv(int src, Lane& L) {
             Ready(L, r);
             const char* from = local_ + ((size_t)src * kP2PSlots + s) * slot_bytes_;
             char* to = r.buf + r.issued;
-            if (r.host)
+            uint64_t* word = DevWord(ctl_->consumed[src][rank_].v);
+            if (r.host) {  // DMA, then a signal-only launch (stream order: after the copy landed)
                 hip_check(hipMemcpyAsync(to, from, len, hipMemcpyDeviceToHost, L.stream), "D2H");
-            else
-                hip_check(launch_copy(to, from, len, L.stream), "launch copy");
+                hip_check(launch_copy(nullptr, nullptr, 0, L.stream, arrive_ + RDC_MAX_RANKS + src, word, seq),
+                          "launch signal");
+            } else {
+                hip_check(launch_copy(to, from, len, L.stream, arrive_ + RDC_MAX_RANKS + src, word, seq),
+                          "launch copy");
+            }
             P2P_TRACE("recv piece %llu launched", (unsigned long long)seq);
-            hipEvent_t e = Event();
-            hip_check(hipEventRecord(e, L.stream), "record");
-            r.inflight.emplace_back(e, len);
+            r.inflight.emplace_back(seq, len);
             r.issued += len;
             L.seq_issued = seq;
             moved = true;

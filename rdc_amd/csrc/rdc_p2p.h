@@ -8,7 +8,8 @@
 // slot) straight into the receiver's IPC-mapped p2p slot for this sender over
 // xGMI; the receiver copies it out.  No kernel ever waits: the hand-off lives
 // in a small control block of host shared memory (POSIX shm between the
-// node's processes), one writer per word:
+// node's processes, registered for device access), one writer per word,
+// written by the copy kernels' last block:
 //     posted[src][dst]   pieces src has landed in dst's slots
 //     consumed[src][dst] pieces dst has copied out (slot reusable)
 // and a per-communicator progress thread drives both directions for every
@@ -88,7 +89,7 @@ private:
         hipEvent_t ready = nullptr; // recorded on the caller's stream at post time
         size_t issued = 0;          // bytes whose piece has been issued
         size_t done = 0;            // bytes whose piece completed
-        std::deque<std::pair<hipEvent_t, size_t>> inflight;  // (event, piece bytes)
+        std::deque<std::pair<uint64_t, size_t>> inflight;  // (piece seq, piece bytes)
     };
     struct Lane {           // one direction with one peer
         std::deque<Req> q;
@@ -100,7 +101,8 @@ private:
     WorkComp* Post(Lane& L, char* buf, size_t bytes, hipStream_t after);
     void Loop();
     bool Progress();        // one pass; true if anything moved
-    bool Complete(Lane& L, std::atomic<uint64_t>& word);
+    bool Complete(Lane& L, const std::atomic<uint64_t>& word);
+    uint64_t* DevWord(const std::atomic<uint64_t>& w) const;  // device address of a control word
     bool StepSend(int peer, Lane& L);
     bool StepRecv(int peer, Lane& L);
     void Ready(Lane& L, Req& r);
@@ -113,6 +115,8 @@ private:
     char* local_;
     char* peers_[RDC_MAX_RANKS];
     P2PCtl* ctl_;
+    char* ctl_dev_ = nullptr;      // the control block's device address (host-registered)
+    uint32_t* arrive_ = nullptr;   // device: copy-kernel arrival counters [send n | recv n]
     Lane send_[RDC_MAX_RANKS], recv_[RDC_MAX_RANKS];
     std::vector<hipEvent_t> free_events_;
     std::mutex mu_;
