@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--unfused", action="store_true", help="buckets as separate allreduce calls (no coalescing)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run oracle spot check")
+    ap.add_argument("--rccl-steps", type=int, default=10,
+                    help="N>1: also time RCCL's allreduce of the same buffer (child processes, 0 = skip)")
     ap.add_argument("--extra-steps", type=int, default=5,
                     help="N>1: also time cfg4 (fp16) and cfg5 (1024 buckets) this many steps after the timed region")
     ap.add_argument("--ring-steps", type=int, default=5,
@@ -172,6 +174,35 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps):
     except Exception as e:  # informational: never costs the main line
         out["error"] = str(e)
     return out
+
+
+def rccl_compare(S, world, rank, local, dist, torch, steps):
+    """The same allreduce through RCCL (torch.distributed nccl backend), one
+    child process per rank (tools/rccl_allreduce.py), after every rdc
+    measurement and under a time limit: informational, never costs the line.
+    Skipped when ranks share a GPU (RCCL needs one rank per device)."""
+    import subprocess
+    if torch.cuda.device_count() < world:
+        return {"skipped": "ranks share a GPU (RCCL needs one GPU per rank)"}
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("MASTER_PORT", "29500")) + 7
+    dist.barrier()
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "rccl_allreduce.py"), str(rank), str(world), str(local), addr,
+           str(port), str(S), str(steps)]
+    res = {"error": "no result"}
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=150)
+        lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+        if lines:
+            res = json.loads(lines[-1])
+        elif p.returncode != 0:
+            res = {"error": "rc=%d: %s" % (p.returncode, p.stderr[-300:])}
+    except subprocess.TimeoutExpired:
+        res = {"error": "timed out after 150 s"}
+    except Exception as e:  # noqa: BLE001 - informational only
+        res = {"error": str(e)}
+    dist.barrier()
+    return res
 
 
 def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
@@ -299,11 +330,13 @@ def main():
     ring_cmp = None
     if world > 1 and args.buckets == 1 and args.algo == "auto" and args.ring_steps > 0:
         ring_cmp = time_ring(_LIB, comm, buf, count, dt_enum, sp, dist, torch, args.ring_steps)
-    extra = None
+    extra = rccl = None
     if world > 1 and args.buckets == 1 and args.algo == "auto" and args.extra_steps > 0 and args.dtype == "float32":
         del buf  # room for the other configs' buffers
         torch.cuda.empty_cache()
         extra = time_extra_configs(_LIB, comm, S, world, rank, sp, dist, torch, args.extra_steps)
+    if world > 1 and args.buckets == 1 and args.algo == "auto" and args.rccl_steps > 0 and args.dtype == "float32":
+        rccl = rccl_compare(S, world, rank, local, dist, torch, args.rccl_steps)
 
     # spot check (outside the timed region): N=1 reduce result vs oracle on a slice
     check = None
@@ -386,6 +419,8 @@ def main():
                                         "main region; bit-identical result"}
     if extra is not None:
         out["extra_configs"] = extra
+    if rccl is not None:
+        out["rccl_comparison"] = rccl
     if check is not None:
         out["oracle_check"] = check
     print(json.dumps(out), flush=True)
