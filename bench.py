@@ -205,6 +205,42 @@ def rccl_compare(S, world, rank, local, dist, torch, steps):
     return res
 
 
+def trace_roles(lib, comm, buf, count, dt_enum, sp, dist, torch):
+    """One traced allreduce (RdcCommTraceNext) after the timed region: when
+    each block role started and finished, relative to the launch's first
+    block (max over ranks), in microseconds (wall_clock64 = 100 MHz).  Tells
+    which role bounds the schedule on real links."""
+    import numpy as np
+    from rdc_amd._lib import check_call
+    words = 2 * 8192
+    tr = torch.zeros(words, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    dist.barrier()
+    check_call(lib.RdcCommTraceNext(comm.handle, ctypes.c_void_p(tr.data_ptr()), words))
+    check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), count, dt_enum, 2, 0, sp))
+    torch.cuda.synchronize()
+    comm.check(sp)
+    ll = (ctypes.c_uint64 * 6)()
+    check_call(lib.RdcCommLastLaunch(comm.handle, ll))
+    grid, s, r, g, tile, algo = [int(x) for x in ll]
+    t = tr[:2 * grid].cpu().numpy().view(np.uint64).reshape(grid, 2).astype(np.float64)
+    t0 = t[:, 0].min()
+    names = {1: "ring", 2: "mesh", 3: "oneshot"}
+    roles = {"all": (0, grid)} if algo != 2 else {"scatter": (0, s), "reduce": (s, s + r), "gather": (s + r, grid)}
+    vals = []
+    for lo, hi in roles.values():
+        seg = t[lo:hi]
+        vals += [(seg[:, 0].min() - t0) / 100.0, (seg[:, 1].max() - t0) / 100.0, float(np.mean(seg[:, 1] - seg[:, 0])) / 100.0]
+    v = torch.tensor(vals, dtype=torch.float64)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    out = {"schedule": names.get(algo, str(algo)), "grid": grid, "tile_bytes": tile,
+           "blocks": {"scatter": s, "reduce": r, "gather": g} if algo == 2 else {"all": grid}}
+    for i, k in enumerate(roles):
+        out[k + "_us"] = {"first_start": round(float(v[3 * i]), 1), "last_end": round(float(v[3 * i + 1]), 1),
+                          "mean_block_busy": round(float(v[3 * i + 2]), 1)}
+    return out
+
+
 def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
     """Measured link rates (outside the timed region, every rank idle): the
     copy kernel the collectives use pushes nbytes from each GPU into
@@ -327,6 +363,12 @@ def main():
 
     # the reference's own schedule on the same buffer, after the timed region
     # (informational: same bits, one link direction per GPU)
+    roles = None
+    if world > 1 and args.buckets == 1 and args.algo == "auto":
+        try:
+            roles = trace_roles(_LIB, comm, buf, count, dt_enum, sp, dist, torch)
+        except Exception as e:  # noqa: BLE001 - diagnostics only
+            roles = {"error": str(e)}
     ring_cmp = None
     if world > 1 and args.buckets == 1 and args.algo == "auto" and args.ring_steps > 0:
         ring_cmp = time_ring(_LIB, comm, buf, count, dt_enum, sp, dist, torch, args.ring_steps)
@@ -417,6 +459,8 @@ def main():
                                 "frac_of_one_link_peak": round(rb / XGMI_LINK_DIR_GBPS, 4),
                                 "note": "reference ring schedule (k_ring) on the same buffer, timed after the "
                                         "main region; bit-identical result"}
+    if roles is not None:
+        out["role_timeline"] = roles
     if extra is not None:
         out["extra_configs"] = extra
     if rccl is not None:

@@ -172,6 +172,15 @@ int RdcCommAllocKind(void* comm);
  * overwrites scratch, which every collective rewrites before reading. */
 int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, double* ms_out, size_t* bytes_out);
 
+/* Diagnostics (bench.py at N > 1): the next allreduce on `comm` (mesh or
+ * ring schedule) records, per block, {start, end} wall_clock64 ticks
+ * (100 MHz) into dev_words (device memory, >= 2 x grid uint64 words; a launch
+ * with a larger grid is not traced).  RdcCommLastLaunch: {grid, nb_scatter,
+ * nb_reduce, nb_gather, tile_bytes, algo} of the last allreduce launch
+ * (mesh roles: blocks [0, s) scatter, [s, s+r) reduce, the rest gather). */
+int RdcCommTraceNext(void* comm, void* dev_words, size_t nwords);
+int RdcCommLastLaunch(void* comm, uint64_t* out6);
+
 /* Single process driving n ranks (devices[i] = HIP device of rank i; devices
  * may repeat).  comms[i] receives rank i's handle.  scratch_bytes 0 = default. */
 int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes);

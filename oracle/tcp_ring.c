@@ -64,9 +64,11 @@ static void tune(int fd) {
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
 }
 
-/* rank r listens on port+r; connects to prev's listener (the r -> prev
- * link) and accepts next's connection (the next -> r link) */
-static void connect_ring(int rank, int n, int port, int* to_prev, int* from_next) {
+/* Listeners are made by the parent before the ranks fork (kernel-chosen
+ * ports unless -p is given), so every rank's listener exists before anyone
+ * connects: no port collisions and no loopback self-connect (a connect to a
+ * not-yet-listening port in the ephemeral range can open onto itself). */
+static int make_listener(int port, int* bound) {
     int ls = socket(AF_INET, SOCK_STREAM, 0);
     if (ls < 0) die("socket");
     int one = 1;
@@ -75,21 +77,29 @@ static void connect_ring(int rank, int n, int port, int* to_prev, int* from_next
     memset(&a, 0, sizeof(a));
     a.sin_family = AF_INET;
     a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-    a.sin_port = htons((uint16_t)(port + rank));
+    a.sin_port = htons((uint16_t)port);
     if (bind(ls, (struct sockaddr*)&a, sizeof(a)) < 0) die("bind");
     if (listen(ls, 4) < 0) die("listen");
+    socklen_t al = sizeof(a);
+    if (getsockname(ls, (struct sockaddr*)&a, &al) < 0) die("getsockname");
+    *bound = ntohs(a.sin_port);
+    return ls;
+}
+
+/* rank r connects to prev's listener (the r -> prev link) and accepts
+ * next's connection on its own (the next -> r link) */
+static void connect_ring(int rank, int n, int ls, const int* ports, int* to_prev, int* from_next) {
     const int prev = (rank - 1 + n) % n;
-    int s = -1;
-    for (int tries = 0; tries < 2000; ++tries) {
-        s = socket(AF_INET, SOCK_STREAM, 0);
-        struct sockaddr_in b = a;
-        b.sin_port = htons((uint16_t)(port + prev));
-        if (connect(s, (struct sockaddr*)&b, sizeof(b)) == 0) break;
-        close(s);
-        s = -1;
-        usleep(5000);
-    }
-    if (s < 0) die("connect");
+    struct sockaddr_in b;
+    memset(&b, 0, sizeof(b));
+    b.sin_family = AF_INET;
+    b.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    b.sin_port = htons((uint16_t)ports[prev]);
+    int s = socket(AF_INET, SOCK_STREAM, 0);
+    if (s < 0) die("socket");
+    if (connect(s, (struct sockaddr*)&b, sizeof(b)) != 0) die("connect");
+    struct pollfd p = {ls, POLLIN, 0};
+    if (poll(&p, 1, 60000) <= 0) die("accept wait");
     int c = accept(ls, NULL, NULL);
     if (c < 0) die("accept");
     close(ls);
@@ -177,8 +187,8 @@ static int cmp_d(const void* a, const void* b) {
     return x < y ? -1 : x > y;
 }
 
-static int run_rank(int rank, int n, uint64_t count, int dtype, int op, int iters, int warmup, int port,
-                    const char* outdir, int result_fd) {
+static int run_rank(int rank, int n, uint64_t count, int dtype, int op, int iters, int warmup, int ls,
+                    const int* ports, const char* outdir, int result_fd) {
     Ring R;
     memset(&R, 0, sizeof(R));
     R.n = n;
@@ -189,7 +199,7 @@ static int run_rank(int rank, int n, uint64_t count, int dtype, int op, int iter
     R.esz = rdc_oracle_dtype_size(dtype);
     rdc_oracle_split(0, (int64_t)count, n, R.cb, R.ce);
     if (rdc_oracle_ring_schedule(n, rank, R.rs_send, R.rs_recv, R.ag_send, R.ag_recv)) die("schedule");
-    connect_ring(rank, n, port, &R.to_prev, &R.from_next);
+    connect_ring(rank, n, ls, ports, &R.to_prev, &R.from_next);
     const size_t S = count * R.esz;
     char* input = (char*)malloc(S ? S : 1);
     char* buf = (char*)malloc(S ? S : 1);
@@ -245,7 +255,8 @@ int main(int argc, char** argv) {
         fprintf(stderr, "tcp_ring: bad arguments\n");
         return 2;
     }
-    if (port == 0) port = 20000 + (int)(getpid() % 20000);
+    int ls[RDC_ORACLE_MAX_RANKS], ports[RDC_ORACLE_MAX_RANKS];
+    for (int r = 0; r < n; ++r) ls[r] = make_listener(port ? port + r : 0, &ports[r]);
     int pfd[2];
     if (pipe(pfd) < 0) die("pipe");
     pid_t kids[RDC_ORACLE_MAX_RANKS];
@@ -254,10 +265,13 @@ int main(int argc, char** argv) {
         if (kids[r] < 0) die("fork");
         if (kids[r] == 0) {
             close(pfd[0]);
-            _exit(run_rank(r, n, count, dtype, op, iters, warmup, port, outdir, pfd[1]));
+            for (int q = 0; q < n; ++q)
+                if (q != r) close(ls[q]);
+            _exit(run_rank(r, n, count, dtype, op, iters, warmup, ls[r], ports, outdir, pfd[1]));
         }
     }
     close(pfd[1]);
+    for (int r = 0; r < n; ++r) close(ls[r]);
     double* t = (double*)calloc((size_t)(iters > 0 ? iters : 1), sizeof(double));
     size_t want = sizeof(double) * (size_t)iters, have = 0;
     while (have < want) {

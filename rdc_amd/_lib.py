@@ -56,6 +56,8 @@ def _load():
         "RdcCommBroadcast": (i, [vp, vp, sz, i, vp]),
         "RdcCommCheck": (i, [vp, vp]),
         "RdcCommProbe": (i, [vp, i, sz, i, vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]),
+        "RdcCommTraceNext": (i, [vp, vp, sz]),
+        "RdcCommLastLaunch": (i, [vp, ctypes.POINTER(u64)]),
         "RdcCommRank": (i, [vp]),
         "RdcCommSize": (i, [vp]),
         "RdcCommDevice": (i, [vp]),

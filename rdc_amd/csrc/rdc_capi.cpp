@@ -94,6 +94,13 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_HOST_ZC_BYTES") m.host_zc_bytes = parse_unit(val);
     else if (k == "RDC_COALESCE_FUSED") m.cfg.coalesce_fused = atoi(val) != 0;
     else if (k == "RDC_BCAST_SPLIT_BYTES") m.cfg.bcast_split_bytes = parse_unit(val);
+    else if (k == "RDC_MESH_SPLIT") {
+        int s = 0, r = 0;
+        if (sscanf(val, "%d,%d", &s, &r) != 2 || s < 1 || r < 1 || s + r > 15)
+            throw std::invalid_argument(std::string("rdc: RDC_MESH_SPLIT wants s,r sixteenths (s+r<=15), got ") + val);
+        m.cfg.mesh_split.s16 = s;
+        m.cfg.mesh_split.r16 = r;
+    }
     else if (k == "RDC_FUSE_BYTES_DIRECT") m.cfg.fuse_bytes_direct = std::max<size_t>(parse_unit(val), 1);
     else if (k == "RDC_P2P_SLOT_BYTES") m.cfg.p2p_slot_bytes = std::max<size_t>(parse_unit(val) / 4096 * 4096, 4096);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
@@ -206,7 +213,7 @@ int RdcInit(int argc, char** argv) {
                                      "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
                                      "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES",
                                      "RDC_P2P_SLOT_BYTES", "RDC_COALESCE_FUSED", "RDC_HOST_ZC_BYTES",
-                                     "RDC_FUSE_BYTES_DIRECT", "RDC_BCAST_SPLIT_BYTES"};
+                                     "RDC_FUSE_BYTES_DIRECT", "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT"};
         for (const char* k : keys) env_param(m, k);
         m.env_loaded = true;
         for (int i = 0; i < argc; ++i) {
@@ -534,6 +541,17 @@ int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, dou
     });
 }
 
+int RdcCommTraceNext(void* comm, void* dev_words, size_t nwords) {
+    return guard([&] { as_comm(comm)->TraceNext(static_cast<uint64_t*>(dev_words), dev_words ? nwords : 0); });
+}
+
+int RdcCommLastLaunch(void* comm, uint64_t* out6) {
+    return guard([&] {
+        if (!out6) throw std::invalid_argument("rdc: null argument");
+        as_comm(comm)->LastLaunch(out6);
+    });
+}
+
 int RdcCommRank(void* comm) { return comm ? static_cast<Communicator*>(comm)->rank() : -1; }
 int RdcCommSize(void* comm) { return comm ? static_cast<Communicator*>(comm)->size() : -1; }
 int RdcCommDevice(void* comm) { return comm ? static_cast<Communicator*>(comm)->device() : -1; }
@@ -548,7 +566,7 @@ int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes
         static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
                                      "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES", "RDC_P2P_SLOT_BYTES",
                                      "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT",
-                                     "RDC_BCAST_SPLIT_BYTES"};
+                                     "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT"};
         if (!m.inited && !m.env_loaded) {
             for (const char* k : keys) env_param(m, k);
             m.env_loaded = true;

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <new>
 #include <stdexcept>
 #include <string>
 
@@ -267,15 +268,21 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < i; ++j) shared |= devices[i] == devices[j];
     for (auto& c : cs) c->shared_gpu_ = shared;
-    P2PCtl* raw = new P2PCtl();  // value-initialised: all words 0
-    if (hipHostRegister(raw, sizeof(P2PCtl), hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+    // Pinned coherent pages of its own, not a registered heap object: a
+    // registration covers whole pages, and a heap object shares its first and
+    // last page with unrelated allocations that the runtime may pin and unpin
+    // for its own copies (one run saw an illegal address right after such a
+    // copy; the control block has lived in dedicated pages since).
+    void* mem = nullptr;
+    if (hipHostMalloc(&mem, sizeof(P2PCtl), hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) !=
+        hipSuccess) {
         (void)hipGetLastError();
-        delete raw;
-        throw std::runtime_error("rdc: cannot register the p2p control block for device access");
+        throw std::runtime_error("rdc: cannot allocate the p2p control block in pinned host memory");
     }
-    std::shared_ptr<P2PCtl> ctl(raw, [](P2PCtl* q) {
-        (void)hipHostUnregister(q);
-        delete q;
+    memset(mem, 0, sizeof(P2PCtl));
+    std::shared_ptr<P2PCtl> ctl(new (mem) P2PCtl(), [](P2PCtl* q) {
+        q->~P2PCtl();
+        (void)hipHostFree(q);
     });
     for (int i = 0; i < n; ++i) {
         cs[(size_t)i]->p2p_ctl_ = ctl;
@@ -465,13 +472,19 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         a.notify = notify_;
         a.notify_val = notify_val_;
         notify_ = nullptr;
+        trace_ = nullptr;  // one-shot launches are not traced
+        last_launch_[0] = (uint64_t)p.nb_scatter;
+        last_launch_[1] = (uint64_t)p.nb_scatter;
+        last_launch_[2] = last_launch_[3] = 0;
+        last_launch_[4] = p.tile_bytes;
+        last_launch_[5] = RDC_ALGO_ONESHOT;
         ++seq_;
         hip_check(ks.oneshot(a, p.nb_scatter, stream), "launch one-shot allreduce");
         return;
     }
     const std::vector<Piece> plan =
         PlanAllreduceRanges(n_, off, len, esz, layout(), algo, cfg_.tile_bytes,
-                            algo == RDC_ALGO_MESH ? mesh_blocks() : max_blocks());
+                            algo == RDC_ALGO_MESH ? mesh_blocks() : max_blocks(), cfg_.mesh_split);
     for (const Piece& p : plan) {
         CollArgs a;
         FillArgsCommon(&a);
@@ -487,9 +500,17 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         memcpy(a.tiles, p.tiles, sizeof(a.tiles));
         a.tile_bytes = p.tile_bytes;
         ++seq_;
+        const int grid = algo == RDC_ALGO_RING ? p.nb_scatter : p.nb_scatter + p.nb_reduce + p.nb_gather;
+        if (trace_ && trace_words_ >= 2 * (size_t)grid) a.trace = trace_;
+        last_launch_[0] = (uint64_t)grid;
+        last_launch_[1] = (uint64_t)p.nb_scatter;
+        last_launch_[2] = (uint64_t)(algo == RDC_ALGO_RING ? 0 : p.nb_reduce);
+        last_launch_[3] = (uint64_t)(algo == RDC_ALGO_RING ? 0 : p.nb_gather);
+        last_launch_[4] = p.tile_bytes;
+        last_launch_[5] = (uint64_t)algo;
         if (algo == RDC_ALGO_RING) {
             a.kind = RDC_KIND_RING;
-            hip_check(ks.ring(a, p.nb_scatter, stream), "launch ring allreduce");
+            hip_check(ks.ring(a, grid, stream), "launch ring allreduce");
         } else {
             a.nb_scatter = p.nb_scatter;
             a.nb_reduce = p.nb_reduce;
@@ -497,9 +518,10 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
             a.kind = RDC_KIND_MESH;
             a.units = units;
             a.nunits = nunits;
-            hip_check(ks.mesh(a, p.nb_scatter + p.nb_reduce + p.nb_gather, stream), "launch mesh allreduce");
+            hip_check(ks.mesh(a, grid, stream), "launch mesh allreduce");
         }
     }
+    trace_ = nullptr;  // one call only
 }
 
 // Staging image of the coalesced path, grown on demand (never shrinks).

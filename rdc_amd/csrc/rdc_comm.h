@@ -37,6 +37,7 @@ struct CommConfig {
     bool coalesce_fused = true;                 // coalesced mesh reads/writes user buffers directly (no image)
     size_t fuse_bytes_direct = (size_t)16 << 30;  // ... in groups of up to this many data bytes
     size_t bcast_split_bytes = (size_t)1 << 20;   // broadcast pieces from this size: root -> forwarders -> ranks
+    MeshSplit mesh_split;                          // mesh roles in sixteenths of the grid (RDC_MESH_SPLIT=s,r)
 };
 
 struct KernelSet;
@@ -94,6 +95,17 @@ public:
     // Overwrites scratch contents only, which every collective rewrites.
     double Probe(int mode, size_t* bytes, int reps, hipStream_t stream);  // *bytes: asked in, used out
 
+    // diagnostics: the next allreduce's launches (mesh or ring) record per
+    // block {start, end} wall_clock64 ticks into dev_words (>= 2 x grid words);
+    // LastLaunch() = {grid, nb_scatter, nb_reduce, nb_gather, tile_bytes, algo}
+    void TraceNext(uint64_t* dev_words, size_t nwords) {
+        trace_ = dev_words;
+        trace_words_ = nwords;
+    }
+    void LastLaunch(uint64_t* out6) const {
+        for (int i = 0; i < 6; ++i) out6[i] = last_launch_[i];
+    }
+
     int rank() const { return rank_; }
     int size() const { return n_; }
     int device() const { return device_; }
@@ -143,6 +155,9 @@ private:
     uint32_t* notify_ = nullptr;    // armed: device address of the pinned notify word
     uint32_t notify_val_ = 0;
     uint32_t notify_token_ = 0;
+    uint64_t* trace_ = nullptr;     // TraceNext
+    size_t trace_words_ = 0;
+    uint64_t last_launch_[6] = {};
     size_t slot_bytes_ = 0, region_bytes_ = 0, flag_bytes_ = 0;
     uint32_t max_tiles_ = 0;
     uint32_t seq_ = 0;

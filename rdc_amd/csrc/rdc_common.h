@@ -92,9 +92,10 @@ struct CollArgs {
     uint32_t* launch_kind;               // local: kind of the last completed launch
     int kind;                            // this launch's RDC_KIND_*
     int bcast_split;                     // broadcast: root -> forwarder per tile -> other ranks (n >= 3)
-    uint64_t half_bytes;                // one-shot: offset of the slot half used by odd seq
+    uint64_t half_bytes;                 // one-shot: offset of the slot half used by odd seq
     uint64_t total_bytes;                // one-shot: whole buffer bytes
     const void* units;                   // coalesced mesh: device PackUnit table (off/len are packed
     int nunits;                          //   offsets; user bytes reached through the units), else null
     uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up
+    uint64_t* trace;                     // optional (mesh/ring): per block {start, end} wall_clock64 ticks
 };

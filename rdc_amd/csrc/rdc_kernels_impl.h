@@ -619,10 +619,21 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint32_t seq) {
     }
 }
 
+// RdcCommTraceNext: every block of the traced launch records when it started
+// and when its role finished (wall_clock64, 100 MHz) — role timelines for tuning
+__device__ __forceinline__ void trace_block(const CollArgs& a, uint64_t t0) {
+    if (a.trace && threadIdx.x == 0) {
+        a.trace[2 * blockIdx.x] = t0;
+        a.trace[2 * blockIdx.x + 1] = wall_clock64();
+    }
+}
+
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
+    const uint64_t t0 = wall_clock64();
     const uint32_t seq = launch_seq(a);
     mesh_body<OP, T, NMAX>(a, seq);
+    trace_block(a, t0);
     launch_done(a, seq);
 }
 
@@ -635,8 +646,10 @@ __global__ __launch_bounds__(kBlock) void k_oneshot(CollArgs a) {
 
 template <int OP, typename T>
 __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
+    const uint64_t t0 = wall_clock64();
     const uint32_t seq = launch_seq(a);
     ring_body<OP, T>(a, seq);
+    trace_block(a, t0);
     launch_done(a, seq);
 }
 

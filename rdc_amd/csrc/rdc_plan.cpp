@@ -33,7 +33,8 @@ void SplitRanges(int64_t count, int n, int64_t* b, int64_t* e) {
     }
 }
 
-void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blocks, Piece* p) {
+void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blocks, Piece* p, MeshSplit split) {
+    const int s16 = std::min(std::max(split.s16, 1), 14), r16 = std::min(std::max(split.r16, 1), 15 - s16);
     size_t t = cfg_tile;
     if (t == 0) {
         // ring: each block walks 2(n-1) hand-offs per tile, so one tile per
@@ -48,7 +49,7 @@ void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blo
         if (algo == RDC_ALGO_RING) {
             want = chunk_bytes / G;
         } else {
-            want = chunk_bytes / (2 * std::max<size_t>(1, G * 3 / 8));
+            want = chunk_bytes / (2 * std::max<size_t>(1, G * (size_t)r16 / 16));
             lo = (size_t)64 << 10;
         }
         t = std::min<size_t>(std::max<size_t>(want, lo), (size_t)1 << 20);
@@ -63,8 +64,8 @@ void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blo
         return;
     }
     const int items_s = (n - 1) * T;
-    const int s = std::max(1, std::min(items_s, G * 3 / 8));
-    const int r = std::max(1, std::min(T, G * 3 / 8));
+    const int s = std::max(1, std::min(items_s, G * s16 / 16));
+    const int r = std::max(1, std::min(T, G * r16 / 16));
     const int g = std::max(1, std::min(items_s, G - s - r));
     p->nb_scatter = s;
     p->nb_reduce = r;
@@ -72,7 +73,7 @@ void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blo
 }
 
 std::vector<Piece> PlanAllreduceRanges(int n, const uint64_t* off, const uint64_t* len, size_t esz,
-                                       const Layout& L, int algo, size_t cfg_tile, int max_blocks) {
+                                       const Layout& L, int algo, size_t cfg_tile, int max_blocks, MeshSplit split) {
     std::vector<Piece> out;
     if (n <= 1 || esz == 0) return out;
     uint64_t maxlen = 0;
@@ -95,7 +96,7 @@ std::vector<Piece> PlanAllreduceRanges(int n, const uint64_t* off, const uint64_
             p.mis[c] = (uint32_t)(p.off[c] % 16);
             chunk_max = std::max<size_t>(chunk_max, p.len[c]);
         }
-        PlanTiles(chunk_max, n, algo, cfg_tile, max_blocks, &p);
+        PlanTiles(chunk_max, n, algo, cfg_tile, max_blocks, &p, split);
         for (int c = 0; c < n; ++c) p.tiles[c] = (int)((p.len[c] + p.tile_bytes - 1) / p.tile_bytes);
         out.push_back(p);
     }

@@ -38,8 +38,16 @@ struct Piece {
     int nb_scatter, nb_reduce, nb_gather;  // mesh roles; ring uses nb_scatter as its grid
 };
 
+// Mesh role split of the grid in sixteenths: scatter s16/16, reduce r16/16,
+// gather the rest (default 4 / 8 / 4: tools/mesh_split_sweep.sh, 2 ranks on one GPU,
+// 1 GiB 1.69 -> 1.54 ms at 512 blocks against 6 / 6 / 4 — the reduce role has
+// the most work per byte: n loads, n stores).
+struct MeshSplit {
+    int s16 = 4, r16 = 8;
+};
 // tile size and grid for a piece whose largest chunk is chunk_bytes
-void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blocks, Piece* p);
+void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blocks, Piece* p,
+               MeshSplit split = MeshSplit());
 
 // Every launch of an allreduce of `count` elements of `esz` bytes.
 std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout& L, int algo, size_t cfg_tile,
@@ -65,7 +73,8 @@ std::vector<Piece> PlanBroadcast(uint64_t bytes, const Layout& L, size_t cfg_til
 // of one buffer (PlanAllreduce is this with the Split ranges; the coalesced
 // path passes the packed chunk ranges).  Each range length is a multiple of esz.
 std::vector<Piece> PlanAllreduceRanges(int n, const uint64_t* off, const uint64_t* len, size_t esz,
-                                       const Layout& L, int algo, size_t cfg_tile, int max_blocks);
+                                       const Layout& L, int algo, size_t cfg_tile, int max_blocks,
+                                       MeshSplit split = MeshSplit());
 Piece PlanOneshotRanges(int n, const uint64_t* off, const uint64_t* len, uint64_t total, const Layout& L,
                         size_t cfg_tile, int max_blocks);
 
