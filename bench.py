@@ -127,30 +127,32 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps):
     """The other BASELINE.json multi-GPU configs on the same communicator,
     after the timed region (informational): cfg4 = fp16 allreduce of a buffer
     of S bytes, cfg5 = 1024 buckets of S/1024 bytes fp32 in one coalesced
-    call.  ms per step = max over ranks of the wall time of `steps` calls."""
+    call, cfg1 = a 256 MiB fp32 buffer (with the sizes below it as
+    `sizes_fp32`).  ms per step = max over ranks of the wall time of `steps`
+    calls."""
     from rdc_amd._lib import check_call
     out = {}
 
-    def timed(one):
+    def timed(one, nsteps=steps):
         for _ in range(2):
             one()
         torch.cuda.synchronize()
         comm.check(sp)
         dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(steps):
+        for _ in range(nsteps):
             one()
         torch.cuda.synchronize()
         dist.barrier()
-        t = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64)
+        t = torch.tensor([(time.perf_counter() - t0) / nsteps], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         comm.check(sp)
         return float(t[0]) * 1e3
 
-    def entry(ms, nbytes, what):
+    def entry(ms, nbytes, what, nsteps=steps):
         bb = nbytes / (ms * 1e-3) / 1e9 * 2 * (world - 1) / world
         return {"workload": what, "bytes_per_gpu": nbytes, "ms_per_step": round(ms, 4), "busbw_GBps": round(bb, 2),
-                "steps": steps}
+                "steps": nsteps}
 
     try:
         h = torch.empty(S // 2, dtype=torch.float16, device="cuda")
@@ -171,6 +173,26 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps):
         ms = timed(lambda: check_call(lib.RdcCommAllreduceCoalesced(comm.handle, ptrs, cnts, K, 6, 2, 0, sp)))
         out["cfg5_buckets"] = entry(ms, per * 4 * K, "%d x %d KiB float32 buckets, one coalesced call "
                                                      "(test/mallreduce.cc shape)" % (K, per * 4 >> 10))
+        del bks
+        # cfg1's 256 MiB fp32 buffer and the sizes below it (prefixes of one
+        # buffer): where the mesh's per-launch fill / drain and the one-shot
+        # hand-off decide the rate, for the next round's size thresholds
+        big = min(S, 256 << 20)
+        f = torch.empty(big // 4, dtype=torch.float32, device="cuda")
+        rdc_amd.fill_(f, 0x5EED0000, rank)
+        sizes = {}
+        for nb in (64 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, big):
+            if nb > big:
+                continue
+            ns = max(steps, 50) if nb <= (16 << 20) else steps  # small calls: more of them
+            ms = timed(lambda: check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(f.data_ptr()),
+                                                                 nb // 4, 6, 2, 0, sp)), ns)
+            e = entry(ms, nb, "in-place allreduce(sum) of %d KiB float32" % (nb >> 10), ns)
+            sizes[str(nb)] = {k: e[k] for k in ("ms_per_step", "busbw_GBps", "steps")}
+            if nb == (256 << 20):
+                out["cfg1_256MiB"] = e
+        out["sizes_fp32"] = sizes
+        del f
     except Exception as e:  # informational: never costs the main line
         out["error"] = str(e)
     return out
