@@ -227,6 +227,29 @@ def rccl_compare(S, world, rank, local, dist, torch, steps):
     return res
 
 
+def cpu_tcp_ring(S, world, rank, dist):
+    """The reference's CPU ring allreduce over loopback TCP (oracle/tcp_ring,
+    the C restatement of TryAllreduceRing) at this run's rank
+    count, on a bounded 64 MiB fp32 sample, rank 0 only, after every GPU
+    measurement: the north star's CPU figure beside the N>1 line (a reported
+    baseline, informational)."""
+    import subprocess
+    res = None
+    if rank == 0:
+        exe = os.path.join(ROOT, "oracle", "tcp_ring")
+        nb = min(S, 64 << 20)
+        try:
+            p = subprocess.run([exe, "-n", str(world), "-c", str(nb // 4), "-i", "3", "-w", "1"], capture_output=True,
+                               text=True, timeout=120)
+            lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+            res = json.loads(lines[-1]) if lines else {"error": "rc=%d: %s" % (p.returncode, p.stderr[-300:])}
+            res["sample"] = "%d ranks as processes, one thread each, %d MiB fp32, median of 3 calls" % (world, nb >> 20)
+        except Exception as e:  # noqa: BLE001 - informational only
+            res = {"error": str(e)}
+    dist.barrier()
+    return res
+
+
 def trace_roles(lib, comm, buf, count, dt_enum, sp, dist, torch):
     """One traced allreduce (RdcCommTraceNext) after the timed region: when
     each block role started and finished, relative to the launch's first
@@ -401,6 +424,9 @@ def main():
         extra = time_extra_configs(_LIB, comm, S, world, rank, sp, dist, torch, args.extra_steps)
     if world > 1 and args.buckets == 1 and args.algo == "auto" and args.rccl_steps > 0 and args.dtype == "float32":
         rccl = rccl_compare(S, world, rank, local, dist, torch, args.rccl_steps)
+    tcp = None
+    if world > 1 and args.cpu_seconds > 0:
+        tcp = cpu_tcp_ring(S, world, rank, dist)
 
     # spot check (outside the timed region): N=1 reduce result vs oracle on a slice
     check = None
@@ -487,6 +513,8 @@ def main():
         out["extra_configs"] = extra
     if rccl is not None:
         out["rccl_comparison"] = rccl
+    if tcp is not None:
+        out["cpu_tcp_ring"] = tcp
     if check is not None:
         out["oracle_check"] = check
     print(json.dumps(out), flush=True)

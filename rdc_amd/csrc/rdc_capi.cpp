@@ -710,8 +710,12 @@ int RdcNewBuffer(void** out, void* addr, size_t size, int pinned) {
         std::unique_ptr<BufferH> b(new BufferH());
         b->addr = addr;
         b->size = size;
-        if (pinned && size && !is_device_pointer(addr)) {
-            // a performance hint: an unregistrable range stays pageable
+        const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
+        if (pinned && size && !is_device_pointer(addr) && (uintptr_t)addr % page == 0 && size % page == 0) {
+            // a performance hint: an unregistrable range stays pageable.  Whole
+            // pages only: a registration covers whole pages, and pages shared
+            // with unrelated heap objects can be pinned and unpinned by the
+            // runtime's own copies behind this registration's back
             b->registered = hipHostRegister(addr, size, hipHostRegisterDefault) == hipSuccess;
             (void)hipGetLastError();
         }
