@@ -290,10 +290,13 @@ def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
     """Measured link rates (outside the timed region, every rank idle): the
     copy kernel the collectives use pushes nbytes from each GPU into
     (a) rank+1 only - one link, one direction, every link busy in a ring;
-    (b) every peer at once - all n-1 links out of each GPU (the mesh's egress).
+    (b) every peer at once - all n-1 links out of each GPU (the mesh's egress);
+    then the same two reading instead (pull: remote loads into local scratch),
+    the data for choosing push or pull hand-offs on real xGMI.
     Slowest rank's rate.  On a 1-GPU box the ranks share one HBM."""
     out = {}
-    for mode, key in ((0, "one_link_one_direction_GBps"), (1, "all_links_egress_GBps")):
+    for mode, key in ((0, "one_link_one_direction_GBps"), (1, "all_links_egress_GBps"),
+                      (2, "pull_one_link_GBps"), (3, "pull_all_links_GBps")):
         ms, used = ctypes.c_double(), ctypes.c_size_t()
         rc = lib.RdcCommProbe(comm.handle, mode, nbytes, reps, sp, ctypes.byref(ms), ctypes.byref(used))
         if rc != 0:
@@ -301,11 +304,11 @@ def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
         per_target = used.value
         t = torch.tensor([ms.value], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ntarget = 1 if mode == 0 else int(os.environ.get("WORLD_SIZE", "1")) - 1
+        ntarget = 1 if mode in (0, 2) else int(os.environ.get("WORLD_SIZE", "1")) - 1
         out[key] = round(per_target * ntarget / (float(t[0]) * 1e-3) / 1e9, 2)
         dist.barrier()
     out["bytes_per_target"] = per_target
-    out["kernel"] = "k_push (block_copy, 16-B non-temporal remote stores)"
+    out["kernel"] = "k_push (block_copy, 16-B non-temporal lanes; push = remote stores, pull = remote loads)"
     return out
 
 

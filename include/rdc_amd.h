@@ -165,7 +165,8 @@ int RdcCommAllocKind(void* comm);
  * from this rank's scratch into peers' scratch `reps` times on `stream`, all
  * targets at once, with the copy kernel the collectives use for remote
  * stores.  mode 0: rank+1 only (one link, one direction); mode 1: every peer
- * (all n-1 links out of this GPU).  *ms_out = average ms per round;
+ * (all n-1 links out of this GPU); modes 2 / 3: the same links read instead
+ * (pull from rank+1 / from every peer into local scratch).  *ms_out = average ms per round;
  * *bytes_out (may be NULL) = bytes per target actually pushed (clamped to
  * the scratch slot).  Call it
  * between collectives with every rank idle (e.g. after a barrier): it

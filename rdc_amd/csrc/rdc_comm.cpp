@@ -682,9 +682,10 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
 double Communicator::Probe(int mode, size_t* bytes_io, int reps, hipStream_t stream) {
     size_t bytes = *bytes_io;
     if (n_ == 1) throw std::invalid_argument("rdc: probe needs 2 or more ranks");
-    if (mode != 0 && mode != 1) throw std::invalid_argument("rdc: probe mode is 0 (next rank) or 1 (all peers)");
-    bytes = std::min(bytes, region_bytes_ - (size_t)RDC_SLOT_ALIGN);  // source: my own AG region
-    if (mode == 1) bytes = std::min(bytes, slot_bytes_ - (size_t)RDC_SLOT_ALIGN);
+    if (mode < 0 || mode > 3)
+        throw std::invalid_argument("rdc: probe mode is 0 / 1 (push to next rank / all peers), 2 / 3 (pull)");
+    bytes = std::min(bytes, region_bytes_ - (size_t)RDC_SLOT_ALIGN);  // source: an AG region
+    if (mode == 1 || mode == 3) bytes = std::min(bytes, slot_bytes_ - (size_t)RDC_SLOT_ALIGN);
     bytes &= ~(size_t)255;
     if (bytes == 0 || reps <= 0) throw std::invalid_argument("rdc: probe needs bytes and reps");
     *bytes_io = bytes;
@@ -694,9 +695,18 @@ double Communicator::Probe(int mode, size_t* bytes_io, int reps, hipStream_t str
     int nd = 0;
     if (mode == 0) {
         t.dst[nd++] = peer_scratch_[(rank_ + 1) % n_];  // the whole RS region of the next rank
-    } else {
+    } else if (mode == 1) {
         for (int k = 1; k < n_; ++k)  // my slot in every peer's RS region
             t.dst[nd++] = peer_scratch_[(rank_ + k) % n_] + (size_t)rank_ * slot_bytes_;
+    } else if (mode == 2) {  // the next rank's AG region into my RS region (reads over one link)
+        t.src[nd] = peer_ag_[(rank_ + 1) % n_];
+        t.dst[nd++] = scratch_;
+    } else {  // every peer's AG region into my RS slots (reads over all n-1 links)
+        for (int k = 1; k < n_; ++k) {
+            const int p = (rank_ + k) % n_;
+            t.src[nd] = peer_ag_[p] + (size_t)rank_ * slot_bytes_;
+            t.dst[nd++] = scratch_ + (size_t)p * slot_bytes_;
+        }
     }
     hipEvent_t e0, e1;
     hip_check(hipEventCreate(&e0), "event");

@@ -26,9 +26,11 @@ hipError_t launch_pack(const PackUnit* units, int nunits, char* image, int unpac
 // zeroed device counter owned by the stream (reset by that last block).
 hipError_t launch_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s, uint32_t* arrive = nullptr,
                        uint64_t* word = nullptr, uint64_t value = 0);
-// xGMI probe: block b pushes its share of `bytes` from src into dsts[b % ndst]
+// xGMI probe: block b copies its share of `bytes` from src (or srcs[b % ndst]
+// when set: remote reads) into dsts[b % ndst]
 struct PushTargets {
     char* dst[RDC_MAX_RANKS];
+    const char* src[RDC_MAX_RANKS];
 };
 hipError_t launch_push(const PushTargets& t, int ndst, const void* src, uint64_t bytes, int grid, hipStream_t s);
 hipError_t launch_fill(void* buf, uint64_t count, int dtype, uint64_t seed, int rank, hipStream_t s);

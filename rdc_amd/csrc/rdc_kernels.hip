@@ -109,7 +109,8 @@ __global__ __launch_bounds__(kBlock) void k_copy(char* __restrict__ dst, const c
 // ================================================================ probe ===
 // Link probe (Communicator::Probe): the blocks are split evenly over the ndst
 // targets; each target receives the same `bytes` from src with remote
-// stores (16-B non-temporal lanes), all targets concurrently.
+// stores (16-B non-temporal lanes), all targets concurrently.  With t.src[d]
+// set the blocks read that (remote) source instead: pull instead of push.
 __global__ __launch_bounds__(kBlock) void k_push(PushTargets t, int ndst, const char* __restrict__ src,
                                                  uint64_t bytes) {
     const int per = gridDim.x / ndst;
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(kBlock) void k_push(PushTargets t, int ndst, const 
     if (b >= per) return;
     constexpr uint64_t kStep = 64 << 10;
     for (uint64_t off = (uint64_t)b * kStep; off < bytes; off += (uint64_t)per * kStep)
-        block_copy(t.dst[d] + off, src + off, bytes - off < kStep ? bytes - off : kStep);
+        block_copy(t.dst[d] + off, (t.src[d] ? t.src[d] : src) + off, bytes - off < kStep ? bytes - off : kStep);
 }
 
 // ================================================================= fill ===

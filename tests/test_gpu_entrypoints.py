@@ -60,6 +60,7 @@ def test_bench_torchrun_two_ranks():
     assert out["config"]["bytes_per_gpu"] == 64 << 20
     probe = out["roofline"]["xgmi_probe"]
     assert probe["one_link_one_direction_GBps"] > 0 and probe["all_links_egress_GBps"] > 0, probe
+    assert probe["pull_one_link_GBps"] > 0 and probe["pull_all_links_GBps"] > 0, probe
     assert out["roofline"]["frac_of_measured"] > 0
 
 
