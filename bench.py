@@ -123,6 +123,47 @@ def time_ring(lib, comm, buf, count, dt_enum, sp, dist, torch, steps):
     return float(t[0]) * 1e3
 
 
+def mesh_tuning(lib, comm, S, dt_enum, esz, world, rank, sp, dist, torch, steps):
+    """ms per S-byte allreduce for a few mesh role splits and grids
+    (RdcCommTune), max over ranks: which knobs the next round should move on
+    THIS node (the defaults were tuned with every rank on one HBM).  Runs
+    last: the communicator keeps the last shape."""
+    from rdc_amd._lib import check_call
+    import rdc_amd
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    shapes = [(4, 8, 0), (3, 9, 0), (5, 8, 0), (6, 6, 0), (3, 10, 0), (4, 8, cus)]
+    if torch.cuda.device_count() >= world:  # one rank per GPU: more blocks than CUs stay resident
+        shapes.append((4, 8, 3 * cus))
+    out = {}
+    try:
+        buf = torch.empty(S // esz, dtype=torch.float32 if esz == 4 else torch.float16, device="cuda")
+        rdc_amd.fill_(buf, 0x5EED0000, rank)
+        for s16, r16, grid in shapes:
+            check_call(lib.RdcCommTune(comm.handle, s16, r16, grid, 0))
+
+            def one():
+                check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), buf.numel(), dt_enum,
+                                                  2, 2, sp))
+            for _ in range(2):
+                one()
+            torch.cuda.synchronize()
+            comm.check(sp)
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                one()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            comm.check(sp)
+            out["split %d,%d grid %s" % (s16, r16, grid or "auto")] = round(float(t[0]) * 1e3, 4)
+        del buf
+    except Exception as e:  # noqa: BLE001 - informational only
+        out["error"] = str(e)
+    return out
+
+
 def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps):
     """The other BASELINE.json multi-GPU configs on the same communicator,
     after the timed region (informational): cfg4 = fp16 allreduce of a buffer
@@ -427,6 +468,10 @@ def main():
         extra = time_extra_configs(_LIB, comm, S, world, rank, sp, dist, torch, args.extra_steps)
     if world > 1 and args.buckets == 1 and args.algo == "auto" and args.rccl_steps > 0 and args.dtype == "float32":
         rccl = rccl_compare(S, world, rank, local, dist, torch, args.rccl_steps)
+    tuning = None
+    if world > 1 and args.buckets == 1 and args.algo == "auto" and args.extra_steps > 0 and args.dtype == "float32":
+        torch.cuda.empty_cache()
+        tuning = mesh_tuning(_LIB, comm, S, dt_enum, esz, world, rank, sp, dist, torch, args.extra_steps)
     tcp = None
     if world > 1 and args.cpu_seconds > 0:
         tcp = cpu_tcp_ring(S, world, rank, dist)
@@ -512,6 +557,8 @@ def main():
                                         "main region; bit-identical result"}
     if roles is not None:
         out["role_timeline"] = roles
+    if tuning is not None:
+        out["mesh_tuning_ms"] = tuning
     if extra is not None:
         out["extra_configs"] = extra
     if rccl is not None:

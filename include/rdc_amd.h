@@ -173,6 +173,15 @@ int RdcCommAllocKind(void* comm);
  * overwrites scratch, which every collective rewrites before reading. */
 int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, double* ms_out, size_t* bytes_out);
 
+/* Re-tune one communicator between collectives (every rank of it must pass
+ * the same values; the plan is made per call on each host): mesh role split
+ * in sixteenths of the grid (RDC_MESH_SPLIT; mesh_s16 + mesh_r16 <= 15, the
+ * gather role gets the rest), grid size (RDC_NBLOCKS; 0 = auto) and tile
+ * bytes (RDC_TILE_BYTES; 0 = auto, else a multiple of 256).  Results stay
+ * bit-identical (the fold order is per element).  No reference counterpart:
+ * the reference's schedule has no such knobs; bench.py sweeps them at N>1. */
+int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t tile_bytes);
+
 /* Diagnostics (bench.py at N > 1): the next allreduce on `comm` (mesh or
  * ring schedule) records, per block, {start, end} wall_clock64 ticks
  * (100 MHz) into dev_words (device memory, >= 2 x grid uint64 words; a launch

@@ -57,6 +57,7 @@ def _load():
         "RdcCommCheck": (i, [vp, vp]),
         "RdcCommProbe": (i, [vp, i, sz, i, vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]),
         "RdcCommTraceNext": (i, [vp, vp, sz]),
+        "RdcCommTune": (i, [vp, i, i, i, sz]),
         "RdcCommLastLaunch": (i, [vp, ctypes.POINTER(u64)]),
         "RdcCommRank": (i, [vp]),
         "RdcCommSize": (i, [vp]),

@@ -165,6 +165,12 @@ class Comm(object):
         self.irecv(buf, src_rank).wait()
         return buf
 
+    def tune(self, mesh_s16=4, mesh_r16=8, max_blocks=0, tile_bytes=0):
+        """Mesh role split (sixteenths of the grid), grid (0 = auto) and tile
+        bytes (0 = auto) for the following collectives (RdcCommTune); every
+        rank must pass the same values.  Results stay bit-identical."""
+        check_call(_LIB.RdcCommTune(self.handle, int(mesh_s16), int(mesh_r16), int(max_blocks), int(tile_bytes)))
+
     def check(self, stream=None):
         """Synchronise the stream and raise if a device-side wait failed."""
         if stream is None:

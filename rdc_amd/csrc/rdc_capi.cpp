@@ -533,6 +533,10 @@ int RdcCommCheck(void* comm, void* stream) {
     return guard([&] { as_comm(comm)->Check(static_cast<hipStream_t>(stream)); });
 }
 
+int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t tile_bytes) {
+    return guard([&] { as_comm(comm)->Tune(mesh_s16, mesh_r16, max_blocks, tile_bytes); });
+}
+
 int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, double* ms_out, size_t* bytes_out) {
     return guard([&] {
         if (!ms_out) throw std::invalid_argument("rdc: null argument");

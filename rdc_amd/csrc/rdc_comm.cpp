@@ -679,6 +679,16 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
     }
 }
 
+void Communicator::Tune(int s16, int r16, int max_blocks, size_t tile_bytes) {
+    if (s16 < 1 || r16 < 1 || s16 + r16 > 15 || max_blocks < 0)
+        throw std::invalid_argument("rdc: mesh split wants s,r sixteenths with s+r <= 15 and a grid >= 0");
+    if (tile_bytes % RDC_SLOT_ALIGN) throw std::invalid_argument("rdc: tile bytes must be a multiple of 256");
+    cfg_.mesh_split.s16 = s16;
+    cfg_.mesh_split.r16 = r16;
+    cfg_.max_blocks = max_blocks;
+    cfg_.tile_bytes = tile_bytes;
+}
+
 double Communicator::Probe(int mode, size_t* bytes_io, int reps, hipStream_t stream) {
     size_t bytes = *bytes_io;
     if (n_ == 1) throw std::invalid_argument("rdc: probe needs 2 or more ranks");

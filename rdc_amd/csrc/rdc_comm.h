@@ -95,6 +95,12 @@ public:
     // Overwrites scratch contents only, which every collective rewrites.
     double Probe(int mode, size_t* bytes, int reps, hipStream_t stream);  // *bytes: asked in, used out
 
+    // tuning between collectives (stream order keeps launches consistent: the
+    // plan is made on the host per call, every rank must use the same values):
+    // mesh role split in sixteenths (s16 + r16 <= 15), grid (0 = auto), tile
+    // bytes (0 = auto).  Throws std::invalid_argument on a bad split.
+    void Tune(int s16, int r16, int max_blocks, size_t tile_bytes);
+
     // diagnostics: the next allreduce's launches (mesh or ring) record per
     // block {start, end} wall_clock64 ticks into dev_words (>= 2 x grid words);
     // LastLaunch() = {grid, nb_scatter, nb_reduce, nb_gather, tile_bytes, algo}

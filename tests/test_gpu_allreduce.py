@@ -100,6 +100,34 @@ def test_group_multi_piece(group2, algo):
         assert same_bits(got[r], want, O.DT_FLOAT32)
 
 
+@pytest.mark.parametrize("s16,r16,grid,tile", [(1, 14, 0, 0), (7, 1, 24, 0), (3, 10, 48, 64 << 10),
+                                               (5, 5, 16, 16 << 10)])
+def test_group_tuned_mesh_bit_exact(group3, s16, r16, grid, tile):
+    """RdcCommTune (role split, grid, tile) changes only who moves which
+    bytes: the result stays the oracle's bits; defaults restored after."""
+    rng = np.random.default_rng(s16 * 100 + r16)
+    try:
+        for c in group3:
+            c.tune(s16, r16, grid, tile)
+        for count in (3, 70001, (3 << 20) // 4 + 5):
+            inputs = [rng.standard_normal(count).astype(np.float32) for _ in range(3)]
+            want = O.expected_allreduce(inputs, O.DT_FLOAT32, O.OP_SUM)
+            got = run_group(group3, inputs, O.DT_FLOAT32, O.OP_SUM, 2, pads=[0, 1, 2])
+            for r in range(3):
+                assert same_bits(got[r], want, O.DT_FLOAT32), (count, r)
+    finally:
+        for c in group3:
+            c.tune()
+
+
+def test_tune_rejects_bad_split(group2):
+    import rdc_amd
+    with pytest.raises(rdc_amd.RdcError):
+        group2[0].tune(8, 8)
+    with pytest.raises(rdc_amd.RdcError):
+        group2[0].tune(4, 8, 0, 100)
+
+
 def test_group_repeated_calls(group3):
     """seq-numbered flags: many back-to-back launches on the same communicator,
     schedules interleaved (one-shot parity halves, gates after one-shot)."""
