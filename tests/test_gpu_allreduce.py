@@ -340,6 +340,26 @@ def test_mp_full_size_cfg2():
             assert open(os.path.join(tmp, "case%d_rank%d.sha" % (i, r))).read() == h, (i, r)
 
 
+def test_mp_full_size_cfg3_cfg4_eight_ranks():
+    """BASELINE cfg3 / cfg4 at full size and rank count: 1 GiB fp32 and 1 GiB
+    fp16 allreduces over 8 processes (sharing GPU 0 here: 32 blocks each so
+    all 8 grids stay resident), each rank's result checked bit-exact (sha256)
+    against the oracle's ring — the exact launch plan of the 8-GPU run
+    (NMAX = 8 kernels, one launch per call), only the grid is smaller."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import hashlib
+    cases = [{"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 2, "digest": True},
+             {"count": (1 << 30) // 2, "dtype": 10, "op": 2, "algo": 2, "digest": True}]
+    tmp = run_mp(8, cases, timeout=400, env_extra={"RDC_NBLOCKS": "32", "RDC_SCRATCH_BYTES": "4080M"})
+    for i, c in enumerate(cases):
+        want = expected_for(c, 8)
+        h = hashlib.sha256(np.frombuffer(want[0].tobytes(), dtype=np.uint8).tobytes()).hexdigest()
+        del want
+        for r in range(8):
+            assert open(os.path.join(tmp, "case%d_rank%d.sha" % (i, r))).read() == h, (i, r)
+
+
 def test_mp_many_small_buckets_cfg5_shape():
     """test/mallreduce.cc shape: back-to-back 1 MiB fp32 allreduces on one buffer."""
     if not torch.cuda.is_available():
