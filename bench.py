@@ -452,29 +452,58 @@ def main():
 
     # the reference's own schedule on the same buffer, after the timed region
     # (informational: same bits, one link direction per GPU)
+    # Everything after the timed region is informational.  A failure there
+    # (e.g. a device wait timing out) must not cost the headline line: every
+    # extra runs guarded, the ranks agree on failure over the CPU process
+    # group, and once one has failed the communicator is unusable, so the
+    # remaining extras that need it are skipped.
+    extras_error = {}
+
+    def guarded(name, fn, needs_comm=True):
+        if needs_comm and extras_error:
+            return None
+        res, failed = None, 0.0
+        try:
+            res = fn()
+        except Exception as e:  # noqa: BLE001 - diagnostics only
+            extras_error[name] = str(e)[:300]
+            failed = 1.0
+        if world > 1:
+            f = torch.tensor([failed], dtype=torch.float64)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            if float(f[0]) > 0 and name not in extras_error:
+                extras_error[name] = "failed on another rank"
+        return None if name in extras_error else res
+
     roles = None
     if world > 1 and args.buckets == 1 and args.algo == "auto":
-        try:
-            roles = trace_roles(_LIB, comm, buf, count, dt_enum, sp, dist, torch)
-        except Exception as e:  # noqa: BLE001 - diagnostics only
-            roles = {"error": str(e)}
+        roles = guarded("role_timeline", lambda: trace_roles(_LIB, comm, buf, count, dt_enum, sp, dist, torch))
     ring_cmp = None
-    if world > 1 and args.buckets == 1 and args.algo == "auto" and args.ring_steps > 0:
-        ring_cmp = time_ring(_LIB, comm, buf, count, dt_enum, sp, dist, torch, args.ring_steps)
+    ring_shared = world > 2 and torch.cuda.device_count() < world
+    if ring_shared and args.buckets == 1 and args.algo == "auto" and args.ring_steps > 0:
+        # rehearsal with >2 ranks on one GPU: the ring's full-grid launches of
+        # every rank are not all resident at once there (4 ranks on one GPU
+        # timed out), so the ring is left to the one-GPU-per-rank node
+        ring_cmp = "%d ranks share %d GPU(s)" % (world, torch.cuda.device_count())
+    elif world > 1 and args.buckets == 1 and args.algo == "auto" and args.ring_steps > 0:
+        ring_cmp = guarded("ring_schedule", lambda: time_ring(_LIB, comm, buf, count, dt_enum, sp, dist, torch,
+                                                              args.ring_steps))
     extra = rccl = None
     if world > 1 and args.buckets == 1 and args.algo == "auto" and args.extra_steps > 0 and args.dtype == "float32":
         del buf  # room for the other configs' buffers
         torch.cuda.empty_cache()
-        extra = time_extra_configs(_LIB, comm, S, world, rank, sp, dist, torch, args.extra_steps)
+        extra = guarded("extra_configs", lambda: time_extra_configs(_LIB, comm, S, world, rank, sp, dist, torch,
+                                                                    args.extra_steps))
     if world > 1 and args.buckets == 1 and args.algo == "auto" and args.rccl_steps > 0 and args.dtype == "float32":
-        rccl = rccl_compare(S, world, rank, local, dist, torch, args.rccl_steps)
+        rccl = guarded("rccl_comparison", lambda: rccl_compare(S, world, rank, local, dist, torch, args.rccl_steps))
     tuning = None
     if world > 1 and args.buckets == 1 and args.algo == "auto" and args.extra_steps > 0 and args.dtype == "float32":
         torch.cuda.empty_cache()
-        tuning = mesh_tuning(_LIB, comm, S, dt_enum, esz, world, rank, sp, dist, torch, args.extra_steps)
+        tuning = guarded("mesh_tuning_ms", lambda: mesh_tuning(_LIB, comm, S, dt_enum, esz, world, rank, sp, dist,
+                                                               torch, args.extra_steps))
     tcp = None
     if world > 1 and args.cpu_seconds > 0:
-        tcp = cpu_tcp_ring(S, world, rank, dist)
+        tcp = guarded("cpu_tcp_ring", lambda: cpu_tcp_ring(S, world, rank, dist), needs_comm=False)
 
     # spot check (outside the timed region): N=1 reduce result vs oracle on a slice
     check = None
@@ -492,7 +521,7 @@ def main():
 
     if rank != 0:
         dist.barrier()
-        rdc_amd.finalize()
+        _finalize(rdc_amd, extras_error)
         return
     value = world * S / wall * args.steps / 1e9
     algbw = S / (kern_ms * 1e-3) / 1e9
@@ -549,7 +578,9 @@ def main():
     }
     if world > 1:
         out["busbw_GBps"] = round(algbw * 2 * (world - 1) / world, 2)
-    if ring_cmp is not None:
+    if isinstance(ring_cmp, str):
+        out["ring_schedule"] = {"skipped": ring_cmp}
+    elif ring_cmp is not None:
         rb = S / (ring_cmp * 1e-3) / 1e9 * 2 * (world - 1) / world
         out["ring_schedule"] = {"ms_per_step": round(ring_cmp, 4), "busbw_GBps": round(rb, 2),
                                 "frac_of_one_link_peak": round(rb / XGMI_LINK_DIR_GBPS, 4),
@@ -567,10 +598,23 @@ def main():
         out["cpu_tcp_ring"] = tcp
     if check is not None:
         out["oracle_check"] = check
+    if extras_error:
+        out["extras_error"] = extras_error
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
+        _finalize(rdc_amd, extras_error)
+
+
+def _finalize(rdc_amd, extras_error):
+    """Tear the communicators down; after a failed extra the library may
+    refuse, which must not turn a printed line into a failed run."""
+    try:
         rdc_amd.finalize()
+    except Exception as e:  # noqa: BLE001
+        if not extras_error:
+            raise
+        print("bench: finalize after a failed extra: %s" % e, file=sys.stderr)
 
 
 if __name__ == "__main__":
