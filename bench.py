@@ -14,8 +14,13 @@ from the device generator, resident in HBM before timing starts.
   N > 1 : one step = one in-place allreduce of the buffer across the N ranks
           (one process per GPU, HIP IPC over xGMI), bit-identical to the
           reference's ring.  xGMI-bound: 2(N-1)/N x S egress bytes per GPU.
-value = bytes of input buffers all ranks reduced per second = N x S / t
+value: N = 1 -> S / t of the reduce kernel (algbw of dst += src);
+       N > 1 -> busbw = S / t x 2(N-1)/N (nccl-tests convention, SURVEY.md
+       8(d)), with algbw = S / t beside it
 (t = wall time of the K timed steps, max over ranks, barrier+sync brackets).
+When ranks share a GPU (rehearsals on a 1-GPU box) every byte moves through
+one HBM and no xGMI link is exercised: the roofline is reported as
+bound "shared-hbm" with frac null.
 """
 import argparse
 import ctypes
@@ -100,17 +105,27 @@ def cpu_baseline(nbytes_workload, seconds):
     }
 
 
-def time_ring(lib, comm, buf, count, dt_enum, sp, dist, torch, steps):
-    """ms per in-place allreduce with the reference's ring schedule (k_ring),
-    max over ranks, after 2 warm-up launches."""
-    from rdc_amd._lib import check_call
+def sync_check(comm, sp, dist, torch):
+    """Synchronise, read this rank's device error word, and agree over the CPU
+    process group: every rank raises if any rank failed, so all ranks leave a
+    failed step together (no rank waits in a barrier its peers never reach)."""
+    err = ""
+    try:
+        torch.cuda.synchronize()
+        comm.check(sp)
+    except Exception as e:  # noqa: BLE001 - re-raised below on every rank
+        err = str(e)[:300] or "error"
+    f = torch.tensor([1.0 if err else 0.0], dtype=torch.float64)
+    dist.all_reduce(f, op=dist.ReduceOp.MAX)
+    if float(f[0]) > 0:
+        raise RuntimeError(err or "failed on another rank")
 
-    def one():
-        check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), count, dt_enum, 2, 1, sp))
-    for _ in range(2):
+
+def timed_ms(one, comm, sp, dist, torch, steps, warm=2):
+    """ms per call of one(), max over ranks, after `warm` checked calls."""
+    for _ in range(warm):
         one()
-    torch.cuda.synchronize()
-    comm.check(sp)
+    sync_check(comm, sp, dist, torch)
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -119,123 +134,179 @@ def time_ring(lib, comm, buf, count, dt_enum, sp, dist, torch, steps):
     dist.barrier()
     t = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    comm.check(sp)
+    sync_check(comm, sp, dist, torch)
     return float(t[0]) * 1e3
 
 
-def mesh_tuning(lib, comm, S, dt_enum, esz, world, rank, sp, dist, torch, steps):
+def time_ring(lib, comm, buf, count, dt_enum, sp, dist, torch, steps):
+    """ms per in-place allreduce with the reference's ring schedule (k_ring),
+    max over ranks, after 2 warm-up launches."""
+    from rdc_amd._lib import check_call
+
+    def one():
+        check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), count, dt_enum, 2, 1, sp))
+    return timed_ms(one, comm, sp, dist, torch, steps)
+
+
+def mesh_tuning(lib, comm, S, dt_enum, esz, world, rank, sp, dist, torch, steps, out):
     """ms per S-byte allreduce for a few mesh role splits and grids
     (RdcCommTune), max over ranks: which knobs the next round should move on
-    THIS node (the defaults were tuned with every rank on one HBM).  Runs
-    last: the communicator keeps the last shape."""
+    THIS node (the defaults were tuned with every rank on one HBM).  Grids
+    are clamped to what stays resident (ResidentGrid).  Runs last: the
+    communicator keeps the last shape.  Fills `out` as it goes (a failure
+    keeps the shapes measured so far)."""
     from rdc_amd._lib import check_call
     import rdc_amd
     cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    shapes = [(4, 8, 0), (3, 9, 0), (5, 8, 0), (6, 6, 0), (3, 10, 0), (4, 8, cus)]
-    if torch.cuda.device_count() >= world:  # one rank per GPU: more blocks than CUs stay resident
-        shapes.append((4, 8, 3 * cus))
-    out = {}
-    try:
-        buf = torch.empty(S // esz, dtype=torch.float32 if esz == 4 else torch.float16, device="cuda")
-        rdc_amd.fill_(buf, 0x5EED0000, rank)
-        for s16, r16, grid in shapes:
-            check_call(lib.RdcCommTune(comm.handle, s16, r16, grid, 0))
+    shapes = [(4, 8, 0), (3, 9, 0), (5, 8, 0), (6, 6, 0), (3, 10, 0), (4, 8, cus), (4, 8, 3 * cus)]
+    buf = torch.empty(S // esz, dtype=torch.float32 if esz == 4 else torch.float16, device="cuda")
+    rdc_amd.fill_(buf, 0x5EED0000, rank)
+    for s16, r16, grid in shapes:
+        check_call(lib.RdcCommTune(comm.handle, s16, r16, grid, 0))
 
-            def one():
-                check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), buf.numel(), dt_enum,
-                                                  2, 2, sp))
-            for _ in range(2):
-                one()
-            torch.cuda.synchronize()
-            comm.check(sp)
-            dist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                one()
-            torch.cuda.synchronize()
-            dist.barrier()
-            t = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            comm.check(sp)
-            out["split %d,%d grid %s" % (s16, r16, grid or "auto")] = round(float(t[0]) * 1e3, 4)
-        del buf
-    except Exception as e:  # noqa: BLE001 - informational only
-        out["error"] = str(e)
+        def one():
+            check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), buf.numel(), dt_enum,
+                                              2, 2, sp))
+        ms = timed_ms(one, comm, sp, dist, torch, steps)
+        ll = (ctypes.c_uint64 * 6)()
+        check_call(lib.RdcCommLastLaunch(comm.handle, ll))
+        out["split %d,%d grid %s" % (s16, r16, grid or "auto")] = {"ms": round(ms, 4), "launched_grid": int(ll[0])}
+    check_call(lib.RdcCommTune(comm.handle, 4, 8, 0, 0))
+    del buf
     return out
 
 
-def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps):
-    """The other BASELINE.json multi-GPU configs on the same communicator,
-    after the timed region (informational): cfg4 = fp16 allreduce of a buffer
-    of S bytes, cfg5 = 1024 buckets of S/1024 bytes fp32 in one coalesced
-    call, cfg1 = a 256 MiB fp32 buffer (with the sizes below it as
-    `sizes_fp32`).  ms per step = max over ranks of the wall time of `steps`
-    calls."""
+def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out):
+    """The other BASELINE.json configs on the same communicator, after the
+    timed region (informational): cfg4 = fp16 allreduce of a buffer of S
+    bytes, cfg5 = 1024 buckets of S/1024 bytes fp32 in one coalesced call,
+    cfg1 = a 4 KiB fp32 allreduce of HOST memory through the reference's own
+    entry point (RdcAllreduce on a numpy array: pinned zero-copy launch, the
+    real host path) and cfg2's 256 MiB fp32 buffer, with a device size curve
+    4 KiB - 256 MiB (`sizes_fp32`).  ms per step = max over ranks of the wall
+    time of `steps` calls.  Fills `out` as it goes."""
     from rdc_amd._lib import check_call
-    out = {}
+    import numpy as np
+    import rdc_amd
 
     def timed(one, nsteps=steps):
-        for _ in range(2):
-            one()
-        torch.cuda.synchronize()
-        comm.check(sp)
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(nsteps):
-            one()
-        torch.cuda.synchronize()
-        dist.barrier()
-        t = torch.tensor([(time.perf_counter() - t0) / nsteps], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        comm.check(sp)
-        return float(t[0]) * 1e3
+        return timed_ms(one, comm, sp, dist, torch, nsteps)
 
     def entry(ms, nbytes, what, nsteps=steps):
         bb = nbytes / (ms * 1e-3) / 1e9 * 2 * (world - 1) / world
         return {"workload": what, "bytes_per_gpu": nbytes, "ms_per_step": round(ms, 4), "busbw_GBps": round(bb, 2),
                 "steps": nsteps}
 
-    try:
-        h = torch.empty(S // 2, dtype=torch.float16, device="cuda")
-        import rdc_amd
-        rdc_amd.fill_(h, 0x5EED0000, rank)
-        ms = timed(lambda: check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(h.data_ptr()), h.numel(),
-                                                             10, 2, 0, sp)))
-        out["cfg4_fp16"] = entry(ms, S, "in-place allreduce(sum) of a %d MiB float16 buffer (packed half "
-                                        "reduce kernel)" % (S >> 20))
-        del h
-        K = 1024
-        per = S // 4 // K
-        bks = [torch.empty(per, dtype=torch.float32, device="cuda") for _ in range(K)]
-        for b, t in enumerate(bks):
-            rdc_amd.fill_(t, 0x5EED0000 + b, rank)
-        ptrs = (ctypes.c_void_p * K)(*[t.data_ptr() for t in bks])
-        cnts = (ctypes.c_size_t * K)(*([per] * K))
-        ms = timed(lambda: check_call(lib.RdcCommAllreduceCoalesced(comm.handle, ptrs, cnts, K, 6, 2, 0, sp)))
-        out["cfg5_buckets"] = entry(ms, per * 4 * K, "%d x %d KiB float32 buckets, one coalesced call "
-                                                     "(test/mallreduce.cc shape)" % (K, per * 4 >> 10))
-        del bks
-        # cfg1's 256 MiB fp32 buffer and the sizes below it (prefixes of one
-        # buffer): where the mesh's per-launch fill / drain and the one-shot
-        # hand-off decide the rate, for the next round's size thresholds
-        big = min(S, 256 << 20)
-        f = torch.empty(big // 4, dtype=torch.float32, device="cuda")
-        rdc_amd.fill_(f, 0x5EED0000, rank)
-        sizes = {}
-        for nb in (64 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, big):
-            if nb > big:
-                continue
-            ns = max(steps, 50) if nb <= (16 << 20) else steps  # small calls: more of them
-            ms = timed(lambda: check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(f.data_ptr()),
-                                                                 nb // 4, 6, 2, 0, sp)), ns)
-            e = entry(ms, nb, "in-place allreduce(sum) of %d KiB float32" % (nb >> 10), ns)
-            sizes[str(nb)] = {k: e[k] for k in ("ms_per_step", "busbw_GBps", "steps")}
-            if nb == (256 << 20):
-                out["cfg1_256MiB"] = e
-        out["sizes_fp32"] = sizes
-        del f
-    except Exception as e:  # informational: never costs the main line
-        out["error"] = str(e)
+    h = torch.empty(S // 2, dtype=torch.float16, device="cuda")
+    rdc_amd.fill_(h, 0x5EED0000, rank)
+    ms = timed(lambda: check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(h.data_ptr()), h.numel(),
+                                                         10, 2, 0, sp)))
+    out["cfg4_fp16"] = entry(ms, S, "in-place allreduce(sum) of a %d MiB float16 buffer (packed half "
+                                    "reduce kernel)" % (S >> 20))
+    del h
+    K = 1024
+    per = S // 4 // K
+    bks = [torch.empty(per, dtype=torch.float32, device="cuda") for _ in range(K)]
+    for b, t in enumerate(bks):
+        rdc_amd.fill_(t, 0x5EED0000 + b, rank)
+    ptrs = (ctypes.c_void_p * K)(*[t.data_ptr() for t in bks])
+    cnts = (ctypes.c_size_t * K)(*([per] * K))
+    ms = timed(lambda: check_call(lib.RdcCommAllreduceCoalesced(comm.handle, ptrs, cnts, K, 6, 2, 0, sp)))
+    out["cfg5_buckets"] = entry(ms, per * 4 * K, "%d x %d KiB float32 buckets, one coalesced call "
+                                                 "(test/mallreduce.cc shape)" % (K, per * 4 >> 10))
+    del bks
+    # cfg1 on the real path: 4 KiB of fp32 in pageable host memory through
+    # RdcAllreduce (rdc/core.py's entry point), synchronous per call
+    a = np.ones(1024, dtype=np.float32)
+    ms = timed(lambda: check_call(lib.RdcAllreduce(ctypes.c_void_p(a.ctypes.data), 1024, 6, 2, None, None)),
+               max(steps, 200))
+    e = entry(ms, 4096, "4 KiB float32 allreduce of HOST memory via RdcAllreduce (cfg1 shape, synchronous)",
+              max(steps, 200))
+    e["us_per_call"] = round(ms * 1e3, 2)
+    out["cfg1_host_4KiB"] = e
+    # cfg2's 256 MiB fp32 buffer and the sizes below it (prefixes of one
+    # buffer): where the mesh's per-launch fill / drain and the one-shot
+    # hand-off decide the rate, for the size thresholds at this rank count
+    big = min(S, 256 << 20)
+    f = torch.empty(big // 4, dtype=torch.float32, device="cuda")
+    rdc_amd.fill_(f, 0x5EED0000, rank)
+    sizes = {}
+    out["sizes_fp32"] = sizes
+    for nb in (4 << 10, 64 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, big):
+        if nb > big:
+            continue
+        ns = max(steps, 50) if nb <= (16 << 20) else steps  # small calls: more of them
+        ms = timed(lambda: check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(f.data_ptr()),
+                                                             nb // 4, 6, 2, 0, sp)), ns)
+        e = entry(ms, nb, "in-place allreduce(sum) of %d KiB float32" % (nb >> 10), ns)
+        sizes[str(nb)] = {k: e[k] for k in ("ms_per_step", "busbw_GBps", "steps")}
+        if nb == (256 << 20):
+            out["cfg2_256MiB"] = e
+    del f
+    return out
+
+
+def parity_checks(lib, comm, S, world, rank, sp, dist, torch, out):
+    """Bit-exact checks at the bench's own shapes (after all timing): fresh
+    synthetic inputs, ONE collective, then windows of every rank's result -
+    each chunk's head and tail, i.e. every Split boundary, where a misplanned
+    tile or a stale hand-off shows first - compared with the oracle's ring
+    order computed on the window alone.  cfg3 (mesh and the reference ring
+    schedule), cfg4 (fp16) and cfg5 (1024 buckets, three whole buckets).
+    Every rank checks its own result; the line reports the AND over ranks."""
+    from rdc_amd._lib import check_call
+    import numpy as np
+    import rdc_amd
+    from oracle import oracle as O
+
+    def agree(ok):
+        f = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        return float(f[0]) == 0.0
+
+    def windows(count):
+        W = min(count, 1 << 14)
+        starts = {0, max(0, count - W)}
+        for b, _ in O.split(count, world)[1:]:
+            starts.add(max(0, b - W // 2))
+        return sorted((st, min(W, count - st)) for st in starts)
+
+    def check_buf(t, count, dt, seed):
+        ok = True
+        for st, m in windows(count):
+            got = t[st:st + m].cpu().contiguous().view(torch.uint8).numpy().tobytes()
+            ok = ok and got == O.expected_window(count, st, m, world, dt, 2, seed).tobytes()
+        return ok
+
+    for name, dt, algo, tdt in (("cfg3_mesh", 6, 2, torch.float32), ("cfg3_ring", 6, 1, torch.float32),
+                                ("cfg4_fp16", 10, 0, torch.float16)):
+        esz = 4 if dt == 6 else 2
+        count = S // esz
+        t = torch.empty(count, dtype=tdt, device="cuda")
+        seed = 0x5EED1000 + dt * 16 + algo
+        check_call(lib.RdcFill(ctypes.c_void_p(t.data_ptr()), count, dt, seed, rank, sp))
+        check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(t.data_ptr()), count, dt, 2, algo, sp))
+        sync_check(comm, sp, dist, torch)
+        out[name] = agree(check_buf(t, count, dt, seed))
+        del t
+    K = 1024
+    per = S // 4 // K
+    bks = [torch.empty(per, dtype=torch.float32, device="cuda") for _ in range(K)]
+    for b, t in enumerate(bks):
+        check_call(lib.RdcFill(ctypes.c_void_p(t.data_ptr()), per, 6, 0x5EED2000 + b, rank, sp))
+    ptrs = (ctypes.c_void_p * K)(*[t.data_ptr() for t in bks])
+    cnts = (ctypes.c_size_t * K)(*([per] * K))
+    check_call(lib.RdcCommAllreduceCoalesced(comm.handle, ptrs, cnts, K, 6, 2, 0, sp))
+    sync_check(comm, sp, dist, torch)
+    ok = True
+    for b in (0, K // 2 + 1, K - 1):
+        got = bks[b].cpu().numpy().tobytes()
+        ok = ok and got == O.expected_window(per, 0, per, world, 6, 2, 0x5EED2000 + b).tobytes()
+    out["cfg5_buckets"] = agree(ok)
+    del bks
+    out["method"] = ("one collective on fresh synthetic inputs; windows of 16 Ki elements at both ends of every "
+                     "Split chunk (cfg3/cfg4) and three whole buckets (cfg5) compared bit-exact with the oracle's "
+                     "ring order on every rank")
     return out
 
 
@@ -269,11 +340,13 @@ def rccl_compare(S, world, rank, local, dist, torch, steps):
 
 
 def cpu_tcp_ring(S, world, rank, dist):
-    """The reference's CPU ring allreduce over loopback TCP (oracle/tcp_ring,
-    the C restatement of TryAllreduceRing) at this run's rank
-    count, on a bounded 64 MiB fp32 sample, rank 0 only, after every GPU
-    measurement: the north star's CPU figure beside the N>1 line (a reported
-    baseline, informational)."""
+    """A PORT of the reference's CPU ring allreduce over loopback TCP
+    (oracle/tcp_ring: a C restatement of TryAllreduceRing's schedule and
+    op::Reducer over one TCP socket per ring link, without the reference's
+    epoll poller, thread pool or its partial-write liveness bug - the shipped
+    reference does not build, SURVEY finding 1) at this run's
+    rank count, on a bounded 64 MiB fp32 sample, rank 0 only, after every GPU
+    measurement (a reported baseline, informational)."""
     import subprocess
     res = None
     if rank == 0:
@@ -285,6 +358,8 @@ def cpu_tcp_ring(S, world, rank, dist):
             lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
             res = json.loads(lines[-1]) if lines else {"error": "rc=%d: %s" % (p.returncode, p.stderr[-300:])}
             res["sample"] = "%d ranks as processes, one thread each, %d MiB fp32, median of 3 calls" % (world, nb >> 20)
+            res["kind"] = "port"
+            res["cores"] = world
         except Exception as e:  # noqa: BLE001 - informational only
             res = {"error": str(e)}
     dist.barrier()
@@ -304,8 +379,7 @@ def trace_roles(lib, comm, buf, count, dt_enum, sp, dist, torch):
     dist.barrier()
     check_call(lib.RdcCommTraceNext(comm.handle, ctypes.c_void_p(tr.data_ptr()), words))
     check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), count, dt_enum, 2, 0, sp))
-    torch.cuda.synchronize()
-    comm.check(sp)
+    sync_check(comm, sp, dist, torch)
     ll = (ctypes.c_uint64 * 6)()
     check_call(lib.RdcCommLastLaunch(comm.handle, ll))
     grid, s, r, g, tile, algo = [int(x) for x in ll]
@@ -340,11 +414,12 @@ def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
                       (2, "pull_one_link_GBps"), (3, "pull_all_links_GBps")):
         ms, used = ctypes.c_double(), ctypes.c_size_t()
         rc = lib.RdcCommProbe(comm.handle, mode, nbytes, reps, sp, ctypes.byref(ms), ctypes.byref(used))
-        if rc != 0:
-            return {"error": lib.RdcGetLastError().decode()}
+        err = lib.RdcGetLastError().decode() if rc != 0 else ""
         per_target = used.value
-        t = torch.tensor([ms.value], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor([ms.value, 1.0 if rc != 0 else 0.0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # every rank leaves together on a failure
+        if float(t[1]) > 0:
+            return {"error": err or "failed on another rank"}
         ntarget = 1 if mode in (0, 2) else int(os.environ.get("WORLD_SIZE", "1")) - 1
         out[key] = round(per_target * ntarget / (float(t[0]) * 1e-3) / 1e9, 2)
         dist.barrier()
@@ -422,12 +497,13 @@ def main():
     step()
     torch.cuda.synchronize()
     if world > 1:
-        comm.check(sp)
+        sync_check(comm, sp, dist, torch)
     for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
+    probe = None
     if world > 1:
-        comm.check(sp)
+        sync_check(comm, sp, dist, torch)
         dist.barrier()
         probe = xgmi_probe(_LIB, comm, sp, dist, torch)
     torch.cuda.synchronize()
@@ -442,7 +518,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     if world > 1:
-        comm.check(sp)
+        sync_check(comm, sp, dist, torch)
     wall = t1 - t0
     kern_ms = e0.elapsed_time(e1) / args.steps
     if world > 1:
@@ -450,16 +526,15 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall, kern_ms = float(tt[0]), float(tt[1])
 
-    # the reference's own schedule on the same buffer, after the timed region
-    # (informational: same bits, one link direction per GPU)
     # Everything after the timed region is informational.  A failure there
     # (e.g. a device wait timing out) must not cost the headline line: every
-    # extra runs guarded, the ranks agree on failure over the CPU process
-    # group, and once one has failed the communicator is unusable, so the
-    # remaining extras that need it are skipped.
+    # extra runs guarded; inside, every step agrees on failure over the CPU
+    # process group (sync_check), so all ranks leave a failed extra together;
+    # once one has failed the communicator is unusable, and the remaining
+    # extras that need it are skipped.  Partial results are kept.
     extras_error = {}
 
-    def guarded(name, fn, needs_comm=True):
+    def guarded(name, fn, needs_comm=True, partial=None):
         if needs_comm and extras_error:
             return None
         res, failed = None, 0.0
@@ -473,35 +548,39 @@ def main():
             dist.all_reduce(f, op=dist.ReduceOp.MAX)
             if float(f[0]) > 0 and name not in extras_error:
                 extras_error[name] = "failed on another rank"
-        return None if name in extras_error else res
+        if name in extras_error:
+            return partial if partial else None
+        return res
 
-    roles = None
-    if world > 1 and args.buckets == 1 and args.algo == "auto":
+    multi = world > 1 and args.buckets == 1 and args.algo == "auto"
+    f32 = args.dtype == "float32"
+    roles = ring_cmp = extra = rccl = tuning = tcp = checks = None
+    if multi:
         roles = guarded("role_timeline", lambda: trace_roles(_LIB, comm, buf, count, dt_enum, sp, dist, torch))
-    ring_cmp = None
-    ring_shared = world > 2 and torch.cuda.device_count() < world
-    if ring_shared and args.buckets == 1 and args.algo == "auto" and args.ring_steps > 0:
-        # rehearsal with >2 ranks on one GPU: the ring's full-grid launches of
-        # every rank are not all resident at once there (4 ranks on one GPU
-        # timed out), so the ring is left to the one-GPU-per-rank node
-        ring_cmp = "%d ranks share %d GPU(s)" % (world, torch.cuda.device_count())
-    elif world > 1 and args.buckets == 1 and args.algo == "auto" and args.ring_steps > 0:
+    if multi and args.ring_steps > 0:
+        # the reference's own schedule on the same buffer (same bits, one link
+        # direction per GPU).  Grids are clamped to what stays resident next
+        # to the ranks sharing a GPU, so this runs in rehearsals too.
         ring_cmp = guarded("ring_schedule", lambda: time_ring(_LIB, comm, buf, count, dt_enum, sp, dist, torch,
                                                               args.ring_steps))
-    extra = rccl = None
-    if world > 1 and args.buckets == 1 and args.algo == "auto" and args.extra_steps > 0 and args.dtype == "float32":
+    if multi:
         del buf  # room for the other configs' buffers
         torch.cuda.empty_cache()
+    if multi and f32 and args.extra_steps > 0:
+        part = {}
         extra = guarded("extra_configs", lambda: time_extra_configs(_LIB, comm, S, world, rank, sp, dist, torch,
-                                                                    args.extra_steps))
-    if world > 1 and args.buckets == 1 and args.algo == "auto" and args.rccl_steps > 0 and args.dtype == "float32":
+                                                                    args.extra_steps, part), partial=part)
+    if multi and f32 and not args.no_check:
+        part_c = {}
+        checks = guarded("parity_checks", lambda: parity_checks(_LIB, comm, S, world, rank, sp, dist, torch, part_c),
+                         partial=part_c)
+    if multi and f32 and args.rccl_steps > 0:
         rccl = guarded("rccl_comparison", lambda: rccl_compare(S, world, rank, local, dist, torch, args.rccl_steps))
-    tuning = None
-    if world > 1 and args.buckets == 1 and args.algo == "auto" and args.extra_steps > 0 and args.dtype == "float32":
+    if multi and f32 and args.extra_steps > 0:
         torch.cuda.empty_cache()
+        part_t = {}
         tuning = guarded("mesh_tuning_ms", lambda: mesh_tuning(_LIB, comm, S, dt_enum, esz, world, rank, sp, dist,
-                                                               torch, args.extra_steps))
-    tcp = None
+                                                               torch, args.extra_steps, part_t), partial=part_t)
     if world > 1 and args.cpu_seconds > 0:
         tcp = guarded("cpu_tcp_ring", lambda: cpu_tcp_ring(S, world, rank, dist), needs_comm=False)
 
@@ -509,7 +588,6 @@ def main():
     check = None
     if world == 1 and not args.no_check:
         from oracle import oracle as O
-        import numpy as np
         m = min(count, 1 << 16)
         d0 = O.fill(m, dt_enum, 0x5EED0000, 0)  # the generator is position-keyed: first m elements
         s0 = O.fill(m, dt_enum, 0x5EED0000, 1)
@@ -523,9 +601,11 @@ def main():
         dist.barrier()
         _finalize(rdc_amd, extras_error)
         return
-    value = world * S / wall * args.steps / 1e9
     algbw = S / (kern_ms * 1e-3) / 1e9
+    gpus_here = torch.cuda.device_count()
+    shared = world > 1 and gpus_here < world
     if world == 1:
+        value = S / wall * args.steps / 1e9
         achieved = 3 * S / (kern_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
@@ -535,6 +615,9 @@ def main():
         workload = "reduce kernel alone (n=1): dst += src, %s, %d MiB per buffer" % (args.dtype, S >> 20)
         par = "single GPU"
     else:
+        # busbw of the whole job: S / t x 2(n-1)/n, t = the
+        # wall time per step (max over ranks, barrier-bracketed)
+        value = S / (wall / args.steps) / 1e9 * 2 * (world - 1) / world
         busbw = algbw * 2 * (world - 1) / world
         algo_name = args.algo
         if algo_name == "auto":  # the library's own choice (rdc_plan.cpp OneshotEligible, 1 MiB push budget)
@@ -551,6 +634,13 @@ def main():
             meas = probe["one_link_one_direction_GBps"] if algo_name == "ring" else probe["all_links_egress_GBps"]
             roof["peak_measured"] = meas
             roof["frac_of_measured"] = round(busbw / meas, 4)
+        if shared:
+            # every rank's bytes move through ONE HBM: no xGMI link is timed,
+            # so no xGMI fraction is meaningful (round 1 printed 7.996 here)
+            roof.update({"bound": "shared-hbm", "peak": None, "frac": None, "frac_of_bidir_ring_roofline": None,
+                         "frac_of_measured": None,
+                         "note": "%d ranks share %d GPU(s): rehearsal of the protocol, not an xGMI measurement"
+                                 % (world, gpus_here)})
         workload = "in-place allreduce(sum) of a %d MiB %s buffer per GPU, %s schedule" % (S >> 20, args.dtype,
                                                                                         algo_name)
         if args.buckets > 1:
@@ -572,18 +662,19 @@ def main():
         "dtype": DT_SHORT[args.dtype],
         "data": "synthetic (splitmix64 device generator, seed 0x5EED0000)",
         "config": {"workload": workload, "bytes_per_gpu": S, "parallelism": par},
-        "algbw_GBps": round(algbw, 2),
+        "value_definition": "reduce kernel alone: S / t" if world == 1 else
+                            "busbw = S / t x 2(n-1)/n (algbw_GBps = S / t)",
+        "algbw_GBps": round(S / (wall / args.steps) / 1e9, 2),
         "roofline": roof,
         "cpu_baseline": cpu_baseline(S, args.cpu_seconds) if world == 1 else None,
     }
     if world > 1:
-        out["busbw_GBps"] = round(algbw * 2 * (world - 1) / world, 2)
-    if isinstance(ring_cmp, str):
-        out["ring_schedule"] = {"skipped": ring_cmp}
-    elif ring_cmp is not None:
+        out["busbw_GBps"] = round(value, 2)
+        out["ranks_share_gpu"] = shared
+    if ring_cmp is not None:
         rb = S / (ring_cmp * 1e-3) / 1e9 * 2 * (world - 1) / world
         out["ring_schedule"] = {"ms_per_step": round(ring_cmp, 4), "busbw_GBps": round(rb, 2),
-                                "frac_of_one_link_peak": round(rb / XGMI_LINK_DIR_GBPS, 4),
+                                "frac_of_one_link_peak": None if shared else round(rb / XGMI_LINK_DIR_GBPS, 4),
                                 "note": "reference ring schedule (k_ring) on the same buffer, timed after the "
                                         "main region; bit-identical result"}
     if roles is not None:
@@ -592,6 +683,8 @@ def main():
         out["mesh_tuning_ms"] = tuning
     if extra is not None:
         out["extra_configs"] = extra
+    if checks is not None:
+        out["oracle_check"] = checks
     if rccl is not None:
         out["rccl_comparison"] = rccl
     if tcp is not None:

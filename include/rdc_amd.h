@@ -213,6 +213,15 @@ int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, voi
  *    off[16], len[16], mis[16], tiles[16]]   (per chunk c < n)
  * *out_pieces = number of launches (records written: min(that, max_pieces)). */
 #define RDC_PLAN_WORDS 68
+/* Grid of a collective launch whose blocks wait on other ranks' blocks: the
+ * requested grid `want` clamped so that every rank's blocks stay resident at
+ * once, min(want, blocks_per_cu x cus / ranks_per_gpu) (at least 1).
+ * Communicators apply it to every ring / mesh / one-shot / tree / broadcast /
+ * allgather launch, including grids forced by RDC_NBLOCKS or RdcCommTune;
+ * blocks_per_cu is the kernel's occupancy, ranks_per_gpu the most ranks of
+ * the communicator on one physical GPU, cus the fewest CUs of any rank's GPU.
+ * Returns the grid (not a status). */
+int RdcPlanResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu);
 int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4);
 int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int algo, size_t tile_bytes,
                      int max_blocks, uint64_t* out, int max_pieces, int* out_pieces);

@@ -57,6 +57,9 @@ def lib():
         L.rdc_oracle_allreduce_ring.argtypes = [ctypes.POINTER(vp), ctypes.c_int, u64, ctypes.c_int, ctypes.c_int]
         L.rdc_oracle_allreduce_closed_form.argtypes = [ctypes.POINTER(vp), ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, vp]
         L.rdc_oracle_fill.argtypes = [vp, u64, ctypes.c_int, u64, ctypes.c_int]
+        L.rdc_oracle_fill_at.argtypes = [vp, u64, u64, ctypes.c_int, u64, ctypes.c_int]
+        L.rdc_oracle_allreduce_window.argtypes = [ctypes.POINTER(vp), ctypes.c_int, u64, u64, u64, ctypes.c_int,
+                                                  ctypes.c_int, vp]
         L.rdc_oracle_splitmix64.restype = u64
         L.rdc_oracle_splitmix64.argtypes = [u64]
         L.rdc_oracle_f32_to_f16.restype = ctypes.c_uint16
@@ -154,6 +157,28 @@ def fill(count, dtype, seed, rank):
     if rc:
         raise ValueError("fill rc=%d" % rc)
     return a
+
+
+def fill_at(first, count, dtype, seed, rank):
+    """Elements [first, first+count) of fill()'s stream (position-keyed)."""
+    a = np.empty(count, dtype=NP_DTYPE[dtype])
+    rc = lib().rdc_oracle_fill_at(_ptr(a), first, count, dtype, seed, rank)
+    if rc:
+        raise ValueError("fill_at rc=%d" % rc)
+    return a
+
+
+def expected_window(total, first, m, n, dtype, op, seed):
+    """Allreduce result at positions [first, first+m) of a `total`-element
+    buffer whose rank-r input is fill(total, dtype, seed, r): the ring's
+    per-chunk closed form on the window alone (for full-size checks)."""
+    wins = [fill_at(first, m, dtype, seed, r) for r in range(n)]
+    out = np.empty(m, dtype=NP_DTYPE[dtype])
+    arr = (ctypes.c_void_p * n)(*[w.ctypes.data for w in wins])
+    rc = lib().rdc_oracle_allreduce_window(arr, n, total, first, m, dtype, op, _ptr(out))
+    if rc:
+        raise ValueError("allreduce_window rc=%d" % rc)
+    return out
 
 
 def expected_allreduce(inputs, dtype, op):

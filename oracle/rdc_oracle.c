@@ -379,9 +379,15 @@ uint64_t rdc_oracle_splitmix64(uint64_t x) {
 }
 
 int rdc_oracle_fill(void* buf, uint64_t count, int dtype, uint64_t seed, int rank) {
+    return rdc_oracle_fill_at(buf, 0, count, dtype, seed, rank);
+}
+
+/* elements [first, first+count) of the same stream (the generator is keyed
+   by position, so a window of a huge buffer costs only its own length) */
+int rdc_oracle_fill_at(void* buf, uint64_t first, uint64_t count, int dtype, uint64_t seed, int rank) {
     uint64_t key = seed ^ ((uint64_t)rank << 40);
     for (uint64_t i = 0; i < count; ++i) {
-        uint64_t u = rdc_oracle_splitmix64(key ^ i);
+        uint64_t u = rdc_oracle_splitmix64(key ^ (first + i));
         switch (dtype) {
             case RDC_DT_INT8: case RDC_DT_UINT8: ((uint8_t*)buf)[i] = (uint8_t)u; break;
             case RDC_DT_INT32: case RDC_DT_UINT32: ((uint32_t*)buf)[i] = (uint32_t)u; break;
@@ -397,6 +403,45 @@ int rdc_oracle_fill(void* buf, uint64_t count, int dtype, uint64_t seed, int ran
                 ((uint16_t*)buf)[i] = rdc_oracle_f32_to_bf16((float)(int32_t)(u >> 32) * 0x1p-31f); break;
             default: return -1;
         }
+    }
+    return 0;
+}
+
+/* The closed form above on a window of a buffer too large for the CPU check:
+   wins[q] holds rank q's elements [first, first+m) of a `total`-element
+   buffer; out receives the allreduce result of those positions, each folded
+   in the ring order of its Split(0, total, n) chunk. */
+int rdc_oracle_allreduce_window(const void* const* wins, int n, uint64_t total, uint64_t first, uint64_t m,
+                                int dtype, int op, void* out) {
+    size_t esz = rdc_oracle_dtype_size(dtype);
+    int64_t cb[RDC_ORACLE_MAX_RANKS], ce[RDC_ORACLE_MAX_RANKS];
+    if (esz == 0 || n < 1 || n > RDC_ORACLE_MAX_RANKS || first + m > total) return -1;
+    if (m == 0) return 0;
+    memcpy(out, wins[0], m * esz);
+    if (n == 1) return 0;
+    rdc_oracle_split(0, (int64_t)total, n, cb, ce);
+    {
+        char* acc = (char*)malloc(m * esz);
+        char* tmp = (char*)malloc(m * esz);
+        if (!acc || !tmp) { free(acc); free(tmp); return -8; }
+        for (int c = 0; c < n; ++c) {
+            uint64_t lo = (uint64_t)cb[c] > first ? (uint64_t)cb[c] : first;
+            uint64_t hi = (uint64_t)ce[c] < first + m ? (uint64_t)ce[c] : first + m;
+            if (lo >= hi) continue;
+            uint64_t off = (lo - first) * esz, len = hi - lo;
+            int q = (c - 1 + n) % n;
+            memcpy(acc, (const char*)wins[q] + off, len * esz);
+            for (int k = 2; k <= n; ++k) {
+                q = ((c - k) % n + n) % n;
+                memcpy(tmp, (const char*)wins[q] + off, len * esz);
+                int rc = rdc_oracle_reducer(acc, tmp, len, dtype, op);
+                if (rc) { free(acc); free(tmp); return rc; }
+                memcpy(acc, tmp, len * esz);
+            }
+            memcpy((char*)out + off, acc, len * esz);
+        }
+        free(acc);
+        free(tmp);
     }
     return 0;
 }

@@ -39,6 +39,9 @@ int rdc_oracle_allreduce_closed_form(const void* const* bufs, int n, uint64_t co
                                      int dtype, int op, void* out);
 uint64_t rdc_oracle_splitmix64(uint64_t x);
 int rdc_oracle_fill(void* buf, uint64_t count, int dtype, uint64_t seed, int rank);
+int rdc_oracle_fill_at(void* buf, uint64_t first, uint64_t count, int dtype, uint64_t seed, int rank);
+int rdc_oracle_allreduce_window(const void* const* wins, int n, uint64_t total, uint64_t first, uint64_t m,
+                                int dtype, int op, void* out);
 float rdc_oracle_f16_to_f32(uint16_t h);
 uint16_t rdc_oracle_f32_to_f16(float f);
 float rdc_oracle_bf16_to_f32(uint16_t b);

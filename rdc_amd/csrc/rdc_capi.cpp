@@ -36,7 +36,6 @@ struct Manager {
     int rank = 0, world = 1, device = -1;
     std::string tracker_uri = "127.0.0.1";
     int tracker_port = 29571;
-    size_t ring_mincount = 1;  // rdc_reduce_ring_mincount (communicator_manager.cc:46)
     double bootstrap_timeout_s = 300.0;
     size_t host_zc_bytes = (size_t)1 << 20;  // host buffers up to this run zero-copy on pinned memory
     CommConfig cfg;
@@ -78,7 +77,7 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_TRACKER_PORT") m.tracker_port = atoi(val);
     else if (k == "rdc_world_size" || k == "RDC_WORLD_SIZE") m.world = atoi(val);
     else if (k == "RDC_RANK" || k == "rdc_rank") m.rank = atoi(val);
-    else if (k == "rdc_reduce_ring_mincount") m.ring_mincount = parse_unit(val);
+    else if (k == "rdc_reduce_ring_mincount") m.cfg.ring_mincount = parse_unit(val);
     else if (k == "RDC_DEVICE") m.device = atoi(val);
     else if (k == "RDC_SCRATCH_BYTES" || k == "rdc_reduce_buffer") m.cfg.scratch_bytes = parse_unit(val);
     else if (k == "RDC_ALGO") {
@@ -570,7 +569,7 @@ int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes
         static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
                                      "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES", "RDC_P2P_SLOT_BYTES",
                                      "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT",
-                                     "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT"};
+                                     "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "rdc_reduce_ring_mincount"};
         if (!m.inited && !m.env_loaded) {
             for (const char* k : keys) env_param(m, k);
             m.env_loaded = true;
@@ -612,6 +611,10 @@ int RdcReduce(void* dst, const void* src, size_t count, int dtype, int op, void*
 
 int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, void* stream) {
     return guard([&] { DeviceFill(dev_buf, count, dtype, seed, rank, static_cast<hipStream_t>(stream)); });
+}
+
+int RdcPlanResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu) {
+    return ResidentGrid(want, blocks_per_cu, cus, ranks_per_gpu);
 }
 
 int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4) {

@@ -77,9 +77,28 @@ struct PeerInfo {
     uint64_t slot_bytes;
     uint64_t max_tiles;
     uint64_t p2p_slot_bytes;
+    int32_t num_cus;
+    int32_t pad2;
+    uint64_t plan[12];  // PlanKey: the parameters that shape a launch plan (must agree)
     char host[64];
     char pci[32];  // physical GPU (ranks may share one: tests, emulation)
 };
+
+// Launch plans are made on each host; flags are matched by tile index while
+// data lands by byte offset, so ranks that planned differently would read
+// contributions that have not landed (silent wrong bits, not a timeout).
+// Every parameter a plan depends on is exchanged at creation and compared.
+void PlanKey(const CommConfig& c, uint64_t* k) {
+    const uint64_t v[12] = {(uint64_t)c.algo, (uint64_t)c.max_blocks, (uint64_t)c.tile_bytes,
+                            (uint64_t)c.oneshot_push_max, (uint64_t)c.fuse_bytes, (uint64_t)c.coalesce_fused,
+                            (uint64_t)c.fuse_bytes_direct, (uint64_t)c.bcast_split_bytes, (uint64_t)c.mesh_split.s16,
+                            (uint64_t)c.mesh_split.r16, (uint64_t)c.ring_mincount, (uint64_t)c.scratch_bytes};
+    memcpy(k, v, sizeof(v));
+}
+const char* kPlanKeyNames[12] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES",
+                                 "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT", "RDC_BCAST_SPLIT_BYTES",
+                                 "RDC_MESH_SPLIT", "RDC_MESH_SPLIT", "rdc_reduce_ring_mincount",
+                                 "RDC_SCRATCH_BYTES"};
 
 // The point-to-point control block (rdc_p2p.h) in POSIX shared memory: rank 0
 // creates it, every rank maps it, rank 0 unlinks the name once all mapped.
@@ -194,6 +213,8 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     mine.alloc_kind = c->alloc_kind_;
     mine.slot_bytes = c->slot_bytes_;
     mine.max_tiles = c->max_tiles_;
+    mine.num_cus = c->num_cus_;
+    PlanKey(cfg, mine.plan);
     gethostname(mine.host, sizeof(mine.host) - 1);
     if (hipDeviceGetPCIBusId(mine.pci, sizeof(mine.pci) - 1, device) != hipSuccess) {
         (void)hipGetLastError();
@@ -204,15 +225,30 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     bs->allgather(&mine, sizeof(mine), all.data());
     dbg("[rdc %d] %s\n", c->rank_, "handles exchanged");
     for (int p = 0; p < c->n_; ++p) {
-        if (all[(size_t)p].slot_bytes != mine.slot_bytes || all[(size_t)p].max_tiles != mine.max_tiles ||
-            all[(size_t)p].p2p_slot_bytes != mine.p2p_slot_bytes)
+        const PeerInfo& q = all[(size_t)p];
+        if (q.slot_bytes != mine.slot_bytes || q.max_tiles != mine.max_tiles ||
+            q.p2p_slot_bytes != mine.p2p_slot_bytes)
             throw std::runtime_error("rdc: ranks disagree on scratch size (set RDC_SCRATCH_BYTES identically)");
-        if (strncmp(all[(size_t)p].host, mine.host, sizeof(mine.host)) != 0)
+        for (int k = 0; k < 12; ++k)
+            if (q.plan[k] != mine.plan[k])
+                throw std::runtime_error(std::string("rdc: rank ") + std::to_string(p) + " and rank " +
+                                         std::to_string(c->rank_) + " disagree on " + kPlanKeyNames[k] + " (" +
+                                         std::to_string(q.plan[k]) + " vs " + std::to_string(mine.plan[k]) +
+                                         "): every rank must plan launches identically");
+        if (strncmp(q.host, mine.host, sizeof(mine.host)) != 0)
             throw std::runtime_error("rdc: xGMI path needs every rank on one node (rank " + std::to_string(p) +
-                                     " is on " + all[(size_t)p].host + ")");
+                                     " is on " + q.host + ")");
     }
-    for (int p = 0; p < c->n_; ++p)
-        if (p != c->rank_ && strncmp(all[(size_t)p].pci, mine.pci, sizeof(mine.pci)) == 0) c->shared_gpu_ = true;
+    // grids are planned from values every rank sees: the fewest CUs of any
+    // rank's GPU and the most ranks sharing one physical GPU (ResidentGrid)
+    c->cus_min_ = c->num_cus_;
+    c->share_max_ = 1;
+    for (int p = 0; p < c->n_; ++p) {
+        c->cus_min_ = std::min(c->cus_min_, std::max(1, (int)all[(size_t)p].num_cus));
+        int same = 0;
+        for (int q = 0; q < c->n_; ++q) same += strncmp(all[(size_t)p].pci, all[(size_t)q].pci, sizeof(mine.pci)) == 0;
+        c->share_max_ = std::max(c->share_max_, same);
+    }
     // direct peer access between distinct devices (xGMI); IPC mapping with
     // hipIpcMemLazyEnablePeerAccess covers the rest.
     for (int p = 0; p < c->n_; ++p) {
@@ -264,10 +300,17 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
         c->AllocLocal();
         cs.push_back(std::move(c));
     }
-    bool shared = false;
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < i; ++j) shared |= devices[i] == devices[j];
-    for (auto& c : cs) c->shared_gpu_ = shared;
+    int share = 1, cus = cs[0]->num_cus_;
+    for (int i = 0; i < n; ++i) {
+        int same = 0;
+        for (int j = 0; j < n; ++j) same += devices[i] == devices[j];
+        share = std::max(share, same);
+        cus = std::min(cus, cs[(size_t)i]->num_cus_);
+    }
+    for (auto& c : cs) {
+        c->share_max_ = share;
+        c->cus_min_ = cus;
+    }
     // Pinned coherent pages of its own, not a registered heap object: a
     // registration covers whole pages, and a heap object shares its first and
     // last page with unrelated allocations that the runtime may pin and unpin
@@ -326,8 +369,11 @@ Communicator::~Communicator() {
         } catch (...) {
         }
     }
-    for (auto& kv : pack_cache_) (void)hipFree(kv.second.dtable);
-    if (image_) (void)hipFree(image_);
+    for (auto& kv : pack_cache_)
+        if (kv.second.dtable) (void)hipFreeAsync(kv.second.dtable, nullptr);
+    if (image_) (void)hipFreeAsync(image_, nullptr);
+    (void)hipStreamSynchronize(nullptr);
+    for (auto& r : retired_) (void)hipEventDestroy(r.first);
     if (scratch_) (void)hipFree(scratch_);
     if (scratch_ag_) (void)hipFree(scratch_ag_);
     if (flags_) (void)hipFree(flags_);
@@ -397,16 +443,16 @@ Layout Communicator::layout() const {
     return L;
 }
 
-int Communicator::max_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_blocks : num_cus_; }
+int Communicator::max_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_blocks : cus_min_; }
 
 // The mesh keeps more remote stores in flight with two blocks per CU (k_mesh:
 // 100 VGPRs, 4 blocks per CU fit): 1 GiB on 2 ranks 1.86 -> 1.65-1.69 ms at
-// 384-512 blocks (tools/mesh_sweep*.sh).  Only when no other rank shares this
-// GPU: several ranks' oversubscribed launches on one GPU could keep a waiting
-// role's partner blocks from being dispatched.
-int Communicator::mesh_blocks() const {
-    if (cfg_.max_blocks > 0) return cfg_.max_blocks;
-    return shared_gpu_ ? num_cus_ : 2 * num_cus_;
+// 384-512 blocks (tools/mesh_sweep*.sh).  Ranks sharing a GPU get their share
+// of the resident blocks through LaunchGrid.
+int Communicator::mesh_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_blocks : 2 * cus_min_; }
+
+int Communicator::LaunchGrid(int want, int blocks_per_cu) const {
+    return ResidentGrid(want, blocks_per_cu, cus_min_, share_max_);
 }
 
 void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStream_t stream, int algo) {
@@ -459,7 +505,8 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
     algo = PickAlgo(algo, total);
     if (units && algo != RDC_ALGO_MESH) throw std::logic_error("rdc: unit-table launch needs the mesh schedule");
     if (algo == RDC_ALGO_ONESHOT) {
-        const Piece p = PlanOneshotRanges(n_, off, len, total, layout(), cfg_.tile_bytes, max_blocks());
+        const Piece p = PlanOneshotRanges(n_, off, len, total, layout(), cfg_.tile_bytes,
+                                          LaunchGrid(max_blocks(), ks.occupancy(RDC_KIND_ONESHOT, n_)));
         CollArgs a;
         FillArgsCommon(&a);
         a.kind = RDC_KIND_ONESHOT;
@@ -482,9 +529,11 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         hip_check(ks.oneshot(a, p.nb_scatter, stream), "launch one-shot allreduce");
         return;
     }
+    const int grid_cap =
+        algo == RDC_ALGO_MESH ? LaunchGrid(mesh_blocks(), ks.occupancy(RDC_KIND_MESH, n_))
+                              : LaunchGrid(max_blocks(), ks.occupancy(RDC_KIND_RING, n_));
     const std::vector<Piece> plan =
-        PlanAllreduceRanges(n_, off, len, esz, layout(), algo, cfg_.tile_bytes,
-                            algo == RDC_ALGO_MESH ? mesh_blocks() : max_blocks(), cfg_.mesh_split);
+        PlanAllreduceRanges(n_, off, len, esz, layout(), algo, cfg_.tile_bytes, grid_cap, cfg_.mesh_split);
     for (const Piece& p : plan) {
         CollArgs a;
         FillArgsCommon(&a);
@@ -524,17 +573,20 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
     trace_ = nullptr;  // one call only
 }
 
-// Staging image of the coalesced path, grown on demand (never shrinks).
-char* Communicator::Image(uint64_t bytes) {
+// Staging image of the coalesced path, grown on demand (never shrinks).  The
+// old image is released stream-ordered (hipFreeAsync): launches already queued
+// may still read it, and a device-wide sync here would wait on kernels that
+// wait for ranks a single-process group has not launched yet.  Callers size it
+// once per call, before the call's first launch.
+char* Communicator::Image(uint64_t bytes, hipStream_t stream) {
     if (bytes > image_bytes_) {
         if (image_) {
-            hip_check(hipDeviceSynchronize(), "sync before image regrow");  // launches may still read it
-            (void)hipFree(image_);
+            hip_check(hipFreeAsync(image_, stream), "release coalesced image");
             image_ = nullptr;
             image_bytes_ = 0;
         }
         const uint64_t want = (bytes + ((uint64_t)1 << 20) - 1) & ~(((uint64_t)1 << 20) - 1);
-        hip_check(hipMalloc(&image_, want), "hipMalloc coalesced image");
+        hip_check(hipMallocAsync(reinterpret_cast<void**>(&image_), want, stream), "allocate coalesced image");
         image_bytes_ = want;
     }
     return image_;
@@ -542,9 +594,14 @@ char* Communicator::Image(uint64_t bytes) {
 
 // Unit table of one fusion group, cached by (dtype size, buffers, counts) so
 // repeated buckets (every training step) launch with no host->device traffic
-// and can be captured in a hipGraph once warm.
+// and can be captured in a hipGraph once warm.  Tables are stream-ordered
+// allocations uploaded on `stream` (no host sync: in a single-process group
+// a sync here would wait on kernels waiting for ranks not launched yet); an
+// evicted table is freed stream-ordered after the launches that read it, and
+// its host copy (the upload's source) is kept until an event says the stream
+// passed that point.
 const Communicator::PackEntry& Communicator::PackTable(void* const* bufs, const size_t* counts, int nbuf,
-                                                         size_t esz) {
+                                                         size_t esz, hipStream_t stream) {
     std::vector<uint64_t> key;
     key.reserve(2 + 2 * (size_t)nbuf);
     key.push_back(esz);
@@ -562,9 +619,22 @@ const Communicator::PackEntry& Communicator::PackTable(void* const* bufs, const 
         auto lru = pack_cache_.begin();
         for (auto j = pack_cache_.begin(); j != pack_cache_.end(); ++j)
             if (j->second.last_use < lru->second.last_use) lru = j;
-        hip_check(hipDeviceSynchronize(), "sync before pack-table eviction");
-        (void)hipFree(lru->second.dtable);
+        if (lru->second.dtable) hip_check(hipFreeAsync(lru->second.dtable, stream), "release pack table");
+        hipEvent_t ev = nullptr;
+        hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+        hip_check(hipEventRecord(ev, stream), "record");
+        retired_.emplace_back(ev, lru->second.host);
         pack_cache_.erase(lru);
+    }
+    for (size_t i = 0; i < retired_.size();) {  // host copies whose upload has surely finished
+        if (hipEventQuery(retired_[i].first) == hipSuccess) {
+            (void)hipEventDestroy(retired_[i].first);
+            retired_[i] = retired_.back();
+            retired_.pop_back();
+        } else {
+            (void)hipGetLastError();
+            ++i;
+        }
     }
     std::vector<uint64_t> cnt((size_t)nbuf);
     for (int b = 0; b < nbuf; ++b) cnt[(size_t)b] = counts[b];
@@ -579,10 +649,10 @@ const Communicator::PackEntry& Communicator::PackTable(void* const* bufs, const 
     e.total = P.total;
     e.nunits = (int)P.units.size();
     if (e.nunits > 0) {
-        hip_check(hipMalloc(&e.dtable, P.units.size() * sizeof(PackUnit)), "hipMalloc pack table");
-        // fresh memory no launch has seen: a synchronous copy cannot race
-        hip_check(hipMemcpy(e.dtable, P.units.data(), P.units.size() * sizeof(PackUnit), hipMemcpyHostToDevice),
-                  "upload pack table");
+        e.host = std::make_shared<std::vector<PackUnit>>(std::move(P.units));
+        const size_t tb = e.host->size() * sizeof(PackUnit);
+        hip_check(hipMallocAsync(reinterpret_cast<void**>(&e.dtable), tb, stream), "allocate pack table");
+        hip_check(hipMemcpyAsync(e.dtable, e.host->data(), tb, hipMemcpyHostToDevice, stream), "upload pack table");
     }
     e.last_use = ++pack_tick_;
     return pack_cache_.emplace(std::move(key), e).first->second;
@@ -620,7 +690,7 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
                 live += counts[b] != 0;
             }
             if (live >= 2 && PickAlgo(algo, bytes) == RDC_ALGO_MESH) {
-                const PackEntry& e = PackTable(bufs + b0, counts + b0, b1 - b0, esz);
+                const PackEntry& e = PackTable(bufs + b0, counts + b0, b1 - b0, esz, stream);
                 LaunchRanges(ks, nullptr, e.off, e.len, e.total, esz, RDC_ALGO_MESH, stream, e.dtable, e.nunits);
             } else {
                 CoalescedStaged(ks, bufs + b0, counts + b0, b1 - b0, dtype, op, esz, algo, stream);
@@ -637,6 +707,20 @@ void Communicator::CoalescedStaged(const KernelSet& ks, void* const* bufs, const
     std::vector<uint64_t> cnt((size_t)nbuf);
     for (int b = 0; b < nbuf; ++b) cnt[(size_t)b] = counts[b];
     const std::vector<int> bounds = GroupCoalesced(cnt.data(), nbuf, esz, cfg_.fuse_bytes);
+    // the image is sized once, for the largest group, before the first launch
+    // (an upper bound of PlanCoalesced's total: 16-B segments, 256-B chunks)
+    uint64_t need = 0;
+    for (size_t g = 0; g + 1 < bounds.size(); ++g) {
+        uint64_t bytes = (uint64_t)RDC_SLOT_ALIGN * (uint64_t)n_;
+        int live = 0;
+        for (int b = bounds[g]; b < bounds[g + 1]; ++b)
+            if (counts[b]) {
+                ++live;
+                bytes += (uint64_t)n_ * 16 + ((uint64_t)counts[b] * esz + 15) / 16 * 16;
+            }
+        if (live >= 2) need = std::max(need, bytes);
+    }
+    char* img = need ? Image(need, stream) : nullptr;
     for (size_t g = 0; g + 1 < bounds.size(); ++g) {
         const int b0 = bounds[g], b1 = bounds[g + 1];
         int live = 0, last = -1;
@@ -647,8 +731,8 @@ void Communicator::CoalescedStaged(const KernelSet& ks, void* const* bufs, const
             Allreduce(bufs[last], counts[last], dtype, op, stream, algo);
             continue;
         }
-        const PackEntry& e = PackTable(bufs + b0, counts + b0, b1 - b0, esz);
-        char* img = Image(e.total);
+        const PackEntry& e = PackTable(bufs + b0, counts + b0, b1 - b0, esz, stream);
+        if (e.total > image_bytes_) throw std::logic_error("rdc: coalesced image smaller than its group");
         const int grid = std::max(1, std::min(e.nunits, 2 * num_cus_));
         hip_check(launch_pack(e.dtable, e.nunits, img, 0, grid, stream), "launch pack");
         LaunchRanges(ks, img, e.off, e.len, e.total, esz, algo, stream);
@@ -661,7 +745,8 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
     if (n_ == 1 || bytes == 0) return;
     if (buf == nullptr) throw std::invalid_argument("rdc: null buffer");
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    for (const Piece& p : PlanBroadcast(bytes, layout(), cfg_.tile_bytes, max_blocks())) {
+    for (const Piece& p :
+         PlanBroadcast(bytes, layout(), cfg_.tile_bytes, LaunchGrid(max_blocks(), occupancy_bcast()))) {
         CollArgs a;
         FillArgsCommon(&a);
         a.user = static_cast<char*>(buf);
@@ -739,7 +824,8 @@ void Communicator::Allgather(void* const* bufs, const uint64_t* sizes, hipStream
     for (int c = 0; c < n_; ++c)
         if (sizes[c] && bufs[c] == nullptr) throw std::invalid_argument("rdc: null allgather buffer");
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    for (const Piece& p : PlanAllgather(n_, sizes, layout(), cfg_.tile_bytes, max_blocks())) {
+    for (const Piece& p :
+         PlanAllgather(n_, sizes, layout(), cfg_.tile_bytes, LaunchGrid(max_blocks(), occupancy_allgather()))) {
         CollArgs a;
         FillArgsCommon(&a);
         for (int c = 0; c < n_; ++c) a.cbuf[c] = static_cast<char*>(bufs[c]);

@@ -38,6 +38,10 @@ struct CommConfig {
     size_t fuse_bytes_direct = (size_t)16 << 30;  // ... in groups of up to this many data bytes
     size_t bcast_split_bytes = (size_t)1 << 20;   // broadcast pieces from this size: root -> forwarders -> ranks
     MeshSplit mesh_split;                          // mesh roles in sixteenths of the grid (RDC_MESH_SPLIT=s,r)
+    // rdc_reduce_ring_mincount (src/comm/communicator_manager.cc:46, default 1
+    // byte): allreduces of at most this many bytes take the reference's tree
+    // order instead of the ring's (communicator_collective.cc:6-13)
+    size_t ring_mincount = 1;
 };
 
 struct KernelSet;
@@ -121,9 +125,14 @@ public:
     uint32_t seq() const { return seq_; }
     const CommConfig& config() const { return cfg_; }
     Layout layout() const;
+    // requested grids (RDC_NBLOCKS / Tune, else automatic); every launch is then
+    // clamped to what stays resident next to the other ranks on its GPU
+    // (LaunchGrid, rdc_plan.h ResidentGrid)
     int max_blocks() const;
-    int mesh_blocks() const;        // grid of a mesh launch
-    bool shared_gpu() const { return shared_gpu_; }
+    int mesh_blocks() const;
+    int LaunchGrid(int want, int blocks_per_cu) const;
+    bool shared_gpu() const { return share_max_ > 1; }
+    int ranks_per_gpu() const { return share_max_; }
 
 private:
     Communicator();
@@ -140,10 +149,11 @@ private:
         uint64_t off[RDC_MAX_RANKS] = {}, len[RDC_MAX_RANKS] = {};
         uint64_t total = 0;
         uint64_t last_use = 0;
+        std::shared_ptr<std::vector<PackUnit>> host;  // the upload's source, alive until the copy is done
     };
     static constexpr size_t kPackCacheMax = 64;
-    const PackEntry& PackTable(void* const* bufs, const size_t* counts, int nbuf, size_t esz);
-    char* Image(uint64_t bytes);
+    const PackEntry& PackTable(void* const* bufs, const size_t* counts, int nbuf, size_t esz, hipStream_t stream);
+    char* Image(uint64_t bytes, hipStream_t stream);
     void CoalescedStaged(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, int dtype, int op,
                          size_t esz, int algo, hipStream_t stream);
 
@@ -168,13 +178,15 @@ private:
     uint32_t max_tiles_ = 0;
     uint32_t seq_ = 0;
     int alloc_kind_ = 0;
-    int num_cus_ = 256;
-    bool shared_gpu_ = false;       // another rank of this communicator runs on the same physical GPU
+    int num_cus_ = 256;             // this GPU
+    int cus_min_ = 256;             // fewest CUs of any rank's GPU (grids are planned identically on all ranks)
+    int share_max_ = 1;             // most ranks of this communicator on one physical GPU
     int wall_khz_ = 100000;         // wall_clock64() rate
     char* peer_scratch_[RDC_MAX_RANKS] = {};
     char* peer_ag_[RDC_MAX_RANKS] = {};
     uint32_t* peer_flags_[RDC_MAX_RANKS] = {};
     std::map<std::vector<uint64_t>, PackEntry> pack_cache_;
+    std::vector<std::pair<hipEvent_t, std::shared_ptr<std::vector<PackUnit>>>> retired_;  // evicted host copies
     uint64_t pack_tick_ = 0;
     char* image_ = nullptr;         // coalesced staging image (local HBM)
     uint64_t image_bytes_ = 0;

@@ -12,10 +12,17 @@ struct KernelSet {
     hipError_t (*mesh)(const CollArgs& a, int grid, hipStream_t s);
     hipError_t (*ring)(const CollArgs& a, int grid, hipStream_t s);
     hipError_t (*oneshot)(const CollArgs& a, int grid, hipStream_t s);
+    // resident blocks per CU of the kernel a launch of `kind` (RDC_KIND_MESH /
+    // RING / ONESHOT) on n ranks uses (hipOccupancyMaxActiveBlocksPerMultiprocessor,
+    // cached); the grid clamp of ResidentGrid (rdc_plan.h)
+    int (*occupancy)(int kind, int n);
 };
 
 // false if (dtype, op) is not a valid reference combination
 bool get_kernels(int dtype, int op, KernelSet* ks);
+// resident blocks per CU of k_bcast / k_allgather
+int occupancy_bcast();
+int occupancy_allgather();
 hipError_t launch_bcast(const CollArgs& a, int grid, hipStream_t s);
 hipError_t launch_allgather(const CollArgs& a, int grid, hipStream_t s);
 // coalesced allreduce: units[i].buf = user address; unpack = image -> buffers

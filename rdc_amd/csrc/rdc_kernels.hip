@@ -166,6 +166,30 @@ bool get_kernels(int dtype, int op, KernelSet* ks) {
         default: return false;
     }
 }
+namespace {
+template <typename F>
+int occupancy_of(F kernel, int* cache) {
+    if (*cache > 0) return *cache;
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kBlock, 0) != hipSuccess || b <= 0) {
+        (void)hipGetLastError();
+        b = 1;
+    }
+    *cache = b;
+    return b;
+}
+}  // namespace
+
+int occupancy_bcast() {
+    static int c = 0;
+    return occupancy_of(k_bcast, &c);
+}
+
+int occupancy_allgather() {
+    static int c = 0;
+    return occupancy_of(k_allgather, &c);
+}
+
 hipError_t launch_allgather(const CollArgs& a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_allgather, dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();

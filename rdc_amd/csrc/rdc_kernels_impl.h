@@ -683,6 +683,28 @@ struct Kernels {
         hipLaunchKernelGGL((k_ring<OP, T>), dim3(grid), dim3(kBlock), 0, s, a);
         return hipGetLastError();
     }
+    static int occupancy(int kind, int n) {
+        // [mesh 8, mesh 16, oneshot 8, oneshot 16, ring]; 0 = not queried yet
+        static int cache[5] = {0, 0, 0, 0, 0};
+        const int wide = n > 8 ? 1 : 0;
+        const int slot = kind == RDC_KIND_RING ? 4 : (kind == RDC_KIND_ONESHOT ? 2 : 0) + wide;
+        if (cache[slot] > 0) return cache[slot];
+        int b = 0;
+        hipError_t e = hipSuccess;
+        switch (slot) {
+            case 0: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_mesh<OP, T, 8>, kBlock, 0); break;
+            case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_mesh<OP, T, 16>, kBlock, 0); break;
+            case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_oneshot<OP, T, 8>, kBlock, 0); break;
+            case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_oneshot<OP, T, 16>, kBlock, 0); break;
+            default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_ring<OP, T>, kBlock, 0); break;
+        }
+        if (e != hipSuccess || b <= 0) {
+            (void)hipGetLastError();
+            b = 1;  // unknown: one block per CU is always resident
+        }
+        cache[slot] = b;
+        return b;
+    }
 };
 
 
@@ -691,6 +713,7 @@ struct Kernels {
     ks->mesh = &Kernels<OP, T>::mesh;     \
     ks->ring = &Kernels<OP, T>::ring;     \
     ks->oneshot = &Kernels<OP, T>::oneshot; \
+    ks->occupancy = &Kernels<OP, T>::occupancy; \
     return true;
 
 // integer element types (every operator)

@@ -33,6 +33,11 @@ void SplitRanges(int64_t count, int n, int64_t* b, int64_t* e) {
     }
 }
 
+int ResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu) {
+    const long cap = std::max(1L, (long)std::max(1, blocks_per_cu) * std::max(1, cus) / std::max(1, ranks_per_gpu));
+    return (int)std::max(1L, std::min<long>(want, cap));
+}
+
 void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blocks, Piece* p, MeshSplit split) {
     const int s16 = std::min(std::max(split.s16, 1), 14), r16 = std::min(std::max(split.r16, 1), 15 - s16);
     size_t t = cfg_tile;

@@ -45,6 +45,16 @@ struct Piece {
 struct MeshSplit {
     int s16 = 4, r16 = 8;
 };
+// Grid of a launch whose blocks wait on peers' blocks.  Every waiting block of
+// every rank must be resident at once, or a rank's waiters can occupy the CUs
+// its own (or a co-located rank's) producers need: the launch then ends in the
+// device timeout (4 ranks on one GPU, k_ring at 768 blocks each, round 1).
+// Residency = blocks_per_cu (hipOccupancyMaxActiveBlocksPerMultiprocessor of
+// the kernel) x cus / ranks_per_gpu (the most ranks sharing one physical GPU).
+// Every rank computes it from the same exchanged values, so the grid — and
+// the tile plan derived from it — is identical on all ranks.
+int ResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu);
+
 // tile size and grid for a piece whose largest chunk is chunk_bytes
 void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blocks, Piece* p,
                MeshSplit split = MeshSplit());

@@ -101,10 +101,21 @@ def main():
                     check_call(_LIB.RdcCommAllreduceCoalesced(comm.handle, arr, cnt, len(counts), dtype, c["op"],
                                                               c.get("algo", 0), sp))
             comm.check(sp)
-            out = np.concatenate([t[pd: pd + k * esz[dtype]].cpu().numpy() for t, pd, k in zip(bufs, pads, counts)])
-            np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
+            if c.get("digest"):  # full-size lists: sha256 over the buckets in order
+                import hashlib
+                h = hashlib.sha256()
+                for t, pd, k in zip(bufs, pads, counts):
+                    h.update(t[pd: pd + k * esz[dtype]].cpu().numpy().tobytes())
+                open(os.path.join(outdir, "case%d_rank%d.sha" % (i, rank)), "w").write(h.hexdigest())
+            else:
+                out = np.concatenate([t[pd: pd + k * esz[dtype]].cpu().numpy()
+                                      for t, pd, k in zip(bufs, pads, counts)])
+                np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
+            del bufs
             print("rank %d case %d ok" % (rank, i), flush=True)
             continue
+        if c.get("last_launch"):  # record the launch shape the library chose (grid clamp checks)
+            ll = (ctypes.c_uint64 * 6)()
         reps = c.get("reps", 1)
         for _ in range(reps):
             if kind == "allreduce":
@@ -123,8 +134,12 @@ def main():
                 buf[pad: pad + nbytes] = torch.from_numpy(host).cuda()
         log("rank", rank, "case", i, "launched")
         comm.check(sp)
+        if c.get("last_launch"):
+            check_call(_LIB.RdcCommLastLaunch(comm.handle, ll))
+            open(os.path.join(outdir, "case%d_rank%d.launch" % (i, rank)), "w").write(json.dumps([int(x) for x in ll]))
         log("rank", rank, "case", i, "done")
         out = buf[pad: pad + nbytes].cpu().numpy()
+        del buf
         if c.get("digest"):
             import hashlib
             open(os.path.join(outdir, "case%d_rank%d.sha" % (i, rank)), "w").write(

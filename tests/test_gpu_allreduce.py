@@ -228,7 +228,9 @@ def run_mp(world, cases, timeout=240, env_extra=None):
         json.dump(cases, f)
     port = free_port()
     env = dict(os.environ)
-    env.update({"RDC_DEVICE": "0", "RDC_NBLOCKS": env.get("RDC_NBLOCKS", "32"), "RDC_SCRATCH_BYTES": "64M"})
+    # grids are left to the library (clamped to what stays resident with
+    # `world` ranks on GPU 0) unless a test forces RDC_NBLOCKS
+    env.update({"RDC_DEVICE": "0", "RDC_SCRATCH_BYTES": "64M"})
     env.update(env_extra or {})
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), str(r), str(world),
                                str(port), tmp, cf], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
@@ -340,24 +342,85 @@ def test_mp_full_size_cfg2():
             assert open(os.path.join(tmp, "case%d_rank%d.sha" % (i, r))).read() == h, (i, r)
 
 
+def full_digest(count, dt, world, seed=0x5EED0000):
+    import hashlib
+    want = expected_for({"count": count, "dtype": dt, "op": 2, "seed": seed}, world)
+    h = hashlib.sha256(np.frombuffer(want[0].tobytes(), dtype=np.uint8).tobytes()).hexdigest()
+    del want
+    return h
+
+
 def test_mp_full_size_cfg3_cfg4_eight_ranks():
-    """BASELINE cfg3 / cfg4 at full size and rank count: 1 GiB fp32 and 1 GiB
-    fp16 allreduces over 8 processes (sharing GPU 0 here: 32 blocks each so
-    all 8 grids stay resident), each rank's result checked bit-exact (sha256)
-    against the oracle's ring — the exact launch plan of the 8-GPU run
-    (NMAX = 8 kernels, one launch per call), only the grid is smaller."""
+    """BASELINE cfg3 / cfg4 at full size and rank count: 1 GiB fp32 (mesh AND
+    the reference's ring schedule, k_ring) and 1 GiB fp16 allreduces over 8
+    processes (sharing GPU 0 here; automatic grids, clamped so all 8 grids
+    stay resident), each rank's result checked bit-exact (sha256) against the
+    oracle's ring — the 8-GPU run's launch plan (NMAX = 8 kernels, one launch
+    per call), only the grid is smaller."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [{"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 2, "digest": True},
+             {"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 1, "digest": True, "last_launch": True},
+             {"count": (1 << 30) // 2, "dtype": 10, "op": 2, "algo": 2, "digest": True}]
+    tmp = run_mp(8, cases, timeout=600, env_extra={"RDC_SCRATCH_BYTES": "4080M"})
+    want = {6: full_digest((1 << 30) // 4, 6, 8), 10: full_digest((1 << 30) // 2, 10, 8)}
+    for i, c in enumerate(cases):
+        for r in range(8):
+            assert open(os.path.join(tmp, "case%d_rank%d.sha" % (i, r))).read() == want[c["dtype"]], (i, r)
+    # the ring ran as ONE launch per call with one tile per block
+    grid = json.load(open(os.path.join(tmp, "case1_rank0.launch")))
+    assert grid[5] == 1 and grid[0] >= 1, grid
+
+
+def test_mp_cfg5_exact_shape_eight_ranks():
+    """BASELINE cfg5 at its exact shape: 1024 x 1 MiB fp32 buckets (separate
+    allocations, per-bucket misalignment) in ONE RdcCommAllreduceCoalesced
+    call over 8 processes — the unit-table mesh with NMAX = 8 — twice with
+    the cached unit table; every rank's 1 GiB of results checked (sha256)
+    against 1024 oracle rings (test/mallreduce.cc:17-53 shape)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import hashlib
-    cases = [{"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 2, "digest": True},
-             {"count": (1 << 30) // 2, "dtype": 10, "op": 2, "algo": 2, "digest": True}]
-    tmp = run_mp(8, cases, timeout=400, env_extra={"RDC_NBLOCKS": "32", "RDC_SCRATCH_BYTES": "4080M"})
+    K, per = 1024, 1 << 18
+    cases = [{"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [per] * K, "reps": 2,
+              "digest": True}]
+    tmp = run_mp(8, cases, timeout=600, env_extra={"RDC_SCRATCH_BYTES": "4080M"})
+    h = hashlib.sha256()
+    for b in range(K):
+        xs = [O.fill(per, 6, 0x5EED0000 + b, r) for r in range(8)]
+        for _ in range(2):
+            O.allreduce_ring(xs, 6, 2)
+        h.update(xs[0].tobytes())
+    for r in range(8):
+        assert open(os.path.join(tmp, "case0_rank%d.sha" % r)).read() == h.hexdigest(), r
+
+
+def test_mp_forced_oversized_grid_four_ranks():
+    """RDC_NBLOCKS=4096 (4x what one GPU holds) on 4 processes sharing GPU 0:
+    every waiting launch is clamped to the resident share (ResidentGrid), so
+    the ring (>= 256 tiles per chunk), mesh, one-shot, broadcast and allgather
+    all complete bit-exact instead of timing out (round 1: k_ring at 768
+    blocks x 4 ranks on one GPU hit the device timeout)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [{"count": 16 << 20, "dtype": 6, "op": 2, "algo": 1, "last_launch": True, "reps": 2},
+             {"count": 16 << 20, "dtype": 6, "op": 2, "algo": 2, "last_launch": True},
+             {"count": 100003, "dtype": 6, "op": 2, "algo": 3},
+             {"count": (5 << 20) + 3, "dtype": 0, "kind": "broadcast", "root": 2},
+             {"count": 200001, "dtype": 2, "kind": "allgather"}]
+    tmp = run_mp(4, cases, timeout=400, env_extra={"RDC_NBLOCKS": "4096", "RDC_SCRATCH_BYTES": "512M",
+                                                   "RDC_TILE_BYTES": "16K"})
     for i, c in enumerate(cases):
-        want = expected_for(c, 8)
-        h = hashlib.sha256(np.frombuffer(want[0].tobytes(), dtype=np.uint8).tobytes()).hexdigest()
-        del want
-        for r in range(8):
-            assert open(os.path.join(tmp, "case%d_rank%d.sha" % (i, r))).read() == h, (i, r)
+        want = expected_for(c, 4)
+        for r in range(4):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    for i in (0, 1):
+        ll = json.load(open(os.path.join(tmp, "case%d_rank0.launch" % i)))
+        assert ll[0] < 4096 and ll[0] <= 8 * cus // 4, ll  # clamped (8 blocks per CU is the hardware ceiling)
+    ll = json.load(open(os.path.join(tmp, "case0_rank0.launch")))
+    assert (16 << 20) * 4 // 4 // ll[4] >= 256, ll  # ring: >= 256 tiles per chunk
 
 
 def test_mp_many_small_buckets_cfg5_shape():

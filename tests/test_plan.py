@@ -179,3 +179,34 @@ def test_mixed_plan_is_deterministic():
     assert {op["kind"] for op in a} >= {"allreduce", "bcast", "allgather", "coalesced"}
     small = make_plan(5, 6, 2)
     assert expected(small, 2).size == output_bytes(small)
+
+
+@pytest.mark.parametrize("want,per_cu,cus,share,expect", [
+    (512, 4, 256, 1, 512),        # one rank per GPU: the mesh's 2 blocks per CU fit
+    (768, 4, 256, 1, 768),        # bench tuning sweep, 3 per CU: still resident
+    (4096, 4, 256, 1, 1024),      # RDC_NBLOCKS far above what one GPU holds
+    (768, 4, 256, 4, 256),        # round 1's timeout: 4 ranks on one GPU, 768 ring blocks each
+    (512, 4, 256, 8, 128),        # 8 ranks on one GPU (the rehearsals)
+    (256, 8, 256, 12, 170),       # 12 ranks: floor(8 * 256 / 12)
+    (4096, 1, 1, 16, 1),          # never below one block
+    (0, 4, 256, 1, 1),
+])
+def test_resident_grid_clamp(want, per_cu, cus, share, expect):
+    """Grids of waiting kernels are clamped so every rank's blocks are
+    resident at once (rdc_plan.cpp ResidentGrid): RDC_NBLOCKS / RdcCommTune
+    input included."""
+    from rdc_amd._lib import _LIB
+    got = _LIB.RdcPlanResidentGrid(want, per_cu, cus, share)
+    assert got == expect
+    assert got * share <= max(per_cu * cus, share)  # all ranks' grids fit together
+
+
+def test_resident_grid_never_oversubscribes():
+    from rdc_amd._lib import _LIB
+    rng = np.random.default_rng(3)
+    for _ in range(2000):
+        want, per_cu, cus, share = (int(rng.integers(1, 8192)), int(rng.integers(1, 9)), int(rng.integers(1, 305)),
+                                    int(rng.integers(1, 17)))
+        g = _LIB.RdcPlanResidentGrid(want, per_cu, cus, share)
+        assert 1 <= g <= want
+        assert g == want or g * share <= per_cu * cus or g == 1
