@@ -142,7 +142,11 @@ int RdcCommIRecv(void** wc, void* comm, void* buf, size_t bytes, int src, void* 
 int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op, void* stream);
 /* algo: 0 auto, 1 ring (the reference schedule), 2 mesh (all links), 3 one-shot (small buffers:
  * every rank pushes the whole buffer to every peer, one hand-off); auto = one-shot when
- * (n-1) x bytes <= RDC_ONESHOT_BYTES (default 1 MiB), else mesh.  All bit-identical. */
+ * (n-1) x bytes <= RDC_ONESHOT_BYTES (default 1 MiB), else mesh.  All bit-identical.
+ * Whatever the algo, a buffer of at most rdc_reduce_ring_mincount bytes (default 1) takes
+ * the reference's TREE order (TryAllreduce, src/comm/communicator_collective.cc:6-13: the
+ * fold of TryReduceTree to rank 0, every rank receiving the root's bits) as one one-shot
+ * style hand-off; algo 4 forces that tree order for any size. */
 int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream);
 /* device-resident coalesced allreduce (see RdcAllreduceCoalesced), stream-ordered.
  * The per-group unit table is cached by (buffers, counts): after a first
@@ -222,6 +226,11 @@ int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, voi
  * the communicator on one physical GPU, cus the fewest CUs of any rank's GPU.
  * Returns the grid (not a status). */
 int RdcPlanResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu);
+/* The tree allreduce's fold for n ranks (rdc_reduce_ring_mincount path): the
+ * post-order program acc[dst[i]] = OP(acc[dst[i]], acc[src[i]]), i < n-1,
+ * over the n ranks' inputs (acc[q] = rank q's value); the result is acc[0].
+ * dst/src hold >= 16 ints.  Returns n-1, or -1 on bad arguments. */
+int RdcPlanTree(int n, int* dst, int* src);
 int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4);
 int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int algo, size_t tile_bytes,
                      int max_blocks, uint64_t* out, int max_pieces, int* out_pieces);

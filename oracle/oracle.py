@@ -57,6 +57,9 @@ def lib():
         L.rdc_oracle_allreduce_ring.argtypes = [ctypes.POINTER(vp), ctypes.c_int, u64, ctypes.c_int, ctypes.c_int]
         L.rdc_oracle_allreduce_closed_form.argtypes = [ctypes.POINTER(vp), ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, vp]
         L.rdc_oracle_fill.argtypes = [vp, u64, ctypes.c_int, u64, ctypes.c_int]
+        L.rdc_oracle_allreduce_tree.argtypes = [ctypes.POINTER(vp), ctypes.c_int, u64, ctypes.c_int, ctypes.c_int]
+        L.rdc_oracle_tree_program.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.rdc_oracle_tree.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_int)] * 4
         L.rdc_oracle_fill_at.argtypes = [vp, u64, u64, ctypes.c_int, u64, ctypes.c_int]
         L.rdc_oracle_allreduce_window.argtypes = [ctypes.POINTER(vp), ctypes.c_int, u64, u64, u64, ctypes.c_int,
                                                   ctypes.c_int, vp]
@@ -179,6 +182,42 @@ def expected_window(total, first, m, n, dtype, op, seed):
     if rc:
         raise ValueError("allreduce_window rc=%d" % rc)
     return out
+
+
+def tree_program(n):
+    """The small-buffer (rdc_reduce_ring_mincount) path's fold for n ranks:
+    [(dst, src), ...] with acc[dst] = OP(acc[dst], acc[src]), result acc[0]
+    (oracle/tree_order.cc)."""
+    d, s = (ctypes.c_int * 16)(), (ctypes.c_int * 16)()
+    k = lib().rdc_oracle_tree_program(n, d, s)
+    if k < 0:
+        raise ValueError("tree_program n=%d" % n)
+    return [(d[i], s[i]) for i in range(k)]
+
+
+def tree(n):
+    """(children-in-fold-order per rank, parent, depth) of the reference's tree."""
+    nc, ch, par, dep = (ctypes.c_int * 16)(), (ctypes.c_int * 256)(), (ctypes.c_int * 16)(), (ctypes.c_int * 16)()
+    if lib().rdc_oracle_tree(n, nc, ch, par, dep):
+        raise ValueError("tree n=%d" % n)
+    return [[ch[r * 16 + i] for i in range(nc[r])] for r in range(n)], list(par[:n]), list(dep[:n])
+
+
+def allreduce_tree(bufs, dtype, op):
+    """TryAllreduceTree over per-rank numpy buffers (in place): every buffer
+    receives the root's tree reduction.  Returns bufs."""
+    n = len(bufs)
+    arr = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+    rc = lib().rdc_oracle_allreduce_tree(arr, n, bufs[0].size, dtype, op)
+    if rc:
+        raise ValueError("oracle tree allreduce rc=%d" % rc)
+    return bufs
+
+
+def expected_tree(inputs, dtype, op):
+    bufs = [np.ascontiguousarray(x).copy() for x in inputs]
+    allreduce_tree(bufs, dtype, op)
+    return bufs[0]
 
 
 def expected_allreduce(inputs, dtype, op):

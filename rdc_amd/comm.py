@@ -43,8 +43,8 @@ class WorkComp(object):
 def _is_tensor(x):
     return hasattr(x, "data_ptr") and hasattr(x, "is_cuda")
 
-ALGO_AUTO, ALGO_RING, ALGO_MESH, ALGO_ONESHOT = 0, 1, 2, 3
-_ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "mesh": ALGO_MESH, "oneshot": ALGO_ONESHOT}
+ALGO_AUTO, ALGO_RING, ALGO_MESH, ALGO_ONESHOT, ALGO_TREE = 0, 1, 2, 3, 4
+_ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "mesh": ALGO_MESH, "oneshot": ALGO_ONESHOT, "tree": ALGO_TREE}
 
 
 class Comm(object):

@@ -84,6 +84,7 @@ void set_param(Manager& m, const char* name, const char* val) {
         std::string v(val);
         m.cfg.algo = v == "ring" ? RDC_ALGO_RING : v == "mesh" ? RDC_ALGO_MESH : v == "oneshot" ? RDC_ALGO_ONESHOT
                                                                                                 : RDC_ALGO_AUTO;
+        // (the tree is chosen by size through rdc_reduce_ring_mincount, as in the reference)
     } else if (k == "RDC_NBLOCKS") m.cfg.max_blocks = atoi(val);
     else if (k == "RDC_TILE_BYTES") m.cfg.tile_bytes = parse_unit(val);
     else if (k == "RDC_TIMEOUT") m.cfg.timeout_s = atof(val);
@@ -485,7 +486,7 @@ int RdcAllreduceCoalescedOn(void* comm, void** bufs, const size_t* counts, int n
 int RdcCommAllreduceCoalesced(void* comm, void* const* dev_bufs, const size_t* counts, int nbuf, int dtype, int op,
                               int algo, void* stream) {
     return guard([&] {
-        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_ONESHOT) throw std::invalid_argument("rdc: bad algo");
+        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_TREE) throw std::invalid_argument("rdc: bad algo");
         as_comm(comm)->AllreduceCoalesced(dev_bufs, counts, nbuf, dtype, op, static_cast<hipStream_t>(stream), algo);
     });
 }
@@ -519,7 +520,7 @@ int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op,
 
 int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream) {
     return guard([&] {
-        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_ONESHOT) throw std::invalid_argument("rdc: bad algo");
+        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_TREE) throw std::invalid_argument("rdc: bad algo");
         as_comm(comm)->Allreduce(dev_buf, count, dtype, op, static_cast<hipStream_t>(stream), algo);
     });
 }
@@ -611,6 +612,11 @@ int RdcReduce(void* dst, const void* src, size_t count, int dtype, int op, void*
 
 int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, void* stream) {
     return guard([&] { DeviceFill(dev_buf, count, dtype, seed, rank, static_cast<hipStream_t>(stream)); });
+}
+
+int RdcPlanTree(int n, int* dst, int* src) {
+    if (n < 1 || n > RDC_MAX_RANKS || !dst || !src) return -1;
+    return PlanTreeProgram(n, dst, src);
 }
 
 int RdcPlanResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu) {

@@ -183,6 +183,7 @@ void Communicator::AllocLocal() {
     peer_ag_[rank_] = scratch_ag_;
     peer_flags_[rank_] = flags_;
     peer_p2p_[rank_] = p2p_;
+    tree_len_ = PlanTreeProgram(n_, tree_dst_, tree_src_);
 }
 
 Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int device, const CommConfig& cfg) {
@@ -466,6 +467,12 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
     if (n_ == 1 || count == 0) return;
     if (buf == nullptr) throw std::invalid_argument("rdc: null buffer");
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    // TryAllreduce (communicator_collective.cc:6-13): the ring for buffers of
+    // more than rdc_reduce_ring_mincount bytes, the tree's order otherwise
+    if ((uint64_t)count * esz <= cfg_.ring_mincount || algo == RDC_ALGO_TREE) {
+        LaunchTree(ks, static_cast<char*>(buf), (uint64_t)count * esz, stream);
+        return;
+    }
     int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
     SplitRanges((int64_t)count, n_, cb, ce);  // utils::Split (include/utils/utils.h:59-70)
     uint64_t off[RDC_MAX_RANKS] = {0}, len[RDC_MAX_RANKS] = {0};
@@ -495,6 +502,47 @@ void Communicator::AllreduceRanges(void* buf, const uint64_t* off, const uint64_
     int algo = PickAlgo(RDC_ALGO_AUTO);
     if (algo == RDC_ALGO_ONESHOT) algo = RDC_ALGO_MESH;
     LaunchRanges(ks, static_cast<char*>(buf), off, len, total, esz, algo, stream);
+}
+
+// The reference's small-buffer path (TryAllreduceTree: TryReduceTree to rank
+// 0, TryBroadcast from it, communicator_collective.cc:14-78) as ONE hand-off:
+// every rank pushes its buffer into every peer's one-shot slot, then folds the
+// n inputs in the tree's order (PlanTreeProgram) — the root's bits, which the
+// reference's broadcast gives every rank.  Buffers above half a slot go in
+// pieces (the fold is per element).  Uses the one-shot's slot halves and gates.
+void Communicator::LaunchTree(const KernelSet& ks, char* buf, uint64_t total, hipStream_t stream) {
+    if (total == 0) return;
+    const uint64_t cap = OneshotHalfBytes(layout());
+    const int grid_cap = LaunchGrid(max_blocks(), ks.occupancy(RDC_KIND_TREE, n_));
+    const uint64_t zero[RDC_MAX_RANKS] = {0};
+    for (uint64_t off = 0; off < total; off += cap) {
+        const uint64_t len = std::min<uint64_t>(cap, total - off);
+        const Piece p = PlanOneshotRanges(n_, zero, zero, len, layout(), cfg_.tile_bytes, grid_cap);
+        CollArgs a;
+        FillArgsCommon(&a);
+        a.kind = RDC_KIND_ONESHOT;  // same slot protocol: the next mesh / ring launch gates on it
+        a.user = buf + off;
+        a.tiles[0] = p.tiles[0];
+        a.tile_bytes = p.tile_bytes;
+        a.total_bytes = len;
+        a.tree_len = tree_len_;
+        for (int i = 0; i < tree_len_; ++i) {
+            a.tree_dst[i] = (int8_t)tree_dst_[i];
+            a.tree_src[i] = (int8_t)tree_src_[i];
+        }
+        if (off + len >= total) {
+            a.notify = notify_;
+            a.notify_val = notify_val_;
+            notify_ = nullptr;
+        }
+        last_launch_[0] = last_launch_[1] = (uint64_t)p.nb_scatter;
+        last_launch_[2] = last_launch_[3] = 0;
+        last_launch_[4] = p.tile_bytes;
+        last_launch_[5] = RDC_ALGO_TREE;
+        ++seq_;
+        hip_check(ks.tree(a, p.nb_scatter, stream), "launch tree allreduce");
+    }
+    trace_ = nullptr;
 }
 
 // The schedule over explicit chunk byte ranges of `buf` (chunk c = [off[c],
@@ -672,6 +720,24 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
     }
     if (n_ == 1 || nbuf == 0) return;
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    if (algo == RDC_ALGO_TREE || cfg_.ring_mincount >= esz) {
+        // buffers of <= rdc_reduce_ring_mincount bytes take the tree's order
+        // (TryAllreduce per buffer, communicator_collective.cc:6-13); the
+        // tree fold is the same for every element, so they are packed into
+        // the staging image together and folded in ONE tree launch
+        std::vector<void*> sb, lb;
+        std::vector<size_t> sc, lc;
+        for (int b = 0; b < nbuf; ++b) {
+            if (counts[b] == 0) continue;
+            const bool small = algo == RDC_ALGO_TREE || (uint64_t)counts[b] * esz <= cfg_.ring_mincount;
+            (small ? sb : lb).push_back(bufs[b]);
+            (small ? sc : lc).push_back(counts[b]);
+        }
+        if (!sb.empty()) CoalescedTree(ks, sb.data(), sc.data(), (int)sb.size(), esz, stream);
+        if (!sb.empty() && !lb.empty())
+            AllreduceCoalesced(lb.data(), lc.data(), (int)lb.size(), dtype, op, stream, algo);
+        if (!sb.empty()) return;
+    }
     std::vector<uint64_t> cnt((size_t)nbuf);
     for (int b = 0; b < nbuf; ++b) cnt[(size_t)b] = counts[b];
     // The unit-table mesh needs no staging memory, so its groups are large
@@ -699,6 +765,24 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
         return;
     }
     CoalescedStaged(ks, bufs, counts, nbuf, dtype, op, esz, algo, stream);
+}
+
+// tree-order buffers: pack into the staging image, one tree launch over the
+// packed bytes (padding between segments is folded too, never unpacked), unpack
+void Communicator::CoalescedTree(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, size_t esz,
+                                 hipStream_t stream) {
+    if (nbuf == 1) {
+        LaunchTree(ks, static_cast<char*>(bufs[0]), (uint64_t)counts[0] * esz, stream);
+        return;
+    }
+    uint64_t need = (uint64_t)RDC_SLOT_ALIGN * (uint64_t)n_;
+    for (int b = 0; b < nbuf; ++b) need += (uint64_t)n_ * 16 + ((uint64_t)counts[b] * esz + 15) / 16 * 16;
+    char* img = Image(need, stream);
+    const PackEntry& e = PackTable(bufs, counts, nbuf, esz, stream);
+    const int grid = std::max(1, std::min(e.nunits, 2 * num_cus_));
+    hip_check(launch_pack(e.dtable, e.nunits, img, 0, grid, stream), "launch pack");
+    LaunchTree(ks, img, e.total, stream);
+    hip_check(launch_pack(e.dtable, e.nunits, img, 1, grid, stream), "launch unpack");
 }
 
 // pack -> schedule on the staging image -> unpack, in groups of fuse_bytes

@@ -154,6 +154,9 @@ private:
     static constexpr size_t kPackCacheMax = 64;
     const PackEntry& PackTable(void* const* bufs, const size_t* counts, int nbuf, size_t esz, hipStream_t stream);
     char* Image(uint64_t bytes, hipStream_t stream);
+    void LaunchTree(const KernelSet& ks, char* buf, uint64_t total, hipStream_t stream);
+    void CoalescedTree(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, size_t esz,
+                       hipStream_t stream);
     void CoalescedStaged(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, int dtype, int op,
                          size_t esz, int algo, hipStream_t stream);
 
@@ -174,6 +177,7 @@ private:
     uint64_t* trace_ = nullptr;     // TraceNext
     size_t trace_words_ = 0;
     uint64_t last_launch_[6] = {};
+    int tree_len_ = 0, tree_dst_[RDC_MAX_RANKS] = {}, tree_src_[RDC_MAX_RANKS] = {};  // PlanTreeProgram(n)
     size_t slot_bytes_ = 0, region_bytes_ = 0, flag_bytes_ = 0;
     uint32_t max_tiles_ = 0;
     uint32_t seq_ = 0;

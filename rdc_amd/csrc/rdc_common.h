@@ -27,12 +27,16 @@ enum {
     RDC_ALGO_AUTO = 0,
     RDC_ALGO_RING = 1,  // the reference's ring: n-1 reduce-scatter + n-1 allgather steps
     RDC_ALGO_MESH = 2,  // direct all-links exchange, same per-chunk accumulation order
-    RDC_ALGO_ONESHOT = 3  // small buffers: every rank pushes all of it, every rank folds (one hand-off)
+    RDC_ALGO_ONESHOT = 3,  // small buffers: every rank pushes all of it, every rank folds (one hand-off)
+    RDC_ALGO_TREE = 4      // the reference's tree ORDER (TryAllreduceTree, buffers <= rdc_reduce_ring_mincount),
+                           // moved like the one-shot: every rank folds all n inputs in the tree's order
 };
 
 // launch kinds (recorded on the device: the next launch reads the previous kind)
+// (tree launches use the one-shot's slot protocol and record RDC_KIND_ONESHOT;
+// RDC_KIND_TREE only names the kernel in occupancy queries)
 enum { RDC_KIND_NONE = 0, RDC_KIND_MESH = 1, RDC_KIND_RING = 2, RDC_KIND_BCAST = 3, RDC_KIND_ALLGATHER = 4,
-       RDC_KIND_ONESHOT = 5 };
+       RDC_KIND_ONESHOT = 5, RDC_KIND_TREE = 6 };
 
 #define RDC_MAX_RANKS 16
 #define RDC_SLOT_ALIGN 256         // scratch images keep the user buffer's address mod 256
@@ -94,6 +98,9 @@ struct CollArgs {
     int bcast_split;                     // broadcast: root -> forwarder per tile -> other ranks (n >= 3)
     uint64_t half_bytes;                 // one-shot: offset of the slot half used by odd seq
     uint64_t total_bytes;                // one-shot: whole buffer bytes
+    int tree_len;                        // tree: fold program acc[tree_dst[i]] = OP(acc[tree_dst[i]],
+    int8_t tree_dst[RDC_MAX_RANKS];      //   acc[tree_src[i]]), i < tree_len, over the n inputs indexed
+    int8_t tree_src[RDC_MAX_RANKS];      //   by rank; the result is acc[0] (rdc_plan.h PlanTreeProgram)
     const void* units;                   // coalesced mesh: device PackUnit table (off/len are packed
     int nunits;                          //   offsets; user bytes reached through the units), else null
     uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up

@@ -264,6 +264,17 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
         AllreduceSmall(c, h, count, S, dtype, op, comm_stream);
         return;
     }
+    if (S <= c->config().ring_mincount) {
+        // the tree's order (rdc_reduce_ring_mincount) is per element, but the
+        // pipeline below cuts the buffer by Split chunk for the ring: stage
+        // the whole buffer instead (raised thresholds are for small buffers)
+        Reserve(0, S, 0);
+        hip_check(hipMemcpyAsync(dev_, h, S, hipMemcpyHostToDevice, comm_stream), "H2D");
+        c->Allreduce(dev_, count, dtype, op, comm_stream);
+        hip_check(hipMemcpyAsync(h, dev_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
+        c->Check(comm_stream);
+        return;
+    }
 
     int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
     SplitRanges((int64_t)count, n, cb, ce);

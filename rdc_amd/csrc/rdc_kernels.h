@@ -12,8 +12,9 @@ struct KernelSet {
     hipError_t (*mesh)(const CollArgs& a, int grid, hipStream_t s);
     hipError_t (*ring)(const CollArgs& a, int grid, hipStream_t s);
     hipError_t (*oneshot)(const CollArgs& a, int grid, hipStream_t s);
+    hipError_t (*tree)(const CollArgs& a, int grid, hipStream_t s);
     // resident blocks per CU of the kernel a launch of `kind` (RDC_KIND_MESH /
-    // RING / ONESHOT) on n ranks uses (hipOccupancyMaxActiveBlocksPerMultiprocessor,
+    // RING / ONESHOT / TREE) on n ranks uses (hipOccupancyMaxActiveBlocksPerMultiprocessor,
     // cached); the grid clamp of ResidentGrid (rdc_plan.h)
     int (*occupancy)(int kind, int n);
 };

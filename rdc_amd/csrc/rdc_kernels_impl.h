@@ -476,7 +476,75 @@ __device__ void oneshot_fold_range(const CollArgs& a, int c, const char* slots, 
     }
 }
 
+// ---- tree order (rdc_reduce_ring_mincount, TryAllreduceTree): every element
+// of [lo, hi) folded over the n ranks' values with the host-planned program
+// acc[d] = OP(acc[d], acc[s]) (rdc_plan.h PlanTreeProgram), result acc[0] —
+// the reference root's bits, which its broadcast hands to every rank.  The
+// program indices are uniform (kernel arguments), so pick / put compile to
+// selects over registers instead of a private-memory array.
+template <int NMAX, typename V>
+__device__ __forceinline__ V tree_pick(const V (&v)[NMAX], int i) {
+    V x = v[0];
+#pragma unroll
+    for (int k = 1; k < NMAX; ++k)
+        if (k == i) x = v[k];
+    return x;
+}
+template <int NMAX, typename V>
+__device__ __forceinline__ void tree_put(V (&v)[NMAX], int i, V x) {
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k)
+        if (k == i) v[k] = x;
+}
+
 template <int OP, typename T, int NMAX>
+__device__ void tree_fold_range(const CollArgs& a, const char* slots, uint64_t lo, uint64_t hi) {
+    const int n = a.n, r = a.rank;
+    char* own = a.user;
+    const unsigned tid = threadIdx.x;
+    auto src = [&](int q) -> const char* { return q == r ? (const char*)own : slots + (uint64_t)q * a.slot_bytes; };
+    auto fold_elem = [&](uint64_t x) {
+        T v[NMAX];
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k)
+            if (k < n) v[k] = *reinterpret_cast<const T*>(src(k) + x);
+#pragma unroll
+        for (int i = 0; i < NMAX - 1; ++i)
+            if (i < a.tree_len) {
+                const int d = a.tree_dst[i], s = a.tree_src[i];
+                tree_put<NMAX, T>(v, d, OpF<OP>::apply(tree_pick<NMAX, T>(v, d), tree_pick<NMAX, T>(v, s)));
+            }
+        *reinterpret_cast<T*>(own + x) = v[0];
+    };
+    if ((((uintptr_t)own ^ (uintptr_t)slots) & 15) != 0) {  // this rank's buffer is not 16-B aligned
+        for (uint64_t x = lo + (uint64_t)tid * sizeof(T); x < hi; x += (uint64_t)kBlock * sizeof(T)) fold_elem(x);
+        return;
+    }
+    uint64_t vlo = (lo + 15) & ~(uint64_t)15;
+    if (vlo > hi) vlo = hi;
+    const uint64_t vhi = vlo + ((hi - vlo) & ~(uint64_t)15);
+    {
+        const uint64_t nh = (vlo - lo) / sizeof(T), nt = (hi - vhi) / sizeof(T);
+        if (tid < nh) fold_elem(lo + tid * sizeof(T));
+        else if (tid >= 64 && tid - 64 < nt) fold_elem(vhi + (tid - 64) * sizeof(T));
+    }
+    const uint64_t nvec = (vhi - vlo) >> 4;
+    for (uint64_t i = tid; i < nvec; i += kBlock) {
+        v4u v[NMAX];
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k)
+            if (k < n) v[k] = ld16_nt(src(k) + vlo + i * 16);
+#pragma unroll
+        for (int j = 0; j < NMAX - 1; ++j)
+            if (j < a.tree_len) {
+                const int d = a.tree_dst[j], s = a.tree_src[j];
+                tree_put<NMAX, v4u>(v, d, reduce16<OP, T>(tree_pick<NMAX, v4u>(v, d), tree_pick<NMAX, v4u>(v, s)));
+            }
+        st16(own + vlo + i * 16, v[0]);
+    }
+}
+
+template <int OP, typename T, int NMAX, bool TREE = false>
 __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
     const int n = a.n, r = a.rank;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
@@ -505,11 +573,15 @@ __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
         if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS)) return;
         const uint64_t lo = (uint64_t)t * a.tile_bytes;
         const uint64_t hi = lo + a.tile_bytes < total ? lo + a.tile_bytes : total;
-        for (int c = 0; c < n; ++c) {
-            if (a.len[c] == 0) continue;
-            const uint64_t clo = a.off[c] > lo ? a.off[c] : lo;
-            const uint64_t chi = a.off[c] + a.len[c] < hi ? a.off[c] + a.len[c] : hi;
-            if (clo < chi) oneshot_fold_range<OP, T, NMAX>(a, c, slots, clo, chi);
+        if (TREE) {
+            tree_fold_range<OP, T, NMAX>(a, slots, lo, hi);
+        } else {
+            for (int c = 0; c < n; ++c) {
+                if (a.len[c] == 0) continue;
+                const uint64_t clo = a.off[c] > lo ? a.off[c] : lo;
+                const uint64_t chi = a.off[c] + a.len[c] < hi ? a.off[c] + a.len[c] : hi;
+                if (clo < chi) oneshot_fold_range<OP, T, NMAX>(a, c, slots, clo, chi);
+            }
         }
         __syncthreads();
     }
@@ -644,6 +716,13 @@ __global__ __launch_bounds__(kBlock) void k_oneshot(CollArgs a) {
     launch_done(a, seq);
 }
 
+template <int OP, typename T, int NMAX>
+__global__ __launch_bounds__(kBlock) void k_tree(CollArgs a) {
+    const uint32_t seq = launch_seq(a);
+    oneshot_body<OP, T, NMAX, true>(a, seq);
+    launch_done(a, seq);
+}
+
 template <int OP, typename T>
 __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
     const uint64_t t0 = wall_clock64();
@@ -683,11 +762,21 @@ struct Kernels {
         hipLaunchKernelGGL((k_ring<OP, T>), dim3(grid), dim3(kBlock), 0, s, a);
         return hipGetLastError();
     }
+    static hipError_t tree(const CollArgs& a, int grid, hipStream_t s) {
+        if (a.n <= 8)
+            hipLaunchKernelGGL((k_tree<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_tree<OP, T, 16>), dim3(grid), dim3(kBlock), 0, s, a);
+        return hipGetLastError();
+    }
     static int occupancy(int kind, int n) {
-        // [mesh 8, mesh 16, oneshot 8, oneshot 16, ring]; 0 = not queried yet
-        static int cache[5] = {0, 0, 0, 0, 0};
+        // [mesh 8, mesh 16, oneshot 8, oneshot 16, ring, tree 8, tree 16]; 0 = not queried yet
+        static int cache[7] = {0, 0, 0, 0, 0, 0, 0};
         const int wide = n > 8 ? 1 : 0;
-        const int slot = kind == RDC_KIND_RING ? 4 : (kind == RDC_KIND_ONESHOT ? 2 : 0) + wide;
+        const int slot = kind == RDC_KIND_RING      ? 4
+                         : kind == RDC_KIND_TREE    ? 5 + wide
+                         : kind == RDC_KIND_ONESHOT ? 2 + wide
+                                                    : wide;
         if (cache[slot] > 0) return cache[slot];
         int b = 0;
         hipError_t e = hipSuccess;
@@ -696,6 +785,8 @@ struct Kernels {
             case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_mesh<OP, T, 16>, kBlock, 0); break;
             case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_oneshot<OP, T, 8>, kBlock, 0); break;
             case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_oneshot<OP, T, 16>, kBlock, 0); break;
+            case 5: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_tree<OP, T, 8>, kBlock, 0); break;
+            case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_tree<OP, T, 16>, kBlock, 0); break;
             default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_ring<OP, T>, kBlock, 0); break;
         }
         if (e != hipSuccess || b <= 0) {
@@ -713,6 +804,7 @@ struct Kernels {
     ks->mesh = &Kernels<OP, T>::mesh;     \
     ks->ring = &Kernels<OP, T>::ring;     \
     ks->oneshot = &Kernels<OP, T>::oneshot; \
+    ks->tree = &Kernels<OP, T>::tree;       \
     ks->occupancy = &Kernels<OP, T>::occupancy; \
     return true;
 

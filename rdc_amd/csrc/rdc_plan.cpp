@@ -4,6 +4,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
+#include <queue>
+#include <unordered_map>
+#include <unordered_set>
 
 namespace rdc_amd {
 
@@ -249,6 +253,91 @@ CoalescedPlan PlanCoalesced(int n, const uint64_t* counts, int nbuf, size_t esz,
     }
     P.total = end;
     return P;
+}
+
+// The reference derives the tree in three hash-container passes whose
+// iteration order decides who folds first (topo.cc:20-115, communicator_base.cc:
+// 136-149, graph.h:70-83, communicator_collective.cc:16-27).  The same
+// container operations are replayed here on libstdc++'s unordered_map /
+// unordered_set (the toolchain's standard library, as the reference's), so
+// each rank's children come out in the reference's order; the CPU tests
+// compare every n = 1..16 with the oracle's independent restatement
+// (oracle/tree_order.cc).
+int PlanTreeProgram(int n, int* dst, int* src) {
+    if (n < 2) return 0;
+    typedef std::unordered_map<int, std::vector<int>> NbMap;
+    // heap tree: parent (r+1)/2-1, children 2r+1, 2r+2 (topo.cc:3-30)
+    NbMap heap;
+    std::unordered_map<int, int> up;
+    for (int r = 0; r < n; ++r) {
+        std::vector<int>& v = heap[r];
+        if (r > 0) v.push_back((r + 1) / 2 - 1);
+        for (int c = 2 * r + 1; c <= 2 * r + 2; ++c)
+            if (c < n) v.push_back(c);
+        up[r] = (r + 1) / 2 - 1;
+    }
+    // ring positions: DFS order with the last child's segment reversed (topo.cc:32-94)
+    std::function<std::vector<int>(int)> walk = [&](int r) {
+        std::vector<int> seq(1, r), kids;
+        for (int x : heap[r])
+            if (x != up[r]) kids.push_back(x);
+        for (size_t i = 0; i < kids.size(); ++i) {
+            std::vector<int> part = walk(kids[i]);
+            if (i + 1 == kids.size()) std::reverse(part.begin(), part.end());
+            seq.insert(seq.end(), part.begin(), part.end());
+        }
+        return seq;
+    };
+    const std::vector<int> order = walk(0);
+    std::vector<int> pos((size_t)n);
+    for (int i = 0; i < n; ++i) pos[(size_t)order[(size_t)i]] = i;
+    // relabelled neighbour lists, built by walking the heap map (topo.cc:95-106)
+    NbMap rel;
+    for (const auto& kv : NbMap(heap))
+        for (int x : kv.second) rel[pos[(size_t)kv.first]].push_back(pos[(size_t)x]);
+    // adjacency sets from the edge list of a copy (communicator_base.cc:136-149),
+    // with graph.h:79-80's insertion of `to` into its own set
+    std::unordered_map<int, std::unordered_set<int>> adj;
+    for (const auto& kv : NbMap(rel))
+        for (int x : kv.second) {
+            std::unordered_set<int>& a = adj[kv.first];
+            if (!a.count(x)) a.emplace(x);
+            std::unordered_set<int>& b = adj[x];
+            if (!b.count(kv.first)) b.emplace(x);
+        }
+    // levels from rank 0 (graph.h:45-67); children in the order a fresh
+    // unordered_set returns them (communicator_collective.cc:19-27)
+    std::vector<int> level((size_t)n, -1);
+    std::queue<int> q;
+    q.push(0);
+    level[0] = 0;
+    while (!q.empty()) {
+        const int v = q.front();
+        q.pop();
+        for (int w : adj[v])
+            if (level[(size_t)w] < 0) {
+                level[(size_t)w] = level[(size_t)v] + 1;
+                q.push(w);
+            }
+    }
+    std::vector<std::vector<int>> kids((size_t)n);
+    for (int r = 0; r < n; ++r) {
+        std::unordered_set<int> from;
+        for (int x : std::unordered_set<int>(adj[r]))
+            if (level[(size_t)x] == level[(size_t)r] + 1) from.insert(x);
+        kids[(size_t)r].assign(from.begin(), from.end());
+    }
+    int k = 0;
+    std::function<void(int)> emit = [&](int v) {  // post-order: a subtree is complete before it is folded
+        for (int c : kids[(size_t)v]) {
+            emit(c);
+            dst[k] = v;
+            src[k] = c;
+            ++k;
+        }
+    };
+    emit(0);
+    return k;
 }
 
 std::vector<int> GroupCoalesced(const uint64_t* counts, int nbuf, size_t esz, uint64_t fuse_bytes) {

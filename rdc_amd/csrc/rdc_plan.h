@@ -88,6 +88,19 @@ std::vector<Piece> PlanAllreduceRanges(int n, const uint64_t* off, const uint64_
 Piece PlanOneshotRanges(int n, const uint64_t* off, const uint64_t* len, uint64_t total, const Layout& L,
                         size_t cfg_tile, int max_blocks);
 
+// ------------------------------------------------------ tree allreduce ---
+// rdc_reduce_ring_mincount (communicator_manager.cc:46): TryAllreduce takes
+// TryAllreduceTree for buffers of at most that many bytes
+// (communicator_collective.cc:6-13): TryReduceTree to rank 0 over the tree of
+// GetLinkMap (src/utils/topo.cc:80-115) as the communicator's UndirectedGraph
+// holds it (communicator_base.cc:113-150, include/utils/graph.h:45-83), then
+// TryBroadcast from rank 0.  Rank r folds its children's subtree results
+// into its own buffer one by one, own = OP(own, child), in the iteration
+// order of the unordered_set the reference collects them in (:14-33).
+// The fold as a post-order program over the n inputs: acc[dst[i]] =
+// OP(acc[dst[i]], acc[src[i]]) for i < n-1, result acc[0].  Returns n-1.
+int PlanTreeProgram(int n, int* dst, int* src);
+
 // ---------------------------------------------------- coalesced allreduce ---
 // Many buffers reduced as one launch sequence (BASELINE cfg5: 1024 x 1 MiB,
 // test/mallreduce.cc's back-to-back shape).  The ring order of an element

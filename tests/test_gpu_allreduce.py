@@ -88,6 +88,33 @@ def test_group3_all_types(group3, dtype, op, algo):
             assert same_bits(got[r], want, dtype), (dtype, op, algo, count, r)
 
 
+@pytest.mark.parametrize("dtype,op", VALID)
+def test_group3_tree_order_all_types(group3, dtype, op):
+    """algo 4: the reference's small-buffer TREE order (TryAllreduceTree,
+    communicator_collective.cc:14-78; rdc_reduce_ring_mincount) for every
+    (dtype, op), misaligned buffers, vs the oracle's restated tree
+    (oracle/tree_order.cc).  fp32 tree parity is pinned by the restatement
+    only (the reference's own .cc could not be compiled here)."""
+    rng = np.random.default_rng(91 + dtype * 8 + op)
+    for count in (1, 2, 5, 1001, 4099, 70001):
+        inputs = [rand_input(rng, count, dtype) for _ in range(3)]
+        want = O.expected_tree(inputs, dtype, op)
+        got = run_group(group3, inputs, dtype, op, 4, pads=[1, 0, 3])
+        for r in range(3):
+            assert same_bits(got[r], want, dtype), (dtype, op, count, r)
+
+
+def test_group_tree_multi_piece(group2):
+    """A tree-order buffer larger than half a one-shot slot goes in pieces."""
+    rng = np.random.default_rng(92)
+    count = (5 << 20) // 4 + 3   # 5 MiB fp32 > half of a 8 MiB slot
+    inputs = [rng.standard_normal(count).astype(np.float32) for _ in range(2)]
+    got = run_group(group2, inputs, O.DT_FLOAT32, O.OP_SUM, 4, pads=[0, 1])
+    want = O.expected_tree(inputs, O.DT_FLOAT32, O.OP_SUM)
+    for r in range(2):
+        assert same_bits(got[r], want, O.DT_FLOAT32)
+
+
 @pytest.mark.parametrize("algo", [1, 2])
 def test_group_multi_piece(group2, algo):
     """Buffers larger than the scratch go through several launches (pieces)."""
@@ -263,12 +290,21 @@ def expected_for(case, world):
             O.reducer(O.fill(case["count"], O.DT_INT32, case.get("seed", 0x5EED0000) + k, root), acc, O.DT_INT32,
                       O.OP_SUM)
         return [acc] * world
+    esz = np.dtype(O.NP_DTYPE[dt]).itemsize
+    mincount = case.get("mincount", 1)  # rdc_reduce_ring_mincount of the run (bytes)
+
+    def reduce_all(xs, op):  # TryAllreduce: the tree's order up to mincount bytes, the ring's above
+        if xs[0].size * esz <= mincount or case.get("algo") == 4:
+            O.allreduce_tree(xs, dt, op)
+        else:
+            O.allreduce_ring(xs, dt, op)
+
     if case.get("kind") == "coalesced":
         per = []
         for b, k in enumerate(case["counts"]):
             xs = [O.fill(k, dt, case.get("seed", 0x5EED0000) + b, r) for r in range(world)]
             for _ in range(case.get("reps", 1)):
-                O.allreduce_ring(xs, dt, case["op"])
+                reduce_all(xs, case["op"])
             per.append(xs)
         return [np.concatenate([per[b][r] for b in range(len(per))]) if per else np.zeros(0, np.uint8)
                 for r in range(world)]
@@ -278,7 +314,7 @@ def expected_for(case, world):
         return [inputs[case["root"]]] * world
     bufs = [x.copy() for x in inputs]
     for _ in range(case.get("reps", 1)):
-        O.allreduce_ring(bufs, dt, case["op"])
+        reduce_all(bufs, case["op"])
     return bufs
 
 
@@ -323,6 +359,48 @@ def test_mp_allreduce(world):
             got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
             exp = np.frombuffer(want[r].tobytes(), dtype=np.uint8)
             assert got.tobytes() == exp.tobytes(), (i, c, r)
+
+
+@pytest.mark.parametrize("world", [3, 5, 8])
+def test_mp_tree_path_ring_mincount(world):
+    """rdc_reduce_ring_mincount=64K (communicator_manager.cc:140-162 key):
+    buffers of <= 64 KiB take the reference's tree order, larger ones the
+    ring's — device, host (RdcAllreduce) and coalesced lists mixing both,
+    against the oracle (tree: oracle/tree_order.cc).  Integer cases are
+    test/allreduce.cc-style known answers (order-free); every rank holds the
+    root's bits (the reference's broadcast forwards stale data at n >= 4,
+    SURVEY finding 6 — not reproduced)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    M = 64 << 10
+    cases = [
+        {"count": 1001, "dtype": 6, "op": 2, "mincount": M},
+        {"count": 16384, "dtype": 6, "op": 2, "mincount": M, "pad_per_rank": 4},      # exactly 64 KiB: tree
+        {"count": 16385, "dtype": 6, "op": 2, "mincount": M},                         # one more: ring
+        {"count": 4099, "dtype": 2, "op": 2, "mincount": M},
+        {"count": 3001, "dtype": 10, "op": 0, "mincount": M, "reps": 3},
+        {"count": 777, "dtype": 7, "op": 1, "mincount": M, "algo": 2},                # algo does not change the order
+        {"count": 1, "dtype": 0, "op": 2, "mincount": M},
+        {"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce", "mincount": M},
+        {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1001, 70000, 5, 16384, 0, 20000],
+         "mincount": M, "reps": 2},
+        {"count": 0, "dtype": 2, "op": 0, "kind": "coalesced", "counts": [3, 1000, 77], "host": True,
+         "mincount": M},
+        {"count": 30011, "dtype": 6, "op": 2, "kind": "algo_chain", "algos": [0, 4, 3, 2, 1, 4, 4, 0],
+         "mincount": M},
+    ]
+    tmp = run_mp(world, cases, env_extra={"rdc_reduce_ring_mincount": "64K"})
+    for i, c in enumerate(cases):
+        if c.get("kind") == "algo_chain":
+            bufs = [O.fill(c["count"], 6, 0x5EED0000, r) for r in range(world)]
+            for a in c["algos"]:
+                (O.allreduce_tree if a == 4 else O.allreduce_ring)(bufs, 6, 2)
+            want = bufs
+        else:
+            want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (world, i, c, r)
 
 
 def test_mp_full_size_cfg2():

@@ -202,3 +202,74 @@ def test_tcp_ring_port_matches_oracle(oracle, tmp_path, n, count, dtype, op):
     for r in range(n):
         got = open(os.path.join(str(tmp_path), "rank%d.bin" % r), "rb").read()
         assert got == bufs[r].tobytes(), (n, count, dtype, op, r)
+
+
+# ------------------------------------------------ tree (ring_mincount) path
+def test_tree_shapes_follow_get_link_map():
+    """The tree is GetLinkMap's heap tree relabelled to ring positions
+    (src/utils/topo.cc:3-115): parent/children consistent, rooted at 0, every
+    rank reached, depth = the heap depth."""
+    import math
+    from oracle import oracle as O
+    for n in range(1, 17):
+        kids, parent, depth = O.tree(n)
+        assert parent[0] == -1 and depth[0] == 0
+        seen = {0}
+        for r in range(n):
+            for c in kids[r]:
+                assert parent[c] == r and depth[c] == depth[r] + 1
+                seen.add(c)
+        assert seen == set(range(n))
+        assert max(depth) == (int(math.log2(n)) if n > 1 else 0)
+        prog = O.tree_program(n)
+        assert len(prog) == max(0, n - 1)
+        assert sorted(s for _, s in prog) == list(range(1, n))  # every rank folded exactly once
+
+
+def test_tree_program_matches_library_plan():
+    """The product's own tree planner (rdc_plan.cpp PlanTreeProgram, exported
+    as RdcPlanTree) gives the oracle's fold program for every n = 1..16."""
+    import ctypes
+    from oracle import oracle as O
+    from rdc_amd._lib import _LIB
+    for n in range(1, 17):
+        d, s = (ctypes.c_int * 16)(), (ctypes.c_int * 16)()
+        k = _LIB.RdcPlanTree(n, d, s)
+        assert [(d[i], s[i]) for i in range(k)] == O.tree_program(n), n
+
+
+def test_tree_fold_order_known_cases():
+    """Spot values of the fold (restated libstdc++ unordered_set order): the
+    n = 8 root folds subtree 1 then subtree 7; rank 7 folds 6 then 5."""
+    from oracle import oracle as O
+    kids, _, _ = O.tree(8)
+    assert kids[0] == [1, 7] and kids[7] == [6, 5] and kids[1] == [2, 4] and kids[2] == [3]
+    assert O.tree_program(3) == [(0, 1), (0, 2)]
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 8, 13, 16])
+def test_tree_allreduce_integer_known_answers(n):
+    """test/allreduce.cc's known answers hold on the tree path too (integer
+    Max/Sum are order-free): a[i] = rank + N + i."""
+    from oracle import oracle as O
+    N = 37
+    for op, want in ((O.OP_MAX, lambda i: (n - 1) + N + i), (O.OP_SUM, lambda i: sum(r + N + i for r in range(n)))):
+        bufs = [np.arange(r + N, r + N + N, dtype=np.int32) for r in range(n)]
+        O.allreduce_tree(bufs, O.DT_INT32, op)
+        for b in bufs:
+            assert b.tolist() == [want(i) for i in range(N)]
+
+
+def test_tree_order_differs_from_ring_for_floats():
+    """fp32 Sum: the tree's association differs from the ring's (so the path
+    must be taken by size, like the reference), and from a rank-order sum."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(8)
+    xs = [rng.standard_normal(4001).astype(np.float32) for _ in range(8)]
+    t = O.expected_tree(xs, O.DT_FLOAT32, O.OP_SUM)
+    r = O.expected_allreduce(xs, O.DT_FLOAT32, O.OP_SUM)
+    assert (t != r).sum() > 0
+    # manual evaluation of the n = 8 tree: ((x0 + ((x1 + (x2 + x3)) + x4)) + ((x7 + x6) + x5))
+    a1 = (xs[1] + (xs[2] + xs[3])) + xs[4]
+    a7 = (xs[7] + xs[6]) + xs[5]
+    assert t.tobytes() == ((xs[0] + a1) + a7).tobytes()
