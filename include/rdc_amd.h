@@ -102,6 +102,14 @@ int RdcAllreduceCoalescedOn(void* comm, void** bufs, const size_t* counts, int n
  * NewCommunicator is collective over all ranks. */
 int RdcNewCommunicator(void** out, const char* name);
 int RdcGetCommunicator(void** out, const char* name);
+/* rdc::CreateGroup / ICommunicator::CreateGroup (include/api.h:124-125,
+ * include/comm/communicator.h:133-134; declared, never defined in the
+ * reference): a communicator over `ranks` (ranks of `parent`, NULL = "main";
+ * group rank i = ranks[i]) named `name` ("" = "group<k>").  Collective over
+ * every rank of the parent, all passing the same list; *out = NULL on ranks
+ * not in it.  Members rendezvous through node-local shared memory and get
+ * their own scratch; destroy with RdcCommDestroy (collective over members). */
+int RdcCreateGroup(void** out, void* parent, const int* ranks, int nranks, const char* name);
 
 /* Point-to-point (ICommunicator::ISend/IRecv, include/comm/communicator.h:
  * 56-80; rdc/comm.py:46-80 binds RdcISend / RdcIRecv / RdcWorkCompletion*).
@@ -159,6 +167,10 @@ int RdcCommBroadcast(void* comm, void* dev_buf, size_t bytes, int root, void* st
 int RdcCommAllgather(void* comm, void** dev_bufs, const size_t* sizes, void* stream);
 /* synchronise `stream` and report any device-side collective failure */
 int RdcCommCheck(void* comm, void* stream);
+/* A communicator's parameter: "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES",
+ * "RDC_TILE_BYTES", "RDC_NBLOCKS", "RDC_ONESHOT_BYTES", "slot_bytes",
+ * "ranks_per_gpu" (most ranks of it sharing one physical GPU). */
+int RdcCommGetParam(void* comm, const char* key, uint64_t* value);
 int RdcCommRank(void* comm);
 int RdcCommSize(void* comm);
 int RdcCommDevice(void* comm);
@@ -205,6 +217,9 @@ int RdcCommDestroy(void* comm);
 /* op::Reducer<OP,DType>(src, dst, count) (include/core/mpi.h:113-120) on
  * device memory: dst[i] = OP::Reduce(dst[i], src[i]).  Stream-ordered. */
 int RdcReduce(void* dst, const void* src, size_t count, int dtype, int op, void* stream);
+/* Synchronous copy between any two of host / device memory (the C++ header's
+ * custom-reducer path stages device buffers with it). */
+int RdcMemcpy(void* dst, const void* src, size_t bytes);
 /* Synthetic inputs: u = splitmix64(seed ^ (rank<<40) ^ i) mapped per dtype
  * (identical to the CPU oracle's generator).  Stream-ordered. */
 int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, void* stream);

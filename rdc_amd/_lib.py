@@ -51,6 +51,10 @@ def _load():
         "RdcBroadcastOn": (i, [vp, vp, sz, i]),
         "RdcNewCommunicator": (i, [pvp, ctypes.c_char_p]),
         "RdcGetCommunicator": (i, [pvp, ctypes.c_char_p]),
+        "RdcCreateGroup": (i, [pvp, vp, ctypes.POINTER(ctypes.c_int), i, ctypes.c_char_p]),
+        "RdcCommGetParam": (i, [vp, ctypes.c_char_p, ctypes.POINTER(u64)]),
+        "RdcPlanTree": (i, [i, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+        "RdcPlanResidentGrid": (i, [i, i, i, i]),
         "RdcCommAllreduce": (i, [vp, vp, sz, i, i, vp]),
         "RdcCommAllreduceEx": (i, [vp, vp, sz, i, i, i, vp]),
         "RdcCommBroadcast": (i, [vp, vp, sz, i, vp]),
@@ -67,6 +71,7 @@ def _load():
         "RdcCommDestroy": (i, [vp]),
         "RdcReduce": (i, [vp, vp, sz, i, i, vp]),
         "RdcFill": (i, [vp, sz, i, u64, i, vp]),
+        "RdcMemcpy": (i, [vp, vp, sz]),
         "RdcPlanLayout": (i, [i, sz, ctypes.POINTER(u64)]),
         "RdcPlanAllreduce": (i, [i, sz, i, sz, i, sz, i, ctypes.POINTER(u64), i, ctypes.POINTER(ctypes.c_int)]),
         "RdcAllreduceCoalesced": (i, [pvp, ctypes.POINTER(sz), i, i, i]),

@@ -165,6 +165,13 @@ class Comm(object):
         self.irecv(buf, src_rank).wait()
         return buf
 
+    def get_param(self, key):
+        """A communicator parameter (RdcCommGetParam): "rdc_reduce_ring_mincount",
+        "RDC_SCRATCH_BYTES", "RDC_TILE_BYTES", "RDC_NBLOCKS", "slot_bytes", "ranks_per_gpu"."""
+        v = ctypes.c_uint64()
+        check_call(_LIB.RdcCommGetParam(self.handle, key.encode("utf-8"), ctypes.byref(v)))
+        return v.value
+
     def tune(self, mesh_s16=4, mesh_r16=8, max_blocks=0, tile_bytes=0):
         """Mesh role split (sixteenths of the grid), grid (0 = auto) and tile
         bytes (0 = auto) for the following collectives (RdcCommTune); every
@@ -204,6 +211,17 @@ def get_comm(name="main"):
         raise TypeError("name must be a string or bytearray")
     check_call(_LIB.RdcGetCommunicator(ctypes.byref(comm.handle), name))
     return comm
+
+
+def create_group(ranks, name="", parent=None):
+    """Sub-communicator over ``ranks`` (ranks of ``parent``, default "main";
+    group rank i = ranks[i]), rdc::CreateGroup (include/api.h:124-125).
+    Collective over every rank of the parent; returns None on non-members."""
+    comm = Comm(own_handle=True)
+    arr = (ctypes.c_int * len(ranks))(*[int(r) for r in ranks])
+    check_call(_LIB.RdcCreateGroup(ctypes.byref(comm.handle), parent.handle if parent is not None else None, arr,
+                                   len(ranks), name.encode("utf-8") if isinstance(name, str) else name))
+    return comm if comm.handle else None
 
 
 def init_group(devices, scratch_bytes=0):

@@ -3,6 +3,9 @@
 
 #include <arpa/inet.h>
 #include <errno.h>
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -13,6 +16,8 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <atomic>
 #include <stdexcept>
 #include <string>
 
@@ -95,6 +100,117 @@ void Bootstrap::broadcast(void* buf, size_t bytes, int root) {
 }
 
 void SoloBootstrap::allgather(const void* mine, size_t bytes, void* all) { memcpy(all, mine, bytes); }
+
+// ------------------------------------------------------------ ShmBootstrap --
+struct ShmBootstrap::Block {  // followed by size x kSlotBytes allgather slots
+    alignas(64) std::atomic<uint32_t> arrive;
+    alignas(64) std::atomic<uint32_t> gen;
+};
+
+namespace {
+size_t block_bytes(int size) { return sizeof(ShmBootstrap::Block) + (size_t)size * ShmBootstrap::kSlotBytes; }
+char* slot_of(ShmBootstrap::Block* b, int q) {
+    return reinterpret_cast<char*>(b) + sizeof(ShmBootstrap::Block) + (size_t)q * ShmBootstrap::kSlotBytes;
+}
+}  // namespace
+
+Bootstrap* ShmBootstrap::CreateGroup(Bootstrap* parent, const std::vector<int>& members, double timeout_s) {
+    const int np = parent->size(), pr = parent->rank();
+    const int n = (int)members.size();
+    // every parent rank must pass the same list
+    std::vector<int> sorted(members);
+    std::sort(sorted.begin(), sorted.end());
+    bool ok = n >= 1 && std::unique(sorted.begin(), sorted.end()) == sorted.end() && sorted.front() >= 0 &&
+              sorted.back() < np;
+    uint64_t h = 1469598103934665603ull ^ (uint64_t)n;
+    for (int m : members) h = (h ^ (uint64_t)(uint32_t)m) * 1099511628211ull;
+    std::vector<uint64_t> all((size_t)np);
+    parent->allgather(&h, sizeof(h), all.data());
+    for (uint64_t x : all) ok = ok && x == h;
+    if (!ok) throw std::invalid_argument("rdc: CreateGroup needs the same list of distinct ranks on every rank");
+    int me = -1;
+    for (int i = 0; i < n; ++i)
+        if (members[(size_t)i] == pr) me = i;
+    const int leader = members[0];
+    char name[64];
+    memset(name, 0, sizeof(name));
+    int fd = -1;
+    std::string err;
+    if (pr == leader) {
+        static std::atomic<int> counter{0};
+        snprintf(name, sizeof(name), "/rdc_grp_%d_%d", (int)getpid(), counter++);
+        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0 || ftruncate(fd, (off_t)block_bytes(n)) != 0) {
+            err = std::string("rdc: cannot create group shared memory ") + name + ": " + strerror(errno);
+            if (fd >= 0) {
+                ::close(fd);
+                shm_unlink(name);
+            }
+            fd = -1;
+            memset(name, 0, sizeof(name));
+        }
+    }
+    parent->broadcast(name, sizeof(name), leader);
+    if (!name[0]) throw std::runtime_error(err.empty() ? "rdc: the group's first rank could not create its segment" : err);
+    void* p = MAP_FAILED;
+    if (me >= 0) {
+        if (pr != leader) fd = shm_open(name, O_RDWR, 0600);
+        if (fd >= 0) {
+            p = mmap(nullptr, block_bytes(n), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            ::close(fd);
+        }
+    }
+    const char failed = (me >= 0 && p == MAP_FAILED) ? 1 : 0;
+    std::vector<char> fails((size_t)np);
+    parent->allgather(&failed, 1, fails.data());  // everyone mapped (or failed) before the name goes
+    if (pr == leader) shm_unlink(name);
+    for (char f : fails)
+        if (f) {
+            if (p != MAP_FAILED) munmap(p, block_bytes(n));
+            throw std::runtime_error("rdc: a group member could not map the group segment");
+        }
+    if (me < 0) return nullptr;
+    return new ShmBootstrap(me, n, static_cast<Block*>(p), timeout_s);
+}
+
+ShmBootstrap::~ShmBootstrap() {
+    if (blk_) munmap(blk_, block_bytes(size_));
+}
+
+void ShmBootstrap::wait_all() {
+    const uint32_t g = blk_->gen.load(std::memory_order_acquire);
+    if (blk_->arrive.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)size_) {
+        blk_->arrive.store(0, std::memory_order_relaxed);
+        blk_->gen.fetch_add(1, std::memory_order_release);
+        return;
+    }
+    const double deadline = now_s() + timeout_s_;
+    for (uint32_t spins = 0; blk_->gen.load(std::memory_order_acquire) == g; ++spins) {
+        if (spins < 4096) {
+            sched_yield();
+            continue;
+        }
+        usleep(50);
+        if ((spins & 255) == 0 && now_s() > deadline) {
+            errno = ETIMEDOUT;
+            fail("group barrier: a member did not arrive");
+        }
+    }
+}
+
+void ShmBootstrap::allgather(const void* mine, size_t bytes, void* all) {
+    char* out = static_cast<char*>(all);
+    const char* in = static_cast<const char*>(mine);
+    for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += kSlotBytes) {  // slot-sized rounds
+        const size_t len = std::min(kSlotBytes, bytes - off);
+        if (len) memcpy(slot_of(blk_, rank_), in + off, len);
+        wait_all();
+        for (int q = 0; q < size_; ++q)
+            if (len) memcpy(out + (size_t)q * bytes + off, slot_of(blk_, q), len);
+        wait_all();  // nobody overwrites a slot before every member read it
+        if (bytes == 0) break;
+    }
+}
 
 TcpBootstrap::TcpBootstrap(int rank, int size, const std::string& host, int port, double timeout_s)
     : rank_(rank), size_(size) {

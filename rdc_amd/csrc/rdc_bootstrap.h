@@ -42,6 +42,33 @@ private:
     std::vector<int> peer_fds_;    // root: socket per rank (index = rank)
 };
 
+// Members of a sub-communicator (CreateGroup, include/api.h:124-125): a
+// node-local rendezvous in POSIX shared memory (the xGMI path needs every
+// rank on one node anyway).  Created collectively over the parent's
+// bootstrap: the group's first rank creates the segment, the name travels
+// over the parent, then only members take part in barriers / allgathers.
+class ShmBootstrap : public Bootstrap {
+public:
+    // collective over `parent`: every parent rank calls it with the same
+    // `members` (parent ranks, group rank i = members[i]); non-members get null
+    static Bootstrap* CreateGroup(Bootstrap* parent, const std::vector<int>& members, double timeout_s);
+    ~ShmBootstrap() override;
+    int rank() const override { return rank_; }
+    int size() const override { return size_; }
+    void allgather(const void* mine, size_t bytes, void* all) override;
+
+    static constexpr size_t kSlotBytes = 4096;
+    struct Block;  // barrier words, then size x kSlotBytes allgather slots
+
+private:
+    ShmBootstrap(int rank, int size, Block* blk, double timeout_s) : rank_(rank), size_(size), blk_(blk),
+                                                                       timeout_s_(timeout_s) {}
+    void wait_all();  // generation barrier over the members
+    int rank_, size_;
+    Block* blk_;
+    double timeout_s_;
+};
+
 // One process owning every rank (single-process multi-GPU): trivially local.
 class SoloBootstrap : public Bootstrap {
 public:

@@ -46,6 +46,7 @@ struct Manager {
     size_t stage_bytes = 0;
     hipStream_t stream = nullptr;
     std::unique_ptr<HostPath> host;  // pipelined host-buffer allreduce (rdc_host.h)
+    int group_counter = 0;           // unnamed CreateGroup communicators: "group<k>" (same k on every rank)
 };
 
 Manager& M() {
@@ -288,6 +289,33 @@ int RdcNewCommunicator(void** out, const char* name) {
     return guard([&] {
         if (!out || !name) throw std::invalid_argument("rdc: null argument");
         *out = get_comm(m, name, true);
+    });
+}
+
+int RdcCreateGroup(void** out, void* parent, const int* ranks, int nranks, const char* name) {
+    Manager& m = M();
+    std::lock_guard<std::recursive_mutex> lk(m.mu);
+    return guard([&] {
+        if (!out || (nranks > 0 && !ranks) || nranks < 1) throw std::invalid_argument("rdc: bad CreateGroup arguments");
+        *out = nullptr;
+        require_init(m);
+        Communicator* p = parent ? as_comm(parent) : get_comm(m, "main", true);
+        const std::string nm = name && *name ? std::string(name) : "group" + std::to_string(m.group_counter);
+        ++m.group_counter;
+        if (!p->bootstrap()) throw std::runtime_error("rdc: CreateGroup needs a multi-process communicator");
+        // the name must be free on every member (checked collectively: a
+        // member that refused alone would leave the others waiting)
+        std::vector<int> rs(ranks, ranks + nranks);
+        char taken = 0;
+        for (int r : rs)
+            if (r == p->rank() && m.comms.count(nm)) taken = 1;
+        std::vector<char> all((size_t)p->size());
+        p->bootstrap()->allgather(&taken, 1, all.data());
+        for (char t : all)
+            if (t) throw std::invalid_argument("rdc: communicator '" + nm + "' already exists on a member");
+        Communicator* c = Communicator::CreateSubset(nm, p, rs, p->config());
+        if (c) m.comms[nm].reset(c);
+        *out = c;
     });
 }
 
@@ -556,6 +584,23 @@ int RdcCommLastLaunch(void* comm, uint64_t* out6) {
     });
 }
 
+int RdcCommGetParam(void* comm, const char* key, uint64_t* value) {
+    return guard([&] {
+        if (!key || !value) throw std::invalid_argument("rdc: null argument");
+        Communicator* c = as_comm(comm);
+        const CommConfig& g = c->config();
+        const std::string k(key);
+        if (k == "rdc_reduce_ring_mincount") *value = g.ring_mincount;
+        else if (k == "RDC_SCRATCH_BYTES") *value = g.scratch_bytes;
+        else if (k == "RDC_TILE_BYTES") *value = g.tile_bytes;
+        else if (k == "RDC_NBLOCKS") *value = (uint64_t)g.max_blocks;
+        else if (k == "RDC_ONESHOT_BYTES") *value = g.oneshot_push_max;
+        else if (k == "slot_bytes") *value = c->slot_bytes();
+        else if (k == "ranks_per_gpu") *value = (uint64_t)c->ranks_per_gpu();
+        else throw std::invalid_argument("rdc: unknown parameter " + k);
+    });
+}
+
 int RdcCommRank(void* comm) { return comm ? static_cast<Communicator*>(comm)->rank() : -1; }
 int RdcCommSize(void* comm) { return comm ? static_cast<Communicator*>(comm)->size() : -1; }
 int RdcCommDevice(void* comm) { return comm ? static_cast<Communicator*>(comm)->device() : -1; }
@@ -608,6 +653,18 @@ int RdcCommDestroy(void* comm) {
 
 int RdcReduce(void* dst, const void* src, size_t count, int dtype, int op, void* stream) {
     return guard([&] { DeviceReduce(dst, src, count, dtype, op, static_cast<hipStream_t>(stream)); });
+}
+
+int RdcMemcpy(void* dst, const void* src, size_t bytes) {
+    return guard([&] {
+        if (bytes == 0) return;
+        if (!dst || !src) throw std::invalid_argument("rdc: null argument");
+        if (!is_device_pointer(dst) && !is_device_pointer(src)) {
+            memcpy(dst, src, bytes);
+            return;
+        }
+        hcheck(hipMemcpy(dst, src, bytes, hipMemcpyDefault), "copy");
+    });
 }
 
 int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, void* stream) {

@@ -287,6 +287,17 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     return c.release();
 }
 
+Communicator* Communicator::CreateSubset(const std::string& name, Communicator* parent, const std::vector<int>& ranks,
+                                         const CommConfig& cfg) {
+    if (!parent->bs_)
+        throw std::runtime_error("rdc: CreateGroup needs a communicator of separate processes (not RdcCommInitAll)");
+    std::unique_ptr<Bootstrap> bs(ShmBootstrap::CreateGroup(parent->bs_, ranks, std::max(60.0, 4 * cfg.timeout_s)));
+    if (!bs) return nullptr;
+    Communicator* c = Create(name, bs.get(), parent->device_, cfg);
+    c->owned_bs_ = std::move(bs);
+    return c;
+}
+
 void Communicator::CreateGroup(const std::string& name, int n, const int* devices, const CommConfig& cfg,
                                std::vector<Communicator*>* out) {
     if (n < 1 || n > RDC_MAX_RANKS) throw std::runtime_error("rdc: bad group size");

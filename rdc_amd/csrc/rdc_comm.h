@@ -54,6 +54,11 @@ public:
     // Multi-process: one communicator per process, peers found through `bs`
     // (collective over bs).
     static Communicator* Create(const std::string& name, Bootstrap* bs, int device, const CommConfig& cfg);
+    // Sub-communicator over parent ranks `ranks` (group rank i = ranks[i];
+    // CreateGroup, include/api.h:124-125, include/comm/communicator.h:133-134).
+    // Collective over every rank of `parent`; non-members get null.
+    static Communicator* CreateSubset(const std::string& name, Communicator* parent, const std::vector<int>& ranks,
+                                      const CommConfig& cfg);
     // Single process driving n ranks (devices may repeat, e.g. n ranks on one GPU).
     static void CreateGroup(const std::string& name, int n, const int* devices, const CommConfig& cfg,
                             std::vector<Communicator*>* out);
@@ -118,6 +123,7 @@ public:
 
     int rank() const { return rank_; }
     int size() const { return n_; }
+    Bootstrap* bootstrap() const { return bs_; }
     int device() const { return device_; }
     const std::string& name() const { return name_; }
     int alloc_kind() const { return alloc_kind_; }  // 0 uncached, 1 fine-grained, 2 coarse
@@ -163,7 +169,8 @@ private:
     std::string name_;
     int rank_ = 0, n_ = 1, device_ = 0;
     CommConfig cfg_;
-    Bootstrap* bs_ = nullptr;       // not owned
+    Bootstrap* bs_ = nullptr;       // not owned (unless owned_bs_ holds it: group communicators)
+    std::unique_ptr<Bootstrap> owned_bs_;
     bool owns_peers_ipc_ = false;   // peers opened through IPC
     char* scratch_ = nullptr;       // RS region
     char* scratch_ag_ = nullptr;    // AG region
