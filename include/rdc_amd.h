@@ -169,7 +169,9 @@ int RdcCommAllgather(void* comm, void** dev_bufs, const size_t* sizes, void* str
 int RdcCommCheck(void* comm, void* stream);
 /* A communicator's parameter: "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES",
  * "RDC_TILE_BYTES", "RDC_NBLOCKS", "RDC_ONESHOT_BYTES", "slot_bytes",
- * "ranks_per_gpu" (most ranks of it sharing one physical GPU). */
+ * "ranks_per_gpu" (most ranks of it sharing one physical GPU), "shares_scratch"
+ * (1 when another communicator uses the same scratch channel: every named
+ * communicator over the same ranks shares one, RDC_SHARE_SCRATCH=0 disables). */
 int RdcCommGetParam(void* comm, const char* key, uint64_t* value);
 int RdcCommRank(void* comm);
 int RdcCommSize(void* comm);

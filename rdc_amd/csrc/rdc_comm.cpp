@@ -66,10 +66,7 @@ void dbg(const char* fmt, int rank, const char* what) {
 }
 
 struct PeerInfo {
-    hipIpcMemHandle_t scratch;
-    hipIpcMemHandle_t ag;
-    hipIpcMemHandle_t flags;
-    hipIpcMemHandle_t p2p;
+    uint64_t channel;   // id of the live channel this rank would share (0 = none)
     int32_t device;
     int32_t pid;
     int32_t alloc_kind;
@@ -82,6 +79,13 @@ struct PeerInfo {
     uint64_t plan[12];  // PlanKey: the parameters that shape a launch plan (must agree)
     char host[64];
     char pci[32];  // physical GPU (ranks may share one: tests, emulation)
+};
+
+struct Handles {  // round 2 of Create: IPC handles (scratch ones only for a new channel)
+    hipIpcMemHandle_t scratch;
+    hipIpcMemHandle_t ag;
+    hipIpcMemHandle_t flags;
+    hipIpcMemHandle_t p2p;
 };
 
 // Launch plans are made on each host; flags are matched by tile index while
@@ -150,28 +154,163 @@ std::shared_ptr<P2PCtl> map_p2p_ctl(Bootstrap* bs) {
 
 Communicator::Communicator() {}
 
-void Communicator::AllocLocal() {
+// ------------------------------------------------------------------ Channel --
+namespace {
+// live channels per bootstrap, and how many each bootstrap has created (the
+// id every rank gives its k-th channel on that bootstrap)
+std::mutex g_reg_mu;
+std::map<Bootstrap*, std::vector<std::weak_ptr<Channel>>> g_channels;
+std::map<Bootstrap*, uint64_t> g_channel_count;
+
+bool share_enabled() {
+    const char* v = getenv("RDC_SHARE_SCRATCH");
+    return !(v && *v && atoi(v) == 0);
+}
+}  // namespace
+
+Channel::~Channel() {
+    (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();
+    if (ipc && bs) {
+        try {
+            bs->barrier();  // nobody still pushes into my scratch
+        } catch (...) {
+        }
+        for (int p = 0; p < n; ++p)
+            if (p != rank) {
+                if (peer_scratch[p]) (void)hipIpcCloseMemHandle(peer_scratch[p]);
+                if (peer_ag[p]) (void)hipIpcCloseMemHandle(peer_ag[p]);
+                if (peer_flags[p]) (void)hipIpcCloseMemHandle(peer_flags[p]);
+            }
+        try {
+            bs->barrier();  // every importer closed its mapping
+        } catch (...) {
+        }
+    }
+    if (last_ev) (void)hipEventDestroy(last_ev);
+    if (scratch) (void)hipFree(scratch);
+    if (scratch_ag) (void)hipFree(scratch_ag);
+    if (flags) (void)hipFree(flags);
+    if (err) (void)hipFree(err);
+    if (err_host) (void)hipHostFree(err_host);
+}
+
+void Channel::Order(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (users > 1 && have_last && last_stream != s) hip_check(hipStreamWaitEvent(s, last_ev, 0), "order channel");
+}
+
+void Channel::Mark(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (users <= 1) return;
+    if (!last_ev) hip_check(hipEventCreateWithFlags(&last_ev, hipEventDisableTiming), "channel event");
+    hip_check(hipEventRecord(last_ev, s), "record channel event");
+    last_stream = s;
+    have_last = true;
+}
+
+namespace {
+// a collective call on a channel: ordered behind the channel's previous call
+// (when another communicator may have issued it on another stream), and
+// recorded as the latest one when it returns
+struct ChannelCall {
+    Channel* ch;
+    hipStream_t s;
+    ChannelCall(Channel* c, hipStream_t st) : ch(c), s(st) {
+        if (ch) ch->Order(s);
+    }
+    ~ChannelCall() {
+        try {
+            if (ch) ch->Mark(s);
+        } catch (...) {
+        }
+    }
+};
+}  // namespace
+
+bool Communicator::shares_channel() const {
+    if (!ch_) return false;
+    std::lock_guard<std::mutex> lk(ch_->mu);
+    return ch_->users > 1;
+}
+
+// this rank's scratch regions, flags and error words (uncached, IPC-exportable)
+void Communicator::AllocChannel() {
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    const Layout L = MakeLayout(n_, cfg_.scratch_bytes);
+    std::shared_ptr<Channel> ch = std::make_shared<Channel>();
+    ch->rank = rank_;
+    ch->n = n_;
+    ch->device = device_;
+    ch->bs = bs_;
+    ch->L = MakeLayout(n_, cfg_.scratch_bytes);
+    int k1 = 0, k2 = 0, k3 = 0;
+    ch->scratch = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k1));
+    ch->scratch_ag = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k3));
+    ch->flags = static_cast<uint32_t*>(alloc_shared(ch->L.flag_bytes, &k2));
+    ch->alloc_kind = std::max(std::max(k1, k2), k3);
+    // [0] error word, [16] block arrival counter, [32] completed-launch counter, [48] last kind
+    hip_check(hipMalloc(&ch->err, 256), "hipMalloc err");
+    hip_check(hipMemset(ch->flags, 0, ch->L.flag_bytes), "memset flags");
+    hip_check(hipMemset(ch->err, 0, 256), "memset err");
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&ch->err_host), 64, hipHostMallocCoherent), "hipHostMalloc err");
+    memset(ch->err_host, 0, 64);
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ch->err_host_dev), ch->err_host, 0),
+              "err device pointer");
+    hip_check(hipDeviceSynchronize(), "sync after alloc");
+    ch->peer_scratch[rank_] = ch->scratch;
+    ch->peer_ag[rank_] = ch->scratch_ag;
+    ch->peer_flags[rank_] = ch->flags;
+    if (bs_) {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        ch->id = ++g_channel_count[bs_];
+        g_channels[bs_].push_back(ch);
+    }
+    Attach(ch);
+}
+
+void Communicator::AllocP2P() {
+    int k4 = 0;
+    p2p_ = static_cast<char*>(alloc_shared((size_t)n_ * kP2PSlots * cfg_.p2p_slot_bytes, &k4));
+    alloc_kind_ = std::max(alloc_kind_, k4);
+    peer_p2p_[rank_] = p2p_;
+}
+
+// join a channel as one more user
+void Communicator::Attach(const std::shared_ptr<Channel>& ch) {
+    ch_ = ch;
+    {
+        std::lock_guard<std::mutex> lk(ch->mu);
+        ++ch->users;
+    }
+    Alias();
+}
+
+// the channel's resources under this communicator's (non-owning) names
+void Communicator::Alias() {
+    Channel* ch = ch_.get();
+    const Layout& L = ch->L;
     slot_bytes_ = L.slot_bytes;
     region_bytes_ = L.region_bytes;
     max_tiles_ = L.max_tiles;
     flag_bytes_ = L.flag_bytes;
-    int k1 = 0, k2 = 0, k3 = 0;
-    scratch_ = static_cast<char*>(alloc_shared(region_bytes_, &k1));
-    scratch_ag_ = static_cast<char*>(alloc_shared(region_bytes_, &k3));
-    flags_ = static_cast<uint32_t*>(alloc_shared(flag_bytes_, &k2));
-    int k4 = 0;
-    p2p_ = static_cast<char*>(alloc_shared((size_t)n_ * kP2PSlots * cfg_.p2p_slot_bytes, &k4));
-    alloc_kind_ = std::max(std::max(k1, k2), std::max(k3, k4));
-    // [0] error word, [16] block arrival counter, [32] completed-launch counter
-    hip_check(hipMalloc(&err_, 256), "hipMalloc err");
-    hip_check(hipMemset(flags_, 0, flag_bytes_), "memset flags");
-    hip_check(hipMemset(err_, 0, 256), "memset err");
-    hip_check(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocCoherent), "hipHostMalloc err");
-    memset(err_host_, 0, 64);
-    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_host_dev_), err_host_, 0), "err device pointer");
-    hip_check(hipDeviceSynchronize(), "sync after alloc");
+    alloc_kind_ = ch->alloc_kind;
+    scratch_ = ch->scratch;
+    scratch_ag_ = ch->scratch_ag;
+    flags_ = ch->flags;
+    err_ = ch->err;
+    err_host_ = ch->err_host;
+    err_host_dev_ = ch->err_host_dev;
+    for (int p = 0; p < n_; ++p) {
+        peer_scratch_[p] = ch->peer_scratch[p];
+        peer_ag_[p] = ch->peer_ag[p];
+        peer_flags_[p] = ch->peer_flags[p];
+    }
+}
+
+void Communicator::AllocLocal() {
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    AllocChannel();
+    AllocP2P();
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_) == hipSuccess && cus > 0)
         num_cus_ = cus;
@@ -179,10 +318,6 @@ void Communicator::AllocLocal() {
     if (hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, device_) != hipSuccess || wclk <= 0)
         wclk = 100000;
     wall_khz_ = wclk;
-    peer_scratch_[rank_] = scratch_;
-    peer_ag_[rank_] = scratch_ag_;
-    peer_flags_[rank_] = flags_;
-    peer_p2p_[rank_] = p2p_;
     tree_len_ = PlanTreeProgram(n_, tree_dst_, tree_src_);
 }
 
@@ -198,33 +333,50 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     // world size 1 moves no data (Communicator::Allreduce returns at once,
     // communicator_base.h:133-138): no device resources, no GPU needed
     if (c->n_ == 1) return c.release();
-    dbg("[rdc %d] %s\n", c->rank_, "alloc");
-    c->AllocLocal();
-    dbg("[rdc %d] %s\n", c->rank_, "alloc done");
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->num_cus_ = cus;
+    int wclk = 0;  // kHz
+    if (hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, device) != hipSuccess || wclk <= 0) wclk = 100000;
+    c->wall_khz_ = wclk;
+    c->tree_len_ = PlanTreeProgram(c->n_, c->tree_dst_, c->tree_src_);
+    const Layout L = MakeLayout(c->n_, cfg.scratch_bytes);
 
+    // round 1: the facts every rank must agree on, and the channel this rank
+    // could share (a live channel of this bootstrap with the same geometry)
     PeerInfo mine;
     memset(&mine, 0, sizeof(mine));
-    hip_check(hipIpcGetMemHandle(&mine.scratch, c->scratch_), "hipIpcGetMemHandle(scratch)");
-    hip_check(hipIpcGetMemHandle(&mine.ag, c->scratch_ag_), "hipIpcGetMemHandle(ag)");
-    hip_check(hipIpcGetMemHandle(&mine.flags, c->flags_), "hipIpcGetMemHandle(flags)");
-    hip_check(hipIpcGetMemHandle(&mine.p2p, c->p2p_), "hipIpcGetMemHandle(p2p)");
     mine.p2p_slot_bytes = cfg.p2p_slot_bytes;
     mine.device = device;
     mine.pid = (int32_t)getpid();
-    mine.alloc_kind = c->alloc_kind_;
-    mine.slot_bytes = c->slot_bytes_;
-    mine.max_tiles = c->max_tiles_;
+    mine.slot_bytes = L.slot_bytes;
+    mine.max_tiles = L.max_tiles;
     mine.num_cus = c->num_cus_;
     PlanKey(cfg, mine.plan);
+    std::shared_ptr<Channel> cand;
+    if (share_enabled()) {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        std::vector<std::weak_ptr<Channel>>& live = g_channels[bs];
+        live.erase(std::remove_if(live.begin(), live.end(),
+                                  [](const std::weak_ptr<Channel>& w) { return w.expired(); }),
+                   live.end());
+        for (auto& w : live) {
+            std::shared_ptr<Channel> ch = w.lock();
+            if (ch && ch->device == device && ch->n == c->n_ && ch->L.slot_bytes == L.slot_bytes &&
+                ch->L.max_tiles == L.max_tiles && ch->ipc)
+                cand = ch;
+        }
+    }
+    mine.channel = cand ? cand->id : 0;
     gethostname(mine.host, sizeof(mine.host) - 1);
     if (hipDeviceGetPCIBusId(mine.pci, sizeof(mine.pci) - 1, device) != hipSuccess) {
         (void)hipGetLastError();
         snprintf(mine.pci, sizeof(mine.pci), "device-%d", device);
     }
     std::vector<PeerInfo> all((size_t)c->n_);
-    dbg("[rdc %d] %s\n", c->rank_, "handles exported");
     bs->allgather(&mine, sizeof(mine), all.data());
-    dbg("[rdc %d] %s\n", c->rank_, "handles exchanged");
+    bool share = mine.channel != 0;
     for (int p = 0; p < c->n_; ++p) {
         const PeerInfo& q = all[(size_t)p];
         if (q.slot_bytes != mine.slot_bytes || q.max_tiles != mine.max_tiles ||
@@ -239,6 +391,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         if (strncmp(q.host, mine.host, sizeof(mine.host)) != 0)
             throw std::runtime_error("rdc: xGMI path needs every rank on one node (rank " + std::to_string(p) +
                                      " is on " + q.host + ")");
+        share = share && q.channel == mine.channel;  // every rank holds the same channel
     }
     // grids are planned from values every rank sees: the fewest CUs of any
     // rank's GPU and the most ranks sharing one physical GPU (ResidentGrid)
@@ -262,24 +415,47 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         }
     }
     (void)hipGetLastError();
+
+    // round 2: IPC handles of a new channel (unless shared) and of this
+    // communicator's point-to-point region
+    dbg("[rdc %d] %s\n", c->rank_, share ? "sharing the channel" : "alloc");
+    if (share) c->Attach(cand);
+    else c->AllocChannel();
+    c->AllocP2P();
+    Handles h;
+    memset(&h, 0, sizeof(h));
+    if (!share) {
+        hip_check(hipIpcGetMemHandle(&h.scratch, c->scratch_), "hipIpcGetMemHandle(scratch)");
+        hip_check(hipIpcGetMemHandle(&h.ag, c->scratch_ag_), "hipIpcGetMemHandle(ag)");
+        hip_check(hipIpcGetMemHandle(&h.flags, c->flags_), "hipIpcGetMemHandle(flags)");
+    }
+    hip_check(hipIpcGetMemHandle(&h.p2p, c->p2p_), "hipIpcGetMemHandle(p2p)");
+    std::vector<Handles> hs((size_t)c->n_);
+    bs->allgather(&h, sizeof(h), hs.data());
+    dbg("[rdc %d] %s\n", c->rank_, "handles exchanged");
+    Channel* ch = c->ch_.get();
     for (int p = 0; p < c->n_; ++p) {
         if (p == c->rank_) continue;
-        void* ps = nullptr;
-        void* pa = nullptr;
-        void* pf = nullptr;
-        hip_check(hipIpcOpenMemHandle(&ps, all[(size_t)p].scratch, hipIpcMemLazyEnablePeerAccess),
-                  "hipIpcOpenMemHandle(scratch)");
-        hip_check(hipIpcOpenMemHandle(&pa, all[(size_t)p].ag, hipIpcMemLazyEnablePeerAccess),
-                  "hipIpcOpenMemHandle(ag)");
-        c->peer_ag_[p] = static_cast<char*>(pa);
-        hip_check(hipIpcOpenMemHandle(&pf, all[(size_t)p].flags, hipIpcMemLazyEnablePeerAccess),
-                  "hipIpcOpenMemHandle(flags)");
-        c->peer_scratch_[p] = static_cast<char*>(ps);
-        c->peer_flags_[p] = static_cast<uint32_t*>(pf);
+        if (!share) {
+            void* ps = nullptr;
+            void* pa = nullptr;
+            void* pf = nullptr;
+            hip_check(hipIpcOpenMemHandle(&ps, hs[(size_t)p].scratch, hipIpcMemLazyEnablePeerAccess),
+                      "hipIpcOpenMemHandle(scratch)");
+            ch->peer_scratch[p] = static_cast<char*>(ps);
+            hip_check(hipIpcOpenMemHandle(&pa, hs[(size_t)p].ag, hipIpcMemLazyEnablePeerAccess),
+                      "hipIpcOpenMemHandle(ag)");
+            ch->peer_ag[p] = static_cast<char*>(pa);
+            hip_check(hipIpcOpenMemHandle(&pf, hs[(size_t)p].flags, hipIpcMemLazyEnablePeerAccess),
+                      "hipIpcOpenMemHandle(flags)");
+            ch->peer_flags[p] = static_cast<uint32_t*>(pf);
+            ch->ipc = true;
+        }
         void* pp = nullptr;
-        hip_check(hipIpcOpenMemHandle(&pp, all[(size_t)p].p2p, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(p2p)");
+        hip_check(hipIpcOpenMemHandle(&pp, hs[(size_t)p].p2p, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(p2p)");
         c->peer_p2p_[p] = static_cast<char*>(pp);
     }
+    if (!share) c->Alias();  // the aliases now include the peers' mappings
     c->p2p_ctl_ = map_p2p_ctl(bs);
     dbg("[rdc %d] %s\n", c->rank_, "peers mapped");
     c->owns_peers_ipc_ = true;
@@ -326,8 +502,7 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
     // Pinned coherent pages of its own, not a registered heap object: a
     // registration covers whole pages, and a heap object shares its first and
     // last page with unrelated allocations that the runtime may pin and unpin
-    // for its own copies (one run saw an illegal address right after such a
-    // copy; the control block has lived in dedicated pages since).
+    // for its own copies (see rdc_p2p.h, "Control block").
     void* mem = nullptr;
     if (hipHostMalloc(&mem, sizeof(P2PCtl), hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) !=
         hipSuccess) {
@@ -340,12 +515,13 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
         (void)hipHostFree(q);
     });
     for (int i = 0; i < n; ++i) {
-        cs[(size_t)i]->p2p_ctl_ = ctl;
+        Communicator* ci = cs[(size_t)i].get();
+        ci->p2p_ctl_ = ctl;
         for (int j = 0; j < n; ++j) {
-            cs[(size_t)i]->peer_scratch_[j] = cs[(size_t)j]->scratch_;
-            cs[(size_t)i]->peer_ag_[j] = cs[(size_t)j]->scratch_ag_;
-            cs[(size_t)i]->peer_flags_[j] = cs[(size_t)j]->flags_;
-            cs[(size_t)i]->peer_p2p_[j] = cs[(size_t)j]->p2p_;
+            ci->ch_->peer_scratch[j] = cs[(size_t)j]->scratch_;
+            ci->ch_->peer_ag[j] = cs[(size_t)j]->scratch_ag_;
+            ci->ch_->peer_flags[j] = cs[(size_t)j]->flags_;
+            ci->peer_p2p_[j] = cs[(size_t)j]->p2p_;
             if (devices[i] != devices[j]) {
                 int can = 0;
                 (void)hipSetDevice(devices[i]);
@@ -355,6 +531,7 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
             }
         }
     }
+    for (auto& c : cs) c->Alias();  // the aliases now include the peers
     out->clear();
     for (auto& c : cs) out->push_back(c.release());
 }
@@ -366,16 +543,11 @@ Communicator::~Communicator() {
     (void)hipDeviceSynchronize();
     if (owns_peers_ipc_ && bs_) {
         try {
-            bs_->barrier();  // nobody still pushes into my scratch
+            bs_->barrier();  // nobody still pushes into my p2p slots
         } catch (...) {
         }
         for (int p = 0; p < n_; ++p)
-            if (p != rank_) {
-                if (peer_scratch_[p]) (void)hipIpcCloseMemHandle(peer_scratch_[p]);
-                if (peer_ag_[p]) (void)hipIpcCloseMemHandle(peer_ag_[p]);
-                if (peer_flags_[p]) (void)hipIpcCloseMemHandle(peer_flags_[p]);
-                if (peer_p2p_[p]) (void)hipIpcCloseMemHandle(peer_p2p_[p]);
-            }
+            if (p != rank_ && peer_p2p_[p]) (void)hipIpcCloseMemHandle(peer_p2p_[p]);
         try {
             bs_->barrier();  // every importer closed its mapping
         } catch (...) {
@@ -386,12 +558,14 @@ Communicator::~Communicator() {
     if (image_) (void)hipFreeAsync(image_, nullptr);
     (void)hipStreamSynchronize(nullptr);
     for (auto& r : retired_) (void)hipEventDestroy(r.first);
-    if (scratch_) (void)hipFree(scratch_);
-    if (scratch_ag_) (void)hipFree(scratch_ag_);
-    if (flags_) (void)hipFree(flags_);
     if (p2p_) (void)hipFree(p2p_);
-    if (err_) (void)hipFree(err_);
-    if (err_host_) (void)hipHostFree(err_host_);
+    if (ch_) {
+        {
+            std::lock_guard<std::mutex> lk(ch_->mu);
+            --ch_->users;
+        }
+        ch_.reset();  // the last user frees the channel (collective over its bootstrap)
+    }
 }
 
 P2PEngine* Communicator::P2P() {
@@ -478,6 +652,7 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
     if (n_ == 1 || count == 0) return;
     if (buf == nullptr) throw std::invalid_argument("rdc: null buffer");
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    ChannelCall call(ch_.get(), stream);
     // TryAllreduce (communicator_collective.cc:6-13): the ring for buffers of
     // more than rdc_reduce_ring_mincount bytes, the tree's order otherwise
     if ((uint64_t)count * esz <= cfg_.ring_mincount || algo == RDC_ALGO_TREE) {
@@ -509,6 +684,7 @@ void Communicator::AllreduceRanges(void* buf, const uint64_t* off, const uint64_
     }
     if (total == 0) return;
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    ChannelCall call(ch_.get(), stream);
     // a piece's ranges are not one contiguous span: never one-shot (it pushes [0, total))
     int algo = PickAlgo(RDC_ALGO_AUTO);
     if (algo == RDC_ALGO_ONESHOT) algo = RDC_ALGO_MESH;
@@ -731,6 +907,7 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
     }
     if (n_ == 1 || nbuf == 0) return;
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    ChannelCall call(ch_.get(), stream);
     if (algo == RDC_ALGO_TREE || cfg_.ring_mincount >= esz) {
         // buffers of <= rdc_reduce_ring_mincount bytes take the tree's order
         // (TryAllreduce per buffer, communicator_collective.cc:6-13); the
@@ -840,6 +1017,7 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
     if (n_ == 1 || bytes == 0) return;
     if (buf == nullptr) throw std::invalid_argument("rdc: null buffer");
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    ChannelCall call(ch_.get(), stream);
     for (const Piece& p :
          PlanBroadcast(bytes, layout(), cfg_.tile_bytes, LaunchGrid(max_blocks(), occupancy_bcast()))) {
         CollArgs a;
@@ -880,6 +1058,7 @@ double Communicator::Probe(int mode, size_t* bytes_io, int reps, hipStream_t str
     if (bytes == 0 || reps <= 0) throw std::invalid_argument("rdc: probe needs bytes and reps");
     *bytes_io = bytes;
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    ChannelCall call(ch_.get(), stream);
     PushTargets t;
     memset(&t, 0, sizeof(t));
     int nd = 0;
@@ -919,6 +1098,7 @@ void Communicator::Allgather(void* const* bufs, const uint64_t* sizes, hipStream
     for (int c = 0; c < n_; ++c)
         if (sizes[c] && bufs[c] == nullptr) throw std::invalid_argument("rdc: null allgather buffer");
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    ChannelCall call(ch_.get(), stream);
     for (const Piece& p :
          PlanAllgather(n_, sizes, layout(), cfg_.tile_bytes, LaunchGrid(max_blocks(), occupancy_allgather()))) {
         CollArgs a;
@@ -948,7 +1128,10 @@ void Communicator::Check(hipStream_t stream) {
 uint32_t Communicator::ArmNotify() {
     if (err_host_dev_ == nullptr) return 0;
     notify_ = err_host_dev_ + 4;
-    notify_val_ = ++notify_token_;
+    {
+        std::lock_guard<std::mutex> lk(ch_->mu);  // tokens unique across the channel's communicators
+        notify_val_ = ++ch_->notify_token;
+    }
     return notify_val_;
 }
 

@@ -49,6 +49,48 @@ struct P2PCtl;
 class P2PEngine;
 class WorkComp;
 
+// The collective state of one set of ranks: the RS / AG scratch regions, the
+// flag array, the device error word and launch counter, and the peers' IPC
+// mappings of all of them.  Communicators created over the same bootstrap
+// (every named communicator of the process: "main", "second", the
+// checkpoint-style ones) SHARE one channel instead of 4 GiB of scratch and
+// n-1 peer mappings each: their launches are serialised on the channel in
+// issue order (stream order; a launch on another stream than the channel's
+// previous one waits for it by event), which every rank issues identically —
+// the reference's collectives block the caller, so its communicators see
+// one global order too.  Point-to-point stays per communicator (messages on
+// different communicators must not match each other).  RDC_SHARE_SCRATCH=0
+// gives every communicator its own channel.
+struct Channel {
+    ~Channel();  // closes the peers' mappings (collective over bs) and frees
+    // serialise a call on `s` behind the channel's previous one (only when
+    // several communicators use the channel) / record the call's end on `s`
+    void Order(hipStream_t s);
+    void Mark(hipStream_t s);
+
+    Bootstrap* bs = nullptr;   // not owned; null for single-process groups
+    uint64_t id = 0;           // per-bootstrap creation index (equal on every rank)
+    int rank = 0, n = 1, device = 0;
+    bool ipc = false;          // peers' regions opened through IPC
+    Layout L;
+    int alloc_kind = 0;
+    char* scratch = nullptr;
+    char* scratch_ag = nullptr;
+    uint32_t* flags = nullptr;
+    uint32_t* err = nullptr;           // [0] error word, [16] arrivals, [32] launches, [48] last kind
+    uint32_t* err_host = nullptr;      // pinned: [0] error mirror, [4] notify token
+    uint32_t* err_host_dev = nullptr;
+    char* peer_scratch[RDC_MAX_RANKS] = {};
+    char* peer_ag[RDC_MAX_RANKS] = {};
+    uint32_t* peer_flags[RDC_MAX_RANKS] = {};
+    std::mutex mu;
+    int users = 0;                     // communicators attached
+    uint32_t notify_token = 0;
+    hipEvent_t last_ev = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
+};
+
 class Communicator {
 public:
     // Multi-process: one communicator per process, peers found through `bs`
@@ -129,6 +171,7 @@ public:
     int alloc_kind() const { return alloc_kind_; }  // 0 uncached, 1 fine-grained, 2 coarse
     size_t slot_bytes() const { return slot_bytes_; }
     uint32_t seq() const { return seq_; }
+    bool shares_channel() const;  // another communicator uses this one's scratch
     const CommConfig& config() const { return cfg_; }
     Layout layout() const;
     // requested grids (RDC_NBLOCKS / Tune, else automatic); every launch is then
@@ -142,7 +185,11 @@ public:
 
 private:
     Communicator();
-    void AllocLocal();
+    void AllocLocal();                                   // a fresh channel + this communicator's p2p region
+    void AllocChannel();
+    void AllocP2P();
+    void Attach(const std::shared_ptr<Channel>& ch);     // one more user of the channel, then Alias()
+    void Alias();                                        // copy the channel's pointers into the names below
     void FillArgsCommon(CollArgs* a) const;
     int PickAlgo(int algo) const;
     int PickAlgo(int algo, uint64_t bytes) const;
@@ -171,7 +218,8 @@ private:
     CommConfig cfg_;
     Bootstrap* bs_ = nullptr;       // not owned (unless owned_bs_ holds it: group communicators)
     std::unique_ptr<Bootstrap> owned_bs_;
-    bool owns_peers_ipc_ = false;   // peers opened through IPC
+    std::shared_ptr<Channel> ch_;   // scratch_ ... peer_flags_ below alias its resources
+    bool owns_peers_ipc_ = false;   // peers' p2p regions opened through IPC
     char* scratch_ = nullptr;       // RS region
     char* scratch_ag_ = nullptr;    // AG region
     uint32_t* flags_ = nullptr;
@@ -180,7 +228,6 @@ private:
     uint32_t* err_host_dev_ = nullptr;
     uint32_t* notify_ = nullptr;    // armed: device address of the pinned notify word
     uint32_t notify_val_ = 0;
-    uint32_t notify_token_ = 0;
     uint64_t* trace_ = nullptr;     // TraceNext
     size_t trace_words_ = 0;
     uint64_t last_launch_[6] = {};

@@ -64,6 +64,36 @@ def main():
             np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
             print("rank %d case %d ok" % (rank, i), flush=True)
             continue
+        if kind == "shared_comms":
+            # named communicators over the same ranks share one scratch channel:
+            # memory cost, and launches of different communicators issued on
+            # different streams without host syncs (the channel orders them)
+            free0 = torch.cuda.mem_get_info()[0]
+            extra = [rdc_amd.new_comm("shared_%d_%d" % (i, k)) for k in range(2)]
+            free1 = torch.cuda.mem_get_info()[0]
+            shares = [comm.get_param("shares_scratch")] + [e.get_param("shares_scratch") for e in extra]
+            streams = [torch.cuda.Stream() for _ in range(3)]
+            bufs = [torch.zeros(count, dtype=torch.float32, device="cuda") for _ in range(3)]
+            torch.cuda.synchronize()
+            for j, (cm, st, b) in enumerate(zip([comm] + extra, streams, bufs)):
+                check_call(_LIB.RdcFill(ctypes.c_void_p(b.data_ptr()), count, 6, 0x5EED4000 + j, rank,
+                                        ctypes.c_void_p(st.cuda_stream)))
+            for rep in range(c.get("reps", 1)):
+                for j, (cm, st, b) in enumerate(zip([comm] + extra, streams, bufs)):
+                    algo = (rep + j) % 4
+                    check_call(_LIB.RdcCommAllreduceEx(cm.handle, ctypes.c_void_p(b.data_ptr()), count, 6, 2, algo,
+                                                       ctypes.c_void_p(st.cuda_stream)))
+            torch.cuda.synchronize()
+            for cm, st in zip([comm] + extra, streams):
+                cm.check(ctypes.c_void_p(st.cuda_stream))
+            out = torch.cat(bufs).cpu().numpy().view(np.uint8)
+            np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
+            open(os.path.join(outdir, "case%d_rank%d.json" % (i, rank)), "w").write(
+                json.dumps({"shares": shares, "bytes_used_by_two_comms": free0 - free1}))
+            for e in extra:
+                e.destroy()
+            print("rank %d case %d ok" % (rank, i), flush=True)
+            continue
         if kind == "bcast_chain":
             # stream-ordered chain without host syncs: refill, broadcast from a
             # rotating root, accumulate — exposes a root overwriting a peer's

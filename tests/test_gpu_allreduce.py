@@ -403,6 +403,30 @@ def test_mp_tree_path_ring_mincount(world):
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (world, i, c, r)
 
 
+def test_mp_named_communicators_share_scratch():
+    """Every named communicator over the same ranks shares ONE scratch channel
+    (4080 MiB by default, not 4080 MiB per communicator): two more
+    communicators cost only their point-to-point regions, and allreduces on
+    three communicators issued back to back on three different streams, every
+    schedule, no host syncs, all come out bit-exact (the channel orders them)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [{"count": 300007, "dtype": 6, "op": 2, "kind": "shared_comms", "reps": 4}]
+    tmp = run_mp(3, cases, env_extra={"RDC_SCRATCH_BYTES": "4080M"})
+    for r in range(3):
+        info = json.load(open(os.path.join(tmp, "case0_rank%d.json" % r)))
+        assert info["shares"] == [1, 1, 1], info
+        assert info["bytes_used_by_two_comms"] < (512 << 20), info  # two p2p regions, no 2 x 4 GiB scratch
+        got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
+        want = []
+        for j in range(3):
+            xs = [O.fill(300007, 6, 0x5EED4000 + j, q) for q in range(3)]
+            for _ in range(4):
+                O.allreduce_ring(xs, 6, 2)
+            want.append(xs[r])
+        assert got.tobytes() == np.concatenate(want).view(np.uint8).tobytes(), r
+
+
 def test_mp_full_size_cfg2():
     """BASELINE cfg2 at full size: fp32 256 MiB allreduce over 2 ranks, both
     schedules, checked bit-exact (sha256) against the oracle's ring."""
