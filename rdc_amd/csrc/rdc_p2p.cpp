@@ -34,6 +34,33 @@ bool trace_on() {
 void hip_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string("rdc p2p: ") + what + ": " + hipGetErrorString(e));
 }
+// The control block must sit on pages of its own, wholly inside ONE device
+// mapping (round 1's illegal address, DESIGN.md §4 "Point-to-point": the
+// only host memory a copy kernel touches is this block, and a block that
+// shared pages with heap objects could lose its GPU mapping when the runtime
+// pinned and unpinned those pages for an unrelated copy).  Returns the block's
+// device address; throws if any of that does not hold.
+char* checked_ctl_mapping(const P2PCtl* ctl) {
+    const uintptr_t page = 4096;
+    if ((uintptr_t)ctl % page != 0)
+        throw std::logic_error("rdc p2p: control block not page-aligned (it must own its pages)");
+    void* d0 = nullptr;
+    hip_check(hipHostGetDevicePointer(&d0, const_cast<P2PCtl*>(ctl), 0), "control block device address");
+    const char* last = reinterpret_cast<const char*>(ctl) + sizeof(P2PCtl) - 1;
+    hipPointerAttribute_t a0, a1;
+    memset(&a0, 0, sizeof(a0));
+    memset(&a1, 0, sizeof(a1));
+    hip_check(hipPointerGetAttributes(&a0, ctl), "control block attributes");
+    hip_check(hipPointerGetAttributes(&a1, last), "control block attributes (last byte)");
+    const bool mapped = a0.type == hipMemoryTypeHost && a1.type == hipMemoryTypeHost && a0.devicePointer &&
+                        a1.devicePointer &&
+                        static_cast<char*>(a1.devicePointer) - static_cast<char*>(a0.devicePointer) ==
+                            (ptrdiff_t)(sizeof(P2PCtl) - 1) &&
+                        a0.devicePointer == d0;
+    if (!mapped) throw std::logic_error("rdc p2p: control block is not one contiguous device-mapped host range");
+    return static_cast<char*>(d0);
+}
+
 bool is_host(const void* p) {
     hipPointerAttribute_t a;
     memset(&a, 0, sizeof(a));
@@ -85,9 +112,7 @@ P2PEngine::P2PEngine(int rank, int n, int device, size_t slot_bytes, char* local
     : rank_(rank), n_(n), device_(device), slot_bytes_(slot_bytes), timeout_s_(timeout_s), local_(local), ctl_(ctl) {
     for (int p = 0; p < RDC_MAX_RANKS; ++p) peers_[p] = p < n ? peers[p] : nullptr;
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    void* d = nullptr;
-    hip_check(hipHostGetDevicePointer(&d, ctl_, 0), "control block device address");
-    ctl_dev_ = static_cast<char*>(d);
+    ctl_dev_ = checked_ctl_mapping(ctl_);
     hip_check(hipMalloc(&arrive_, 2 * RDC_MAX_RANKS * sizeof(uint32_t)), "hipMalloc arrival counters");
     hip_check(hipMemset(arrive_, 0, 2 * RDC_MAX_RANKS * sizeof(uint32_t)), "memset arrival counters");
     hip_check(hipDeviceSynchronize(), "sync");
@@ -115,7 +140,19 @@ P2PEngine::~P2PEngine() {
 }
 
 uint64_t* P2PEngine::DevWord(const std::atomic<uint64_t>& w) const {
-    return reinterpret_cast<uint64_t*>(ctl_dev_ + (reinterpret_cast<const char*>(&w) - reinterpret_cast<const char*>(ctl_)));
+    const ptrdiff_t off = reinterpret_cast<const char*>(&w) - reinterpret_cast<const char*>(ctl_);
+    if (off < 0 || off % 8 != 0 || (size_t)off + sizeof(uint64_t) > sizeof(P2PCtl))
+        throw std::logic_error("rdc p2p: control word outside the control block");
+    return reinterpret_cast<uint64_t*>(ctl_dev_ + off);
+}
+
+// every address a copy kernel will touch, checked before the launch
+void P2PEngine::CheckLaunch(const char* slot_base, size_t slot_off, size_t len, const uint32_t* arrive) const {
+    const size_t region = (size_t)n_ * kP2PSlots * slot_bytes_;
+    if (slot_base == nullptr || slot_off + len > region || len > slot_bytes_ || (slot_off % slot_bytes_) != 0)
+        throw std::logic_error("rdc p2p: piece outside the slot region");
+    if (arrive < arrive_ || arrive >= arrive_ + 2 * RDC_MAX_RANKS)
+        throw std::logic_error("rdc p2p: arrival counter outside its allocation");
 }
 
 WorkComp* P2PEngine::Post(Lane& L, char* buf, size_t bytes, hipStream_t after) {
@@ -236,7 +273,9 @@ bool P2PEngine::StepSend(int dest, Lane& L) {
                           "H2D");
                 src = L.bounce + (size_t)s * slot_bytes_;
             }
-            char* dst = peers_[dest] + ((size_t)rank_ * kP2PSlots + s) * slot_bytes_;
+            const size_t slot_off = ((size_t)rank_ * kP2PSlots + s) * slot_bytes_;
+            CheckLaunch(peers_[dest], slot_off, len, arrive_ + dest);
+            char* dst = peers_[dest] + slot_off;
             ctl_->len[rank_][dest][s].v.store(len, std::memory_order_relaxed);  // published by posted's release
             hip_check(launch_copy(dst, src, len, L.stream, arrive_ + dest, DevWord(ctl_->posted[rank_][dest].v), seq),
                       "launch copy");
@@ -267,7 +306,9 @@ bool P2PEngine::StepRecv(int src, Lane& L) {
                 return true;
             }
             Ready(L, r);
-            const char* from = local_ + ((size_t)src * kP2PSlots + s) * slot_bytes_;
+            const size_t slot_off = ((size_t)src * kP2PSlots + s) * slot_bytes_;
+            CheckLaunch(local_, slot_off, len, arrive_ + RDC_MAX_RANKS + src);
+            const char* from = local_ + slot_off;
             char* to = r.buf + r.issued;
             uint64_t* word = DevWord(ctl_->consumed[src][rank_].v);
             if (r.host) {  // DMA, then a signal-only launch (stream order: after the copy landed)

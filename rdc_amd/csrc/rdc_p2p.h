@@ -39,7 +39,21 @@ constexpr int kP2PSlots = 2;
 // reference WorkStatus values (include/core/work_request.h:23-30)
 enum { RDC_WS_PENDING = 1 << 1, RDC_WS_RUNNING = 1 << 2, RDC_WS_FINISHED = 1 << 3, RDC_WS_ERROR = 1 << 6 };
 
-struct P2PCtl {  // in host shared memory, 64-B lines
+// Control block.  Lives on pages of its own (a POSIX shm mapping, or a
+// hipHostMalloc'd block for single-process groups), registered for device
+// access as ONE range: the copy kernels' only host-memory access is the
+// system-scope store of `posted` / `consumed` into it.  Round 1 saw one
+// illegal address in test_device_to_device when the group block was a
+// heap object registered with hipHostRegister: the registration covered
+// whole pages shared with unrelated heap allocations, and the runtime pins
+// and unpins pageable pages around its own copies, which can drop the GPU
+// mapping of exactly those pages; k_copy's `word` store (the last block's
+// release of posted / consumed) was the only access to such a page — its
+// `arrive` counter is hipMalloc'd HBM and its data pointers are HBM slots
+// and the user's device buffer.  P2PEngine now refuses a block that is not
+// page-aligned and mapped as one contiguous range (checked_ctl_mapping), and
+// every launch checks its slot range, arrival counter and control word.
+struct P2PCtl {  // 64-B lines; 16 pages
     struct alignas(64) Word {
         std::atomic<uint64_t> v;
     };
@@ -102,7 +116,8 @@ private:
     void Loop();
     bool Progress();        // one pass; true if anything moved
     bool Complete(Lane& L, const std::atomic<uint64_t>& word);
-    uint64_t* DevWord(const std::atomic<uint64_t>& w) const;  // device address of a control word
+    uint64_t* DevWord(const std::atomic<uint64_t>& w) const;  // device address of a control word (range-checked)
+    void CheckLaunch(const char* slot_base, size_t slot_off, size_t len, const uint32_t* arrive) const;
     bool StepSend(int peer, Lane& L);
     bool StepRecv(int peer, Lane& L);
     void Ready(Lane& L, Req& r);
