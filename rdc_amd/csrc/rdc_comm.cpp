@@ -162,6 +162,16 @@ std::mutex g_reg_mu;
 std::map<Bootstrap*, std::vector<std::weak_ptr<Channel>>> g_channels;
 std::map<Bootstrap*, uint64_t> g_channel_count;
 
+// RDC_STRICT_FENCES=1: keep the system-scope release fences on every hand-off
+// even with uncached scratch (diagnostics; rdc_device.h block_publish)
+bool strict_fences() {
+    static const bool on = [] {
+        const char* v = getenv("RDC_STRICT_FENCES");
+        return v && *v && atoi(v) != 0;
+    }();
+    return on;
+}
+
 bool share_enabled() {
     const char* v = getenv("RDC_SHARE_SCRATCH");
     return !(v && *v && atoi(v) == 0);
@@ -618,6 +628,7 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     a->launch_kind = err_ + 48;
     a->half_bytes = OneshotHalfBytes(layout());
     a->timeout_ticks = (uint64_t)(cfg_.timeout_s * (double)wall_khz_ * 1000.0);
+    a->uc = (alloc_kind_ == 0 && !strict_fences()) ? 1 : 0;
 }
 
 Layout Communicator::layout() const {

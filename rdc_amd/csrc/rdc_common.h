@@ -104,5 +104,7 @@ struct CollArgs {
     const void* units;                   // coalesced mesh: device PackUnit table (off/len are packed
     int nunits;                          //   offsets; user bytes reached through the units), else null
     uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up
+    int uc;                              // 1: every scratch region is uncached (hand-offs need no L2
+                                         //   write-back, rdc_device.h block_publish)
     uint64_t* trace;                     // optional (mesh/ring): per block {start, end} wall_clock64 ticks
 };

@@ -131,23 +131,36 @@ __device__ __forceinline__ void flag_store(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ bool seq_reached(uint32_t v, uint32_t seq) { return (int32_t)(v - seq) >= 0; }
 
 // Called by EVERY thread of the block after its payload stores.  Lanes
-// 0..nflags-1 of wave 0 then store flags[i] = seq after a system release.
-__device__ __forceinline__ void block_publish(uint32_t* const* flags, int nflags, uint32_t seq) {
+// 0..nflags-1 of wave 0 then store flags[i] = seq.
+// Every hand-off payload lives in the peers' scratch slots.  When all scratch
+// is uncached (MTYPE UC, hipDeviceMallocUncached: `uc`), those stores are
+// write-through — no XCD's L2 keeps them — and every storing wave's
+// `s_waitcnt vmcnt(0)` (before the barrier) means they have been performed
+// at memory: the write-through + drained-flag form of MI355X_MICROARCH.md
+// ("Valid forms", R1), with uncached memory in place of `sc1` stores.  The
+// system-scope release fence would only add an L2 write-back (buffer_wbl2
+// sc0 sc1, 1.7-6.5 us per call) of cached lines no peer reads, so it is
+// issued only for fine- / coarse-grained scratch (alloc fallbacks).
+__device__ __forceinline__ void block_publish(uint32_t* const* flags, int nflags, uint32_t seq, int uc) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < (unsigned)nflags) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!uc) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         flag_store(flags[threadIdx.x], seq);
     }
 }
 
-__device__ __forceinline__ void block_publish1(uint32_t* flag, uint32_t seq) {
+__device__ __forceinline__ void block_publish1(uint32_t* flag, uint32_t seq, int uc) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!uc) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         flag_store(flag, seq);
     }
 }

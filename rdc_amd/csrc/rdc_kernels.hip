@@ -39,7 +39,7 @@ __device__ void allgather_body(const CollArgs& a, uint32_t seq) {
             uint64_t tlen = a.len[r] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
             block_copy(a.ag[p] + (uint64_t)r * a.slot_bytes + a.mis[r] + toff, a.cbuf[r] + a.off[r] + toff, tlen);
-            block_publish1(a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t, seq);
+            block_publish1(a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t, seq, a.uc);
         }
         return;
     }

@@ -260,7 +260,7 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
                 });
             else
                 block_copy(dst + toff, a.user + a.off[c] + toff, tlen);
-            block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, seq);
+            block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, seq, a.uc);
         }
         return;
     }
@@ -288,7 +288,7 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
                 const int p = (r + 1 + threadIdx.x) % n;
                 s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
             }
-            block_publish(s_flags, n - 1, seq);
+            block_publish(s_flags, n - 1, seq, a.uc);
             __syncthreads();
         }
         return;
@@ -375,7 +375,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
                 block_copy(a.rs[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
                            tlen);
-                block_publish1(a.flags[prev] + (uint64_t)j * a.max_tiles + t, seq);
+                block_publish1(a.flags[prev] + (uint64_t)j * a.max_tiles + t, seq, a.uc);
             }
             const int cr = (r + 2 + j) % n;
             if (t < a.tiles[cr]) {
@@ -398,7 +398,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
                 block_copy(a.ag[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
                            tlen);
-                block_publish1(a.flags[prev] + (uint64_t)(n + j) * a.max_tiles + t, seq);
+                block_publish1(a.flags[prev] + (uint64_t)(n + j) * a.max_tiles + t, seq, a.uc);
             }
             const int cr = (r + 1 + j) % n;
             if (t < a.tiles[cr]) {
@@ -561,7 +561,7 @@ __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
             block_copy(a.rs[(r + k) % n] + (uint64_t)r * a.slot_bytes + half + toff, a.user + toff, tlen);
         if (threadIdx.x < (unsigned)(n - 1))
             s_flags[threadIdx.x] = a.flags[(r + 1 + threadIdx.x) % n] + (uint64_t)r * a.max_tiles + t;
-        block_publish(s_flags, n - 1, seq);
+        block_publish(s_flags, n - 1, seq, a.uc);
         __syncthreads();
     }
     // 2) fold my tiles once every peer's copy landed
@@ -633,11 +633,11 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
             if (split) {
                 const int f = bcast_forwarder(n, root, t);
                 block_copy(a.ag[f] + soff, mine, tlen);
-                block_publish1(a.flags[f] + frow, seq);
+                block_publish1(a.flags[f] + frow, seq, a.uc);
             } else {
                 for (int k = 1; k < n; ++k) block_copy(a.ag[(root + k) % n] + soff, mine, tlen);
                 if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.flags[(root + 1 + threadIdx.x) % n] + frow;
-                block_publish(s_flags, n - 1, seq);
+                block_publish(s_flags, n - 1, seq, a.uc);
             }
             __syncthreads();
         } else {
@@ -655,7 +655,7 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
                     for (int q = 0; q < n; ++q)
                         if (q != r && q != root) s_flags[k++] = a.flags[q] + frow;
                 }
-                block_publish(s_flags, n - 2, seq);  // its barrier orders thread 0's list before use
+                block_publish(s_flags, n - 2, seq, a.uc);  // its barrier orders thread 0's list before use
             }
             block_copy(mine, land, tlen);
             __syncthreads();
@@ -668,16 +668,23 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
 // publishes done = seq into every peer's flag array (row 2n, column = this
 // rank: "this rank finished reading its scratch for launch seq") and
 // advances the launch counter.
+// The done words mean "finished READING my scratch for launch seq": every
+// wave's loads have returned once it passed `s_waitcnt vmcnt(0)`, so with
+// uncached scratch and no host memory involved the arrival add and the done
+// stores need no fence (the next launch of this communicator sees this one's
+// buffer writes through the kernel boundary).  A launch that writes host
+// memory (zero-copy host path: `notify`) or uses cached scratch keeps the
+// system-scope fences, so the host reads the results after the notify word.
 __device__ __forceinline__ void launch_done(const CollArgs& a, uint32_t seq) {
+    const bool fence = a.notify != nullptr || !a.uc;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        // system scope: a launch may write host memory (zero-copy host path),
-        // which must be visible before the last block's notify store
-        __threadfence_system();
+        if (fence) __threadfence_system();
         const uint32_t prev = atomicAdd(a.done_ctr, 1u);
         if (prev == gridDim.x - 1) {
             __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int p = 0; p < a.n; ++p)
                 if (p != a.rank) flag_store(done_word(a, p, a.rank), seq);
