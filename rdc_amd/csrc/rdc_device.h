@@ -173,9 +173,13 @@ struct Abort {
 // Block-wide wait until every flags[i] (i < nflags <= 64) reached seq.  Wave 0
 // polls (one lane per flag), sleeping between polls; the other waves park at
 // the barrier.  Returns false (uniformly) on timeout or if another block of
-// this launch already aborted.
+// this launch already aborted.  With cached scratch the matching lane then
+// runs a system-scope acquire (L2 / L1 invalidate) so the block's plain loads
+// of the handed-off bytes cannot hit stale lines; uncached scratch (`uc`) is
+// never held in any GPU cache, so its loads after the matched poll read
+// memory and need no invalidate (MI355X_MICROARCH.md: an acquire is ≈1.7 us).
 __device__ __forceinline__ bool block_wait(uint32_t* const* flags, int nflags, uint32_t seq,
-                                           const Abort& ab, uint32_t code) {
+                                           const Abort& ab, uint32_t code, int uc) {
     __shared__ int s_ok;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
@@ -193,10 +197,10 @@ __device__ __forceinline__ bool block_wait(uint32_t* const* flags, int nflags, u
             __builtin_amdgcn_s_sleep(1);
         }
         if (lane == 0) {
-            if (ok) {
+            if (ok && !uc) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            } else {
+            } else if (!ok) {
                 uint32_t expected = 0;
                 __hip_atomic_compare_exchange_strong(ab.err, &expected, code, __ATOMIC_RELAXED,
                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

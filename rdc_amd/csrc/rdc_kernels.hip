@@ -30,7 +30,7 @@ __device__ void allgather_body(const CollArgs& a, uint32_t seq) {
         if (b < items) {
             if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = done_word(a, r, (r + 1 + threadIdx.x) % n);
             __syncthreads();
-            if (!block_wait(s_flags, n - 1, seq - 1, ab, RDC_KERR_TIMEOUT_ALLGATHER)) return;
+            if (!block_wait(s_flags, n - 1, seq - 1, ab, RDC_KERR_TIMEOUT_ALLGATHER, a.uc)) return;
         }
         for (int it = b; it < items; it += a.nb_scatter) {
             const int t = it / (n - 1);
@@ -53,7 +53,7 @@ __device__ void allgather_body(const CollArgs& a, uint32_t seq) {
         if (t >= a.tiles[c]) continue;
         if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
         __syncthreads();
-        if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_ALLGATHER)) return;
+        if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_ALLGATHER, a.uc)) return;
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[c] - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;

@@ -53,7 +53,7 @@ __device__ __forceinline__ bool gate_on_peers(const CollArgs& a, uint32_t seq, i
     __shared__ uint32_t* s_gate[RDC_MAX_RANKS];
     if (threadIdx.x < (unsigned)count) s_gate[threadIdx.x] = done_word(a, a.rank, (first + threadIdx.x) % a.n);
     __syncthreads();
-    return block_wait(s_gate, count, seq - 1, ab, code);
+    return block_wait(s_gate, count, seq - 1, ab, code, a.uc);
 }
 
 
@@ -273,7 +273,7 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
                 s_flags[threadIdx.x] = a.flags[r] + (uint64_t)p * a.max_tiles + t;
             }
             __syncthreads();
-            if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS)) return;
+            if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return;
             const uint64_t toff = (uint64_t)t * a.tile_bytes;
             uint64_t tlen = a.len[r] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
@@ -302,7 +302,7 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
         if (t >= a.tiles[c]) continue;
         if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
         __syncthreads();
-        if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_AG)) return;
+        if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_AG, a.uc)) return;
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[c] - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
@@ -381,7 +381,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
             if (t < a.tiles[cr]) {
                 if (threadIdx.x == 0) s_flag[0] = a.flags[r] + (uint64_t)j * a.max_tiles + t;
                 __syncthreads();
-                if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING)) return;
+                if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING, a.uc)) return;
                 uint64_t tlen = a.len[cr] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
                 block_reduce_into<OP, T>(a.user + a.off[cr] + toff,
@@ -404,7 +404,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
             if (t < a.tiles[cr]) {
                 if (threadIdx.x == 0) s_flag[0] = a.flags[r] + (uint64_t)(n + j) * a.max_tiles + t;
                 __syncthreads();
-                if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING)) return;
+                if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING, a.uc)) return;
                 uint64_t tlen = a.len[cr] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
                 block_copy(a.user + a.off[cr] + toff, a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr] + toff,
@@ -570,7 +570,7 @@ __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
         if (threadIdx.x < (unsigned)(n - 1))
             s_flags[threadIdx.x] = a.flags[r] + (uint64_t)((r + 1 + threadIdx.x) % n) * a.max_tiles + t;
         __syncthreads();
-        if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS)) return;
+        if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return;
         const uint64_t lo = (uint64_t)t * a.tile_bytes;
         const uint64_t hi = lo + a.tile_bytes < total ? lo + a.tile_bytes : total;
         if (TREE) {
@@ -620,7 +620,7 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
             s_cnt = k;
         }
         __syncthreads();
-        if (!block_wait(s_flags, s_cnt, seq - 1, ab, RDC_KERR_TIMEOUT_BCAST)) return;
+        if (!block_wait(s_flags, s_cnt, seq - 1, ab, RDC_KERR_TIMEOUT_BCAST, a.uc)) return;
     }
     for (int t = blockIdx.x; t < a.tiles[0]; t += gridDim.x) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
@@ -643,7 +643,7 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
         } else {
             if (threadIdx.x == 0) s_flags[0] = a.flags[r] + frow;
             __syncthreads();
-            if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_BCAST)) return;
+            if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_BCAST, a.uc)) return;
             const char* land = a.ag[r] + soff;
             if (split && bcast_forwarder(n, root, t) == r) {
                 for (int k = 1; k < n; ++k) {
@@ -690,9 +690,12 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint32_t seq) {
                 if (p != a.rank) flag_store(done_word(a, p, a.rank), seq);
             __hip_atomic_store(a.launch_kind, (uint32_t)a.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.launch_ctr, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // the host reads the (sticky) error word here after a stream sync: no copy needed
-            __hip_atomic_store(a.err_mirror, __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the host reads the (sticky) error word here after a stream sync: no
+            // copy needed.  The mirror starts at 0 and only ever changes to an
+            // error, so the PCIe write (whose completion the kernel's end waits
+            // for) is made only when there is one.
+            const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e != 0) __hip_atomic_store(a.err_mirror, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (a.notify) __hip_atomic_store(a.notify, a.notify_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
