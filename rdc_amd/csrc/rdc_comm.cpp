@@ -19,6 +19,7 @@
 #include "rdc_kernels.h"
 #include "rdc_p2p.h"
 #include "rdc_plan.h"
+#include "rdc_service.h"
 
 namespace rdc_amd {
 
@@ -85,6 +86,7 @@ struct Handles {  // round 2 of Create: IPC handles (scratch ones only for a new
     hipIpcMemHandle_t scratch;
     hipIpcMemHandle_t ag;
     hipIpcMemHandle_t flags;
+    hipIpcMemHandle_t svc;
     hipIpcMemHandle_t p2p;
 };
 
@@ -179,6 +181,7 @@ bool share_enabled() {
 }  // namespace
 
 Channel::~Channel() {
+    svc.reset();  // the resident service block leaves first
     (void)hipSetDevice(device);
     (void)hipDeviceSynchronize();
     if (ipc && bs) {
@@ -191,6 +194,7 @@ Channel::~Channel() {
                 if (peer_scratch[p]) (void)hipIpcCloseMemHandle(peer_scratch[p]);
                 if (peer_ag[p]) (void)hipIpcCloseMemHandle(peer_ag[p]);
                 if (peer_flags[p]) (void)hipIpcCloseMemHandle(peer_flags[p]);
+                if (peer_svc_region[p]) (void)hipIpcCloseMemHandle(peer_svc_region[p]);
             }
         try {
             bs->barrier();  // every importer closed its mapping
@@ -201,6 +205,7 @@ Channel::~Channel() {
     if (scratch) (void)hipFree(scratch);
     if (scratch_ag) (void)hipFree(scratch_ag);
     if (flags) (void)hipFree(flags);
+    if (svc_region) (void)hipFree(svc_region);  // svc_flags live at its end
     if (err) (void)hipFree(err);
     if (err_host) (void)hipHostFree(err_host);
 }
@@ -257,7 +262,12 @@ void Communicator::AllocChannel() {
     ch->scratch = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k1));
     ch->scratch_ag = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k3));
     ch->flags = static_cast<uint32_t*>(alloc_shared(ch->L.flag_bytes, &k2));
-    ch->alloc_kind = std::max(std::max(k1, k2), k3);
+    int k5 = 0;  // service slots [2][n] x RDC_SVC_MAX_BYTES, then its n arrival words
+    const size_t svc_slots = (size_t)2 * n_ * RDC_SVC_MAX_BYTES;
+    ch->svc_region = static_cast<char*>(alloc_shared(svc_slots + 4096, &k5));
+    ch->svc_flags = reinterpret_cast<uint32_t*>(ch->svc_region + svc_slots);
+    hip_check(hipMemset(ch->svc_flags, 0, 4096), "memset service flags");
+    ch->alloc_kind = std::max(std::max(std::max(k1, k2), k3), k5);
     // [0] error word, [16] block arrival counter, [32] completed-launch counter, [48] last kind
     hip_check(hipMalloc(&ch->err, 256), "hipMalloc err");
     hip_check(hipMemset(ch->flags, 0, ch->L.flag_bytes), "memset flags");
@@ -270,6 +280,8 @@ void Communicator::AllocChannel() {
     ch->peer_scratch[rank_] = ch->scratch;
     ch->peer_ag[rank_] = ch->scratch_ag;
     ch->peer_flags[rank_] = ch->flags;
+    ch->peer_svc_region[rank_] = ch->svc_region;
+    ch->peer_svc_flags[rank_] = ch->svc_flags;
     if (bs_) {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         ch->id = ++g_channel_count[bs_];
@@ -438,6 +450,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         hip_check(hipIpcGetMemHandle(&h.scratch, c->scratch_), "hipIpcGetMemHandle(scratch)");
         hip_check(hipIpcGetMemHandle(&h.ag, c->scratch_ag_), "hipIpcGetMemHandle(ag)");
         hip_check(hipIpcGetMemHandle(&h.flags, c->flags_), "hipIpcGetMemHandle(flags)");
+        hip_check(hipIpcGetMemHandle(&h.svc, c->ch_->svc_region), "hipIpcGetMemHandle(service)");
     }
     hip_check(hipIpcGetMemHandle(&h.p2p, c->p2p_), "hipIpcGetMemHandle(p2p)");
     std::vector<Handles> hs((size_t)c->n_);
@@ -459,6 +472,11 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
             hip_check(hipIpcOpenMemHandle(&pf, hs[(size_t)p].flags, hipIpcMemLazyEnablePeerAccess),
                       "hipIpcOpenMemHandle(flags)");
             ch->peer_flags[p] = static_cast<uint32_t*>(pf);
+            void* sv = nullptr;
+            hip_check(hipIpcOpenMemHandle(&sv, hs[(size_t)p].svc, hipIpcMemLazyEnablePeerAccess),
+                      "hipIpcOpenMemHandle(service)");
+            ch->peer_svc_region[p] = static_cast<char*>(sv);
+            ch->peer_svc_flags[p] = reinterpret_cast<uint32_t*>(ch->peer_svc_region[p] + (size_t)2 * c->n_ * RDC_SVC_MAX_BYTES);
             ch->ipc = true;
         }
         void* pp = nullptr;
@@ -531,6 +549,8 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
             ci->ch_->peer_scratch[j] = cs[(size_t)j]->scratch_;
             ci->ch_->peer_ag[j] = cs[(size_t)j]->scratch_ag_;
             ci->ch_->peer_flags[j] = cs[(size_t)j]->flags_;
+            ci->ch_->peer_svc_region[j] = cs[(size_t)j]->ch_->svc_region;
+            ci->ch_->peer_svc_flags[j] = cs[(size_t)j]->ch_->svc_flags;
             ci->peer_p2p_[j] = cs[(size_t)j]->p2p_;
             if (devices[i] != devices[j]) {
                 int can = 0;
@@ -1126,6 +1146,34 @@ void Communicator::Allgather(void* const* bufs, const uint64_t* sizes, hipStream
         ++seq_;
         hip_check(launch_allgather(a, p.nb_scatter + p.nb_gather, stream), "launch allgather");
     }
+}
+
+bool Communicator::SmallHostAllreduce(void* host, size_t count, int dtype, int op) {
+    const size_t esz = rdc_dtype_size(dtype);
+    const uint64_t bytes = (uint64_t)count * esz;
+    if (n_ == 1 || bytes == 0 || bytes > RDC_SVC_MAX_BYTES || !ch_ || !ch_->svc_region || !SmallService::Enabled())
+        return false;
+    KernelSet ks;
+    if (!get_kernels(dtype, op, &ks))
+        throw std::invalid_argument("rdc: unsupported (dtype, op) = (" + std::to_string(dtype) + ", " +
+                                    std::to_string(op) + ")");
+    SmallService* svc;
+    {
+        std::lock_guard<std::mutex> lk(ch_->mu);
+        if (!ch_->svc)
+            ch_->svc.reset(new SmallService(rank_, n_, device_, ch_->peer_svc_region, ch_->peer_svc_flags, err_ + 56,
+                                            tree_len_, tree_dst_, tree_src_, cfg_.timeout_s, wall_khz_));
+        svc = ch_->svc.get();
+    }
+    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+    SplitRanges((int64_t)count, n_, cb, ce);  // utils::Split: the ring order of each element
+    uint64_t off[RDC_MAX_RANKS] = {0}, len[RDC_MAX_RANKS] = {0};
+    for (int c = 0; c < n_; ++c) {
+        off[c] = (uint64_t)cb[c] * esz;
+        len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
+    }
+    svc->Allreduce(ks, dtype * 8 + op, static_cast<char*>(host), bytes, off, len, bytes <= cfg_.ring_mincount);
+    return true;
 }
 
 void Communicator::Check(hipStream_t stream) {

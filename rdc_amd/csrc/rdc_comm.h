@@ -48,6 +48,7 @@ struct KernelSet;
 struct P2PCtl;
 class P2PEngine;
 class WorkComp;
+class SmallService;
 
 // The collective state of one set of ranks: the RS / AG scratch regions, the
 // flag array, the device error word and launch counter, and the peers' IPC
@@ -83,6 +84,14 @@ struct Channel {
     char* peer_scratch[RDC_MAX_RANKS] = {};
     char* peer_ag[RDC_MAX_RANKS] = {};
     uint32_t* peer_flags[RDC_MAX_RANKS] = {};
+    // small-allreduce service (rdc_service.h): its own uncached slots
+    // [2][n] x RDC_SVC_MAX_BYTES followed by arrival words [n] per rank (one
+    // allocation), IPC-mapped
+    char* svc_region = nullptr;
+    uint32_t* svc_flags = nullptr;  // = svc_region + 2 n RDC_SVC_MAX_BYTES
+    char* peer_svc_region[RDC_MAX_RANKS] = {};
+    uint32_t* peer_svc_flags[RDC_MAX_RANKS] = {};
+    std::unique_ptr<SmallService> svc;  // started on first use
     std::mutex mu;
     int users = 0;                     // communicators attached
     uint32_t notify_token = 0;
@@ -134,6 +143,10 @@ public:
     uint32_t ArmNotify();
     void WaitNotify(uint32_t token, hipStream_t stream);
     void RaiseIfError(uint32_t e) const;
+    // Synchronous allreduce of a small HOST buffer through the resident
+    // service (rdc_service.h); false if it does not apply (too large,
+    // disabled, world size 1) and the caller takes the launch path.
+    bool SmallHostAllreduce(void* host, size_t count, int dtype, int op);
     // point-to-point (rdc_p2p.h): bytes of buf to / from one peer, matched in
     // order per pair; device copies start after the work queued on `after`
     WorkComp* ISend(const void* buf, size_t bytes, int dest, hipStream_t after);

@@ -108,3 +108,37 @@ struct CollArgs {
                                          //   write-back, rdc_device.h block_publish)
     uint64_t* trace;                     // optional (mesh/ring): per block {start, end} wall_clock64 ticks
 };
+
+// ------------------------------------------------ small-allreduce service --
+// A resident one-block kernel per rank (k_svc) that serves small synchronous
+// HOST-buffer allreduces from a pinned mailbox without a kernel launch per
+// call; it exits after RDC_HOST_SERVICE_IDLE_US of idleness (rdc_service.h).
+#define RDC_SVC_MAX_BYTES (64u << 10)  // largest buffer it serves
+enum { RDC_SVC_NEVER = 0, RDC_SVC_RUNNING = 1, RDC_SVC_EXITING = 2, RDC_SVC_EXITED = 3 };
+
+struct SvcBox {  // pinned, coherent host memory; one per rank
+    alignas(64) uint32_t req;     // host: sequence number of the latest posted request
+    alignas(64) uint32_t done;    // device: last completed request
+    alignas(64) uint32_t state;   // device: RDC_SVC_*
+    alignas(64) uint32_t stop;    // host: exit now
+    alignas(64) uint32_t err;     // device: RDC_KERR_* of a failed request (sticky)
+    alignas(64) uint64_t bytes;   // request: buffer bytes (<= RDC_SVC_MAX_BYTES)
+    uint64_t off[RDC_MAX_RANKS];  // request: Split chunk c = [off[c], off[c]+len[c]) in bytes
+    uint64_t len[RDC_MAX_RANKS];
+    int32_t tree;                 // request: fold in the tree's order (rdc_reduce_ring_mincount)
+    alignas(256) char data[RDC_SVC_MAX_BYTES];  // the rank's input in, the result out
+};
+
+struct SvcArgs {
+    SvcBox* box;                    // device address of this rank's mailbox
+    char* region[RDC_MAX_RANKS];    // rank p's service slots: [2 halves][n] x RDC_SVC_MAX_BYTES (uncached)
+    uint32_t* sflags[RDC_MAX_RANKS];  // rank p's arrival words: [n], word w set by rank w
+    uint32_t* derr;                 // device error word of the service (the mailbox gets a copy)
+    int n, rank;
+    int strict;                     // RDC_STRICT_FENCES: system fence before `done`
+    uint64_t idle_ticks;            // wall_clock64 ticks without a request before exiting
+    uint64_t timeout_ticks;         // waiting for a peer's contribution
+    int tree_len;
+    int8_t tree_dst[RDC_MAX_RANKS];
+    int8_t tree_src[RDC_MAX_RANKS];
+};

@@ -223,6 +223,7 @@ void HostPath::DrainLoop() {
 // error word needs no copy (the kernel mirrors it into pinned memory).
 void HostPath::AllreduceSmall(Communicator* c, char* h, size_t count, size_t S, int dtype, int op,
                               hipStream_t comm_stream) {
+    if (c->SmallHostAllreduce(h, count, dtype, op)) return;  // the resident service (rdc_service.h)
     if (!pin_small_) {
         hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_small_), kSmall + 64, hipHostMallocCoherent),
                   "hipHostMalloc");

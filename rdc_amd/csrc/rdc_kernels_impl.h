@@ -425,11 +425,26 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
 // slot (seq parity): a peer can be at most one launch ahead, so it never
 // overwrites the half a slower rank is still folding.
 
+// What a one-shot / tree fold reads and writes: this rank's values `own`
+// (overwritten with the result), rank q's copy at slots + q * slot_bytes, and
+// the tree program.  Built from CollArgs by the collective kernels and from
+// SvcArgs by the small-allreduce service (k_svc).
+struct FoldView {
+    int n, r;
+    char* own;
+    const char* slots;
+    uint64_t slot_bytes;
+    int tree_len;
+    const int8_t* tree_dst;
+    const int8_t* tree_src;
+};
+
 // fold bytes [lo, hi) of the buffer, all inside chunk c
 template <int OP, typename T, int NMAX>
-__device__ void oneshot_fold_range(const CollArgs& a, int c, const char* slots, uint64_t lo, uint64_t hi) {
-    const int n = a.n, r = a.rank;
-    char* own = a.user;
+__device__ void oneshot_fold_range(const FoldView& a, int c, uint64_t lo, uint64_t hi) {
+    const int n = a.n, r = a.r;
+    char* own = a.own;
+    const char* slots = a.slots;
     const unsigned tid = threadIdx.x;
     auto src = [&](int q) -> const char* { return q == r ? (const char*)own : slots + (uint64_t)q * a.slot_bytes; };
     auto fold_elem = [&](uint64_t x) {
@@ -498,9 +513,10 @@ __device__ __forceinline__ void tree_put(V (&v)[NMAX], int i, V x) {
 }
 
 template <int OP, typename T, int NMAX>
-__device__ void tree_fold_range(const CollArgs& a, const char* slots, uint64_t lo, uint64_t hi) {
-    const int n = a.n, r = a.rank;
-    char* own = a.user;
+__device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
+    const int n = a.n, r = a.r;
+    char* own = a.own;
+    const char* slots = a.slots;
     const unsigned tid = threadIdx.x;
     auto src = [&](int q) -> const char* { return q == r ? (const char*)own : slots + (uint64_t)q * a.slot_bytes; };
     auto fold_elem = [&](uint64_t x) {
@@ -565,7 +581,7 @@ __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
         __syncthreads();
     }
     // 2) fold my tiles once every peer's copy landed
-    const char* slots = a.rs[r] + half;
+    const FoldView fv{n, r, a.user, a.rs[r] + half, a.slot_bytes, a.tree_len, a.tree_dst, a.tree_src};
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         if (threadIdx.x < (unsigned)(n - 1))
             s_flags[threadIdx.x] = a.flags[r] + (uint64_t)((r + 1 + threadIdx.x) % n) * a.max_tiles + t;
@@ -574,13 +590,13 @@ __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
         const uint64_t lo = (uint64_t)t * a.tile_bytes;
         const uint64_t hi = lo + a.tile_bytes < total ? lo + a.tile_bytes : total;
         if (TREE) {
-            tree_fold_range<OP, T, NMAX>(a, slots, lo, hi);
+            tree_fold_range<OP, T, NMAX>(fv, lo, hi);
         } else {
             for (int c = 0; c < n; ++c) {
                 if (a.len[c] == 0) continue;
                 const uint64_t clo = a.off[c] > lo ? a.off[c] : lo;
                 const uint64_t chi = a.off[c] + a.len[c] < hi ? a.off[c] + a.len[c] : hi;
-                if (clo < chi) oneshot_fold_range<OP, T, NMAX>(a, c, slots, clo, chi);
+                if (clo < chi) oneshot_fold_range<OP, T, NMAX>(fv, c, clo, chi);
             }
         }
         __syncthreads();
@@ -742,6 +758,122 @@ __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
     launch_done(a, seq);
 }
 
+
+// ================================================ small-allreduce service ===
+// One block per rank, resident while requests keep coming (rdc_service.h).
+// Request k: copy the mailbox input into this rank's own slot of half k&1,
+// push it into every peer's slot [k&1][rank] (uncached), publish an arrival
+// word per peer, wait for the n-1 peers' words, fold every element in its
+// Split chunk's ring order (or the tree's order) exactly as the one-shot
+// does, and copy the result back into the mailbox; then `done` = k.  A rank
+// is at most one request ahead of any peer (it cannot finish k+1 before every
+// peer has sent k+1, i.e. finished k), so the two halves never collide.
+// Exit conditions, all reached by the one block: `stop` set by the host,
+// RDC_HOST_SERVICE_IDLE_US without a request (state EXITING, one more look
+// at `req` so a request posted meanwhile is served), or a peer that never
+// arrives (error, exit).
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int OP, typename T, int NMAX>
+__global__ __launch_bounds__(kBlock) void k_svc(SvcArgs a) {
+    const int n = a.n, r = a.rank;
+    SvcBox* box = a.box;
+    __shared__ uint32_t s_next;
+    __shared__ int s_go, s_tree;
+    __shared__ uint64_t s_bytes, s_off[RDC_MAX_RANKS], s_len[RDC_MAX_RANKS];
+    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
+    if (threadIdx.x == 0) {
+        s_next = sys_load(&box->done) + 1u;
+        sys_store(&box->state, RDC_SVC_RUNNING);
+    }
+    __syncthreads();
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const uint32_t next = s_next;
+            const uint64_t t0 = wall_clock64();
+            int go = 0;
+            for (;;) {
+                if (seq_reached(sys_load(&box->req), next)) {
+                    go = 1;
+                    break;
+                }
+                if (sys_load(&box->stop)) break;
+                if (wall_clock64() - t0 > a.idle_ticks) {
+                    sys_store(&box->state, RDC_SVC_EXITING);
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+                    if (seq_reached(sys_load(&box->req), next)) {  // posted while we were leaving
+                        sys_store(&box->state, RDC_SVC_RUNNING);
+                        go = 1;
+                    }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_go = go;
+            if (go) {  // the request, read once behind the acquire of `req`
+                s_bytes = __hip_atomic_load(&box->bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                s_tree = box->tree;
+                for (int c = 0; c < n; ++c) {
+                    s_off[c] = box->off[c];
+                    s_len[c] = box->len[c];
+                }
+            }
+        }
+        __syncthreads();
+        if (!s_go) break;
+        const uint32_t next = s_next;
+        const uint64_t bytes = s_bytes;
+        const uint64_t half = (uint64_t)(next & 1u) * (uint64_t)n * RDC_SVC_MAX_BYTES;
+        char* own = a.region[r] + half + (uint64_t)r * RDC_SVC_MAX_BYTES;
+        block_copy(own, box->data, bytes);  // one PCIe read of the input
+        __syncthreads();
+        for (int k = 1; k < n; ++k)
+            block_copy(a.region[(r + k) % n] + half + (uint64_t)r * RDC_SVC_MAX_BYTES, own, bytes);
+        if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.sflags[(r + 1 + threadIdx.x) % n] + r;
+        block_publish(s_flags, n - 1, next, 1);
+        __syncthreads();
+        if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.sflags[r] + (r + 1 + threadIdx.x) % n;
+        __syncthreads();
+        const Abort ab{a.derr, wall_clock64() + a.timeout_ticks};
+        if (!block_wait(s_flags, n - 1, next, ab, RDC_KERR_TIMEOUT_RS, 1)) {
+            if (threadIdx.x == 0) {
+                sys_store(&box->err, __hip_atomic_load(a.derr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                sys_store(&box->done, next);  // the host reads err
+            }
+            break;
+        }
+        const FoldView fv{n, r, own, a.region[r] + half, RDC_SVC_MAX_BYTES, a.tree_len, a.tree_dst, a.tree_src};
+        if (s_tree) {
+            tree_fold_range<OP, T, NMAX>(fv, 0, bytes);
+        } else {
+            for (int c = 0; c < n; ++c) {
+                const uint64_t lo = s_off[c], len = s_len[c];
+                if (len) oneshot_fold_range<OP, T, NMAX>(fv, c, lo, lo + len);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        block_copy(box->data, own, bytes);  // the result back over PCIe
+        // the mailbox is coherent (uncached) host memory: once every wave's
+        // stores are performed, the `done` write — posted on the same PCIe
+        // path after them — cannot pass them
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (a.strict) __threadfence_system();
+            __hip_atomic_store(&box->done, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_next = next + 1u;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) sys_store(&box->state, RDC_SVC_EXITED);
+}
+
 // ============================================================ dispatch ===
 template <int OP, typename T>
 struct Kernels {
@@ -770,6 +902,13 @@ struct Kernels {
     }
     static hipError_t ring(const CollArgs& a, int grid, hipStream_t s) {
         hipLaunchKernelGGL((k_ring<OP, T>), dim3(grid), dim3(kBlock), 0, s, a);
+        return hipGetLastError();
+    }
+    static hipError_t svc(const SvcArgs& a, hipStream_t s) {
+        if (a.n <= 8)
+            hipLaunchKernelGGL((k_svc<OP, T, 8>), dim3(1), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_svc<OP, T, 16>), dim3(1), dim3(kBlock), 0, s, a);
         return hipGetLastError();
     }
     static hipError_t tree(const CollArgs& a, int grid, hipStream_t s) {
@@ -815,6 +954,7 @@ struct Kernels {
     ks->ring = &Kernels<OP, T>::ring;     \
     ks->oneshot = &Kernels<OP, T>::oneshot; \
     ks->tree = &Kernels<OP, T>::tree;       \
+    ks->svc = &Kernels<OP, T>::svc;         \
     ks->occupancy = &Kernels<OP, T>::occupancy; \
     return true;
 

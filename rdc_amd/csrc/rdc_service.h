@@ -1,0 +1,63 @@
+// Small-allreduce service: synchronous allreduces of small HOST buffers (the
+// reference's own setting, rdc/core.py:172-217 — BASELINE cfg1 is a 4 KiB
+// fp32 allreduce) without a kernel launch per call.
+//
+// A launch-per-call path pays the host launch, the GPU dispatch and the
+// kernel's completion before the caller sees its result (DESIGN.md §5.3:
+// 14.6 us for a 4 KiB allreduce of device memory at n = 2, 17.4 us from host
+// memory).  Here each rank keeps ONE resident block (k_svc) while calls keep
+// coming: the host copies its input into a pinned mailbox and bumps `req`;
+// the block, polling the mailbox, pushes the input into every peer's service
+// slot over xGMI, waits for the peers' arrival words, folds every element in
+// the reference's order (Split chunk ring order, or the tree's order below
+// rdc_reduce_ring_mincount — the one-shot's fold code) and writes the result
+// back into the mailbox.
+//
+// The block exits after RDC_HOST_SERVICE_IDLE_US (default 1000) without a
+// request, when the host sets `stop` (another (dtype, op), teardown) or when
+// a peer never arrives (RDC_TIMEOUT): nothing stays resident, and a
+// device-wide synchronisation waits at most the idle time.  The next call
+// relaunches it.  Its slots and arrival words are its own (not the channel's
+// scratch), so it never races the channel's stream-ordered launches.
+// RDC_HOST_SERVICE=0 disables it.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <mutex>
+
+#include "rdc_common.h"
+#include "rdc_kernels.h"
+
+namespace rdc_amd {
+
+class SmallService {
+public:
+    // region / sflags: every rank's service slots and arrival words (peers'
+    // IPC-mapped or direct); derr: a device word for the kernel's errors
+    SmallService(int rank, int n, int device, char* const* region, uint32_t* const* sflags, uint32_t* derr,
+                 int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz);
+    ~SmallService();
+    static bool Enabled();
+    // in place on `host` (bytes <= RDC_SVC_MAX_BYTES); off/len: the Split
+    // chunks in bytes; tree: fold in the tree's order.  Synchronous; throws
+    // on a device-side failure (the service is then unusable).
+    void Allreduce(const KernelSet& ks, int kind, char* host, uint64_t bytes, const uint64_t* off,
+                   const uint64_t* len, bool tree);
+
+private:
+    void Stop();
+    void EnsureRunning(const KernelSet& ks, int kind);
+
+    int rank_, n_, device_;
+    double timeout_s_;
+    SvcArgs args_;
+    SvcBox* box_ = nullptr;       // host address
+    hipStream_t stream_ = nullptr;
+    int kind_ = -1;               // (dtype, op) of the kernel launched last, -1 none
+    bool launched_ = false;
+    bool broken_ = false;
+    uint32_t req_ = 0;
+    std::mutex mu_;
+};
+
+}  // namespace rdc_amd

@@ -64,6 +64,32 @@ def main():
             np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
             print("rank %d case %d ok" % (rank, i), flush=True)
             continue
+        if kind == "host_mix":
+            # small synchronous HOST allreduces through the resident service
+            # (rdc_service.h): (dtype, op) switches relaunch it, sleeps longer
+            # than its idle time let it exit between calls, device-resident
+            # collectives run in between; every result saved
+            import time as _time
+            outs = []
+            dev = torch.zeros(20011, dtype=torch.float32, device="cuda")
+            for j, (cnt, dt, op, sleep_ms) in enumerate(c["ops"]):
+                t = torch.zeros(cnt * esz[dt] + 16, dtype=torch.uint8, device="cuda")
+                check_call(_LIB.RdcFill(ctypes.c_void_p(t.data_ptr()), cnt, dt, 0x5EED6000 + j, rank, sp))
+                torch.cuda.synchronize()
+                h = t[: cnt * esz[dt]].cpu().numpy().copy()
+                if sleep_ms:
+                    _time.sleep(sleep_ms / 1000.0)
+                check_call(_LIB.RdcAllreduce(ctypes.c_void_p(h.ctypes.data), cnt, dt, op, None, None))
+                outs.append(h)
+                if j % 3 == 2:  # a device collective between service calls
+                    check_call(_LIB.RdcFill(ctypes.c_void_p(dev.data_ptr()), dev.numel(), 6, 0x5EED6500 + j, rank, sp))
+                    check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(dev.data_ptr()), dev.numel(), 6,
+                                                       2, 0, sp))
+                    comm.check(sp)
+                    outs.append(dev.cpu().numpy().view(np.uint8).copy())
+            np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), np.concatenate(outs))
+            print("rank %d case %d ok" % (rank, i), flush=True)
+            continue
         if kind == "shared_comms":
             # named communicators over the same ranks share one scratch channel:
             # memory cost, and launches of different communicators issued on

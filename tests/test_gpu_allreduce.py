@@ -403,6 +403,44 @@ def test_mp_tree_path_ring_mincount(world):
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (world, i, c, r)
 
 
+HOST_MIX = [(1024, 6, 2, 0), (1024, 6, 2, 0), (1, 6, 2, 0), (16384, 6, 2, 0), (3, 2, 0, 0), (4099, 10, 2, 0),
+            (777, 7, 1, 5), (1024, 6, 2, 0), (8, 0, 3, 3), (5000, 11, 2, 0), (1024, 6, 2, 4), (12345, 1, 2, 0)]
+
+
+def expected_host_mix(world, mincount=1):
+    out = []
+    for j, (cnt, dt, op, _) in enumerate(HOST_MIX):
+        xs = [O.fill(cnt, dt, 0x5EED6000 + j, r) for r in range(world)]
+        esz = np.dtype(O.NP_DTYPE[dt]).itemsize
+        (O.allreduce_tree if cnt * esz <= mincount else O.allreduce_ring)(xs, dt, op)
+        out.append([x.view(np.uint8) for x in xs])
+        if j % 3 == 2:
+            d = [O.fill(20011, 6, 0x5EED6500 + j, r) for r in range(world)]
+            O.allreduce_ring(d, 6, 2)
+            out.append([x.view(np.uint8) for x in d])
+    return [np.concatenate([o[r] for o in out]) for r in range(world)]
+
+
+@pytest.mark.parametrize("world,env", [(2, {}), (3, {"rdc_reduce_ring_mincount": "8K"}), (2, {"RDC_HOST_SERVICE": "0"}),
+                                       (4, {"RDC_HOST_SERVICE_IDLE_US": "50"})])
+def test_mp_host_small_service(world, env):
+    """Small synchronous HOST allreduces (cfg1's path) through the resident
+    service block (rdc_service.h): 12 calls of 1 B - 64 KiB over 8 (dtype, op)
+    pairs (each switch restarts the kernel), sleeps of 3-5 ms longer than its
+    idle time (it exits and is relaunched), device collectives in between,
+    the tree order below rdc_reduce_ring_mincount; and the launch path with
+    RDC_HOST_SERVICE=0.  Every result bit-exact against the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [{"count": 0, "dtype": 6, "op": 2, "kind": "host_mix", "ops": HOST_MIX}]
+    tmp = run_mp(world, cases, env_extra=env)
+    mincount = 8 << 10 if "rdc_reduce_ring_mincount" in env else 1
+    want = expected_host_mix(world, mincount)
+    for r in range(world):
+        got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
+        assert got.tobytes() == want[r].tobytes(), r
+
+
 def test_mp_named_communicators_share_scratch():
     """Every named communicator over the same ranks shares ONE scratch channel
     (4080 MiB by default, not 4080 MiB per communicator): two more
