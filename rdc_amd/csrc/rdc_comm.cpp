@@ -1165,14 +1165,12 @@ bool Communicator::SmallHostAllreduce(void* host, size_t count, int dtype, int o
                                             tree_len_, tree_dst_, tree_src_, cfg_.timeout_s, wall_khz_));
         svc = ch_->svc.get();
     }
-    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
-    SplitRanges((int64_t)count, n_, cb, ce);  // utils::Split: the ring order of each element
-    uint64_t off[RDC_MAX_RANKS] = {0}, len[RDC_MAX_RANKS] = {0};
-    for (int c = 0; c < n_; ++c) {
-        off[c] = (uint64_t)cb[c] * esz;
-        len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
-    }
-    svc->Allreduce(ks, dtype * 8 + op, static_cast<char*>(host), bytes, off, len, bytes <= cfg_.ring_mincount);
+    // every rank allocates the same way on one machine image; a rank without
+    // the uncached mailbox would leave its peers waiting, so that is an error
+    if (!svc->Usable())
+        throw std::runtime_error("rdc: small-allreduce service mailbox (hipHostMallocUncached) unavailable; "
+                                 "set RDC_HOST_SERVICE=0 on every rank");
+    svc->Allreduce(ks, dtype * 8 + op, static_cast<char*>(host), bytes, bytes <= cfg_.ring_mincount);
     return true;
 }
 

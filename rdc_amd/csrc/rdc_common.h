@@ -116,16 +116,12 @@ struct CollArgs {
 #define RDC_SVC_MAX_BYTES (64u << 10)  // largest buffer it serves
 enum { RDC_SVC_NEVER = 0, RDC_SVC_RUNNING = 1, RDC_SVC_EXITING = 2, RDC_SVC_EXITED = 3 };
 
-struct SvcBox {  // pinned, coherent host memory; one per rank
-    alignas(64) uint32_t req;     // host: sequence number of the latest posted request
+struct SvcBox {  // pinned host memory, hipHostMallocUncached; one per rank
+    alignas(64) uint64_t req;     // host: (seq << 32) | tree << 31 | bytes — the whole request in one word
     alignas(64) uint32_t done;    // device: last completed request
     alignas(64) uint32_t state;   // device: RDC_SVC_*
     alignas(64) uint32_t stop;    // host: exit now
     alignas(64) uint32_t err;     // device: RDC_KERR_* of a failed request (sticky)
-    alignas(64) uint64_t bytes;   // request: buffer bytes (<= RDC_SVC_MAX_BYTES)
-    uint64_t off[RDC_MAX_RANKS];  // request: Split chunk c = [off[c], off[c]+len[c]) in bytes
-    uint64_t len[RDC_MAX_RANKS];
-    int32_t tree;                 // request: fold in the tree's order (rdc_reduce_ring_mincount)
     alignas(256) char data[RDC_SVC_MAX_BYTES];  // the rank's input in, the result out
 };
 

@@ -425,13 +425,14 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
 // slot (seq parity): a peer can be at most one launch ahead, so it never
 // overwrites the half a slower rank is still folding.
 
-// What a one-shot / tree fold reads and writes: this rank's values `own`
-// (overwritten with the result), rank q's copy at slots + q * slot_bytes, and
-// the tree program.  Built from CollArgs by the collective kernels and from
-// SvcArgs by the small-allreduce service (k_svc).
+// What a one-shot / tree fold reads and writes: this rank's values `own`,
+// rank q's copy at slots + q * slot_bytes, the tree program, and where the
+// result goes (`out`: `own` itself for the collective kernels, the host
+// mailbox for the small-allreduce service k_svc).
 struct FoldView {
     int n, r;
-    char* own;
+    const char* own;
+    char* out;
     const char* slots;
     uint64_t slot_bytes;
     int tree_len;
@@ -443,16 +444,17 @@ struct FoldView {
 template <int OP, typename T, int NMAX>
 __device__ void oneshot_fold_range(const FoldView& a, int c, uint64_t lo, uint64_t hi) {
     const int n = a.n, r = a.r;
-    char* own = a.own;
+    const char* own = a.own;
+    char* out = a.out;
     const char* slots = a.slots;
     const unsigned tid = threadIdx.x;
-    auto src = [&](int q) -> const char* { return q == r ? (const char*)own : slots + (uint64_t)q * a.slot_bytes; };
+    auto src = [&](int q) -> const char* { return q == r ? own : slots + (uint64_t)q * a.slot_bytes; };
     auto fold_elem = [&](uint64_t x) {
         T acc = *reinterpret_cast<const T*>(src((c - 1 + n) % n) + x);
         for (int k = 2; k <= n; ++k) acc = OpF<OP>::apply(*reinterpret_cast<const T*>(src((c - k + n) % n) + x), acc);
-        *reinterpret_cast<T*>(own + x) = acc;
+        *reinterpret_cast<T*>(out + x) = acc;
     };
-    if ((((uintptr_t)own ^ (uintptr_t)slots) & 15) != 0) {  // this rank's buffer is not 16-B aligned
+    if (((((uintptr_t)own ^ (uintptr_t)slots) | ((uintptr_t)out ^ (uintptr_t)slots)) & 15) != 0) {  // not 16-B aligned
         for (uint64_t x = lo + (uint64_t)tid * sizeof(T); x < hi; x += (uint64_t)kBlock * sizeof(T)) fold_elem(x);
         return;
     }
@@ -486,7 +488,7 @@ __device__ void oneshot_fold_range(const FoldView& a, int c, uint64_t lo, uint64
 #pragma unroll
             for (int k = 2; k <= NMAX; ++k)
                 if (k <= n) acc = reduce16<OP, T>(v[u][k - 1], acc);
-            st16(own + vlo + (i + u * kBlock) * 16, acc);
+            st16(out + vlo + (i + u * kBlock) * 16, acc);
         }
     }
 }
@@ -515,10 +517,11 @@ __device__ __forceinline__ void tree_put(V (&v)[NMAX], int i, V x) {
 template <int OP, typename T, int NMAX>
 __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
     const int n = a.n, r = a.r;
-    char* own = a.own;
+    const char* own = a.own;
+    char* out = a.out;
     const char* slots = a.slots;
     const unsigned tid = threadIdx.x;
-    auto src = [&](int q) -> const char* { return q == r ? (const char*)own : slots + (uint64_t)q * a.slot_bytes; };
+    auto src = [&](int q) -> const char* { return q == r ? own : slots + (uint64_t)q * a.slot_bytes; };
     auto fold_elem = [&](uint64_t x) {
         T v[NMAX];
 #pragma unroll
@@ -530,9 +533,9 @@ __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
                 const int d = a.tree_dst[i], s = a.tree_src[i];
                 tree_put<NMAX, T>(v, d, OpF<OP>::apply(tree_pick<NMAX, T>(v, d), tree_pick<NMAX, T>(v, s)));
             }
-        *reinterpret_cast<T*>(own + x) = v[0];
+        *reinterpret_cast<T*>(out + x) = v[0];
     };
-    if ((((uintptr_t)own ^ (uintptr_t)slots) & 15) != 0) {  // this rank's buffer is not 16-B aligned
+    if (((((uintptr_t)own ^ (uintptr_t)slots) | ((uintptr_t)out ^ (uintptr_t)slots)) & 15) != 0) {  // not 16-B aligned
         for (uint64_t x = lo + (uint64_t)tid * sizeof(T); x < hi; x += (uint64_t)kBlock * sizeof(T)) fold_elem(x);
         return;
     }
@@ -556,7 +559,7 @@ __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
                 const int d = a.tree_dst[j], s = a.tree_src[j];
                 tree_put<NMAX, v4u>(v, d, reduce16<OP, T>(tree_pick<NMAX, v4u>(v, d), tree_pick<NMAX, v4u>(v, s)));
             }
-        st16(own + vlo + i * 16, v[0]);
+        st16(out + vlo + i * 16, v[0]);
     }
 }
 
@@ -581,7 +584,7 @@ __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
         __syncthreads();
     }
     // 2) fold my tiles once every peer's copy landed
-    const FoldView fv{n, r, a.user, a.rs[r] + half, a.slot_bytes, a.tree_len, a.tree_dst, a.tree_src};
+    const FoldView fv{n, r, a.user, a.user, a.rs[r] + half, a.slot_bytes, a.tree_len, a.tree_dst, a.tree_src};
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         if (threadIdx.x < (unsigned)(n - 1))
             s_flags[threadIdx.x] = a.flags[r] + (uint64_t)((r + 1 + threadIdx.x) % n) * a.max_tiles + t;
@@ -772,11 +775,38 @@ __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
 // RDC_HOST_SERVICE_IDLE_US without a request (state EXITING, one more look
 // at `req` so a request posted meanwhile is served), or a peer that never
 // arrives (error, exit).
-__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+// The mailbox is pinned host memory allocated hipHostMallocUncached (MTYPE
+// UC: no GPU cache holds it), so plain loads read what the host wrote last and
+// plain stores are performed at host memory once `s_waitcnt vmcnt(0)` returns
+// (measured: with the default, L2-cacheable host memory the result stores
+// stayed in L2 and the host read its own input back).  Control words are
+// still system-coherent relaxed atomics; no acquire / release fence (an L2
+// invalidate / write-back) on the request path.
+__device__ __forceinline__ uint32_t box_load(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint64_t box_load64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void box_store(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// src[0, bytes) read once (16-byte lanes, rounded up: both sides are 64 KiB
+// areas aligned to 256 B) and stored to every dst[k], k < ndst
+__device__ __forceinline__ void block_scatter(char* const* dst, int ndst, const char* src, uint64_t bytes) {
+    const uint64_t nvec = (bytes + 15) >> 4;
+    constexpr int U = 4;
+    for (uint64_t i = threadIdx.x; i < nvec; i += U * kBlock) {
+        v4u v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i + u * kBlock < nvec) v[u] = ld16_nt(src + (i + u * kBlock) * 16);
+        for (int k = 0; k < ndst; ++k)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (i + u * kBlock < nvec) st16_nt(dst[k] + (i + u * kBlock) * 16, v[u]);
+    }
 }
 
 template <int OP, typename T, int NMAX>
@@ -784,12 +814,13 @@ __global__ __launch_bounds__(kBlock) void k_svc(SvcArgs a) {
     const int n = a.n, r = a.rank;
     SvcBox* box = a.box;
     __shared__ uint32_t s_next;
-    __shared__ int s_go, s_tree;
-    __shared__ uint64_t s_bytes, s_off[RDC_MAX_RANKS], s_len[RDC_MAX_RANKS];
+    __shared__ int s_go;
+    __shared__ uint64_t s_req;
     __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
+    __shared__ char* s_dst[RDC_MAX_RANKS];
     if (threadIdx.x == 0) {
-        s_next = sys_load(&box->done) + 1u;
-        sys_store(&box->state, RDC_SVC_RUNNING);
+        s_next = box_load(&box->done) + 1u;
+        box_store(&box->state, RDC_SVC_RUNNING);
     }
     __syncthreads();
     for (;;) {
@@ -797,81 +828,81 @@ __global__ __launch_bounds__(kBlock) void k_svc(SvcArgs a) {
             const uint32_t next = s_next;
             const uint64_t t0 = wall_clock64();
             int go = 0;
+            uint64_t q = 0;
             for (;;) {
-                if (seq_reached(sys_load(&box->req), next)) {
+                q = box_load64(&box->req);  // (seq << 32) | tree << 31 | bytes: one word, one PCIe read
+                if (seq_reached((uint32_t)(q >> 32), next)) {
                     go = 1;
                     break;
                 }
-                if (sys_load(&box->stop)) break;
+                if (box_load(&box->stop)) break;
                 if (wall_clock64() - t0 > a.idle_ticks) {
-                    sys_store(&box->state, RDC_SVC_EXITING);
+                    // leaving: EXITING, then one more look at `req` (the host
+                    // posts `req` and then reads `state`; seq_cst on both sides)
+                    box_store(&box->state, RDC_SVC_EXITING);
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-                    if (seq_reached(sys_load(&box->req), next)) {  // posted while we were leaving
-                        sys_store(&box->state, RDC_SVC_RUNNING);
+                    q = box_load64(&box->req);
+                    if (seq_reached((uint32_t)(q >> 32), next)) {
+                        box_store(&box->state, RDC_SVC_RUNNING);
                         go = 1;
                     }
                     break;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_s_sleep(1);
             }
             s_go = go;
-            if (go) {  // the request, read once behind the acquire of `req`
-                s_bytes = __hip_atomic_load(&box->bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s_tree = box->tree;
-                for (int c = 0; c < n; ++c) {
-                    s_off[c] = box->off[c];
-                    s_len[c] = box->len[c];
-                }
-            }
+            s_req = q;
         }
         __syncthreads();
         if (!s_go) break;
         const uint32_t next = s_next;
-        const uint64_t bytes = s_bytes;
+        const uint64_t bytes = s_req & 0x7fffffffu;
+        const bool tree = (s_req >> 31) & 1u;
         const uint64_t half = (uint64_t)(next & 1u) * (uint64_t)n * RDC_SVC_MAX_BYTES;
         char* own = a.region[r] + half + (uint64_t)r * RDC_SVC_MAX_BYTES;
-        block_copy(own, box->data, bytes);  // one PCIe read of the input
-        __syncthreads();
-        for (int k = 1; k < n; ++k)
-            block_copy(a.region[(r + k) % n] + half + (uint64_t)r * RDC_SVC_MAX_BYTES, own, bytes);
+        // 1) the input, read once over PCIe, into slot r of every rank's half
+        if (threadIdx.x < (unsigned)n) s_dst[threadIdx.x] = a.region[(r + threadIdx.x) % n] + half + (uint64_t)r * RDC_SVC_MAX_BYTES;
         if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.sflags[(r + 1 + threadIdx.x) % n] + r;
+        __syncthreads();
+        block_scatter(s_dst, n, box->data, bytes);
         block_publish(s_flags, n - 1, next, 1);
         __syncthreads();
+        // 2) every peer's copy
         if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.sflags[r] + (r + 1 + threadIdx.x) % n;
         __syncthreads();
         const Abort ab{a.derr, wall_clock64() + a.timeout_ticks};
         if (!block_wait(s_flags, n - 1, next, ab, RDC_KERR_TIMEOUT_RS, 1)) {
             if (threadIdx.x == 0) {
-                sys_store(&box->err, __hip_atomic_load(a.derr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                sys_store(&box->done, next);  // the host reads err
+                box_store(&box->err, __hip_atomic_load(a.derr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                box_store(&box->done, next);  // the host reads err
             }
             break;
         }
-        const FoldView fv{n, r, own, a.region[r] + half, RDC_SVC_MAX_BYTES, a.tree_len, a.tree_dst, a.tree_src};
-        if (s_tree) {
+        // 3) fold in the reference's order, straight into the mailbox
+        const FoldView fv{n, r, own, box->data, a.region[r] + half, RDC_SVC_MAX_BYTES, a.tree_len, a.tree_dst,
+                          a.tree_src};
+        if (tree) {
             tree_fold_range<OP, T, NMAX>(fv, 0, bytes);
-        } else {
+        } else {  // utils::Split chunks (rdc_plan.cpp SplitRanges), in bytes
+            const uint64_t count = bytes / sizeof(T), k = count / (uint64_t)n, m = count % (uint64_t)n;
             for (int c = 0; c < n; ++c) {
-                const uint64_t lo = s_off[c], len = s_len[c];
-                if (len) oneshot_fold_range<OP, T, NMAX>(fv, c, lo, lo + len);
+                const uint64_t b = (uint64_t)c * k + ((uint64_t)c < m ? (uint64_t)c : m);
+                const uint64_t e = (uint64_t)(c + 1) * k + ((uint64_t)(c + 1) < m ? (uint64_t)(c + 1) : m);
+                if (e > b) oneshot_fold_range<OP, T, NMAX>(fv, c, b * sizeof(T), e * sizeof(T));
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        block_copy(box->data, own, bytes);  // the result back over PCIe
-        // the mailbox is coherent (uncached) host memory: once every wave's
-        // stores are performed, the `done` write — posted on the same PCIe
-        // path after them — cannot pass them
+        // every wave's result stores performed at host memory before `done`
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
             if (a.strict) __threadfence_system();
-            __hip_atomic_store(&box->done, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            box_store(&box->done, next);
             s_next = next + 1u;
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) sys_store(&box->state, RDC_SVC_EXITED);
+    if (threadIdx.x == 0) box_store(&box->state, RDC_SVC_EXITED);
 }
 
 // ============================================================ dispatch ===

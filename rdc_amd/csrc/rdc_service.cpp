@@ -32,7 +32,7 @@ bool SmallService::Enabled() {
 
 SmallService::SmallService(int rank, int n, int device, char* const* region, uint32_t* const* sflags, uint32_t* derr,
                            int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz)
-    : rank_(rank), n_(n), device_(device), timeout_s_(timeout_s) {
+    : rank_(rank), device_(device), timeout_s_(timeout_s) {
     memset(&args_, 0, sizeof(args_));
     for (int p = 0; p < n; ++p) {
         args_.region[p] = region[p];
@@ -50,13 +50,22 @@ SmallService::SmallService(int rank, int n, int device, char* const* region, uin
         args_.tree_src[i] = (int8_t)tree_src[i];
     }
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    hip_check(hipHostMalloc(reinterpret_cast<void**>(&box_), sizeof(SvcBox), hipHostMallocCoherent), "mailbox");
+    // MTYPE UC host memory: the kernel's plain loads and stores of `data` bypass
+    // every GPU cache (k_svc); without it there is no service
+    if (hipHostMalloc(reinterpret_cast<void**>(&box_), sizeof(SvcBox), hipHostMallocUncached | hipHostMallocMapped) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        box_ = nullptr;
+        return;
+    }
     memset(static_cast<void*>(box_), 0, sizeof(SvcBox));
     void* d = nullptr;
     hip_check(hipHostGetDevicePointer(&d, box_, 0), "mailbox device address");
     args_.box = static_cast<SvcBox*>(d);
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "service stream");
 }
+
+bool SmallService::Usable() const { return box_ != nullptr; }
 
 SmallService::~SmallService() {
     try {
@@ -96,22 +105,16 @@ void SmallService::EnsureRunning(const KernelSet& ks, int kind) {
     kind_ = kind;
 }
 
-void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t bytes, const uint64_t* off,
-                             const uint64_t* len, bool tree) {
+void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t bytes, bool tree) {
     std::lock_guard<std::mutex> lk(mu_);
     if (broken_) throw std::runtime_error("rdc service: unusable after an earlier failure");
     if (bytes > RDC_SVC_MAX_BYTES) throw std::logic_error("rdc service: buffer too large");
     hip_check(hipSetDevice(device_), "hipSetDevice");
     if (launched_ && kind != kind_) Stop();  // another (dtype, op) needs another kernel
     memcpy(box_->data, host, bytes);
-    box_->bytes = bytes;
-    box_->tree = tree ? 1 : 0;
-    for (int c = 0; c < n_; ++c) {
-        box_->off[c] = off[c];
-        box_->len[c] = len[c];
-    }
     const uint32_t r = ++req_;
-    host_store(&box_->req, r);  // after the request's fields (x86 stores stay in order)
+    // the whole request in one word, stored after the data (x86 stores stay in order)
+    __atomic_store_n(&box_->req, ((uint64_t)r << 32) | (tree ? 1ull << 31 : 0ull) | bytes, __ATOMIC_SEQ_CST);
     EnsureRunning(ks, kind);
     const auto t0 = std::chrono::steady_clock::now();
     const double limit = timeout_s_ * 2 + 10;

@@ -6,12 +6,13 @@
 // kernel's completion before the caller sees its result (DESIGN.md §5.3:
 // 14.6 us for a 4 KiB allreduce of device memory at n = 2, 17.4 us from host
 // memory).  Here each rank keeps ONE resident block (k_svc) while calls keep
-// coming: the host copies its input into a pinned mailbox and bumps `req`;
-// the block, polling the mailbox, pushes the input into every peer's service
-// slot over xGMI, waits for the peers' arrival words, folds every element in
-// the reference's order (Split chunk ring order, or the tree's order below
-// rdc_reduce_ring_mincount — the one-shot's fold code) and writes the result
-// back into the mailbox.
+// coming: the host copies its input into a pinned, GPU-uncached mailbox and
+// posts one request word (seq, bytes, tree); the block, polling that word,
+// reads the input once over PCIe and stores it into its slot of every rank's
+// service region (xGMI), waits for the peers' arrival words, folds every
+// element in the reference's order (Split chunk ring order, or the tree's
+// order below rdc_reduce_ring_mincount — the one-shot's fold code) straight
+// into the mailbox and bumps `done`.
 //
 // The block exits after RDC_HOST_SERVICE_IDLE_US (default 1000) without a
 // request, when the host sets `stop` (another (dtype, op), teardown) or when
@@ -38,17 +39,18 @@ public:
                  int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz);
     ~SmallService();
     static bool Enabled();
-    // in place on `host` (bytes <= RDC_SVC_MAX_BYTES); off/len: the Split
-    // chunks in bytes; tree: fold in the tree's order.  Synchronous; throws
-    // on a device-side failure (the service is then unusable).
-    void Allreduce(const KernelSet& ks, int kind, char* host, uint64_t bytes, const uint64_t* off,
-                   const uint64_t* len, bool tree);
+    // false when the uncached mailbox could not be allocated (no service then)
+    bool Usable() const;
+    // in place on `host` (bytes <= RDC_SVC_MAX_BYTES); the kernel derives the
+    // Split chunks from bytes / sizeof(T); tree: fold in the tree's order.
+    // Synchronous; throws on a device-side failure (the service is then unusable).
+    void Allreduce(const KernelSet& ks, int kind, char* host, uint64_t bytes, bool tree);
 
 private:
     void Stop();
     void EnsureRunning(const KernelSet& ks, int kind);
 
-    int rank_, n_, device_;
+    int rank_, device_;
     double timeout_s_;
     SvcArgs args_;
     SvcBox* box_ = nullptr;       // host address

@@ -1,6 +1,6 @@
 """Randomized stress of mixed collective chains (tests/mp_mixed_worker.py) at
 2-5 processes on GPU 0, 80 ops per run, every output checked bit-exactly
-against the CPU oracle.  python tools/mixed_stress.py (on the GPU box)."""
+against the CPU oracle.  python tests/stress_mixed.py (on the GPU box)."""
 import os, subprocess, sys, tempfile
 import numpy as np
 sys.path.insert(0, os.getcwd())
