@@ -205,7 +205,7 @@ Channel::~Channel() {
     if (scratch) (void)hipFree(scratch);
     if (scratch_ag) (void)hipFree(scratch_ag);
     if (flags) (void)hipFree(flags);
-    if (svc_region) (void)hipFree(svc_region);  // svc_flags live at its end
+    if (svc_region) (void)hipFree(svc_region);
     if (err) (void)hipFree(err);
     if (err_host) (void)hipHostFree(err_host);
 }
@@ -262,11 +262,10 @@ void Communicator::AllocChannel() {
     ch->scratch = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k1));
     ch->scratch_ag = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k3));
     ch->flags = static_cast<uint32_t*>(alloc_shared(ch->L.flag_bytes, &k2));
-    int k5 = 0;  // service slots [2][n] x RDC_SVC_MAX_BYTES, then its n arrival words
-    const size_t svc_slots = (size_t)2 * n_ * RDC_SVC_MAX_BYTES;
-    ch->svc_region = static_cast<char*>(alloc_shared(svc_slots + 4096, &k5));
-    ch->svc_flags = reinterpret_cast<uint32_t*>(ch->svc_region + svc_slots);
-    hip_check(hipMemset(ch->svc_flags, 0, 4096), "memset service flags");
+    int k5 = 0;  // service LL slots [2][n] x RDC_SVC_SLOT_BYTES; zero: no sequence number matches
+    const size_t svc_bytes = (size_t)2 * n_ * RDC_SVC_SLOT_BYTES;
+    ch->svc_region = static_cast<char*>(alloc_shared(svc_bytes, &k5));
+    hip_check(hipMemset(ch->svc_region, 0, svc_bytes), "memset service slots");
     ch->alloc_kind = std::max(std::max(std::max(k1, k2), k3), k5);
     // [0] error word, [16] block arrival counter, [32] completed-launch counter, [48] last kind
     hip_check(hipMalloc(&ch->err, 256), "hipMalloc err");
@@ -281,7 +280,6 @@ void Communicator::AllocChannel() {
     ch->peer_ag[rank_] = ch->scratch_ag;
     ch->peer_flags[rank_] = ch->flags;
     ch->peer_svc_region[rank_] = ch->svc_region;
-    ch->peer_svc_flags[rank_] = ch->svc_flags;
     if (bs_) {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         ch->id = ++g_channel_count[bs_];
@@ -476,7 +474,6 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
             hip_check(hipIpcOpenMemHandle(&sv, hs[(size_t)p].svc, hipIpcMemLazyEnablePeerAccess),
                       "hipIpcOpenMemHandle(service)");
             ch->peer_svc_region[p] = static_cast<char*>(sv);
-            ch->peer_svc_flags[p] = reinterpret_cast<uint32_t*>(ch->peer_svc_region[p] + (size_t)2 * c->n_ * RDC_SVC_MAX_BYTES);
             ch->ipc = true;
         }
         void* pp = nullptr;
@@ -550,7 +547,6 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
             ci->ch_->peer_ag[j] = cs[(size_t)j]->scratch_ag_;
             ci->ch_->peer_flags[j] = cs[(size_t)j]->flags_;
             ci->ch_->peer_svc_region[j] = cs[(size_t)j]->ch_->svc_region;
-            ci->ch_->peer_svc_flags[j] = cs[(size_t)j]->ch_->svc_flags;
             ci->peer_p2p_[j] = cs[(size_t)j]->p2p_;
             if (devices[i] != devices[j]) {
                 int can = 0;
@@ -1151,7 +1147,12 @@ void Communicator::Allgather(void* const* bufs, const uint64_t* sizes, hipStream
 bool Communicator::SmallHostAllreduce(void* host, size_t count, int dtype, int op) {
     const size_t esz = rdc_dtype_size(dtype);
     const uint64_t bytes = (uint64_t)count * esz;
-    if (n_ == 1 || bytes == 0 || bytes > RDC_SVC_MAX_BYTES || !ch_ || !ch_->svc_region || !SmallService::Enabled())
+    // a persistent block per rank: with many ranks on one GPU their queues
+    // outnumber what the hardware scheduler keeps mapped and it time-slices
+    // them (measured: 8 ranks on one MI355X, ~10 ms per call), so past
+    // RDC_HOST_SERVICE_SHARE_MAX ranks per GPU (default 4) the launch path runs
+    if (n_ == 1 || bytes == 0 || bytes > RDC_SVC_MAX_BYTES || !ch_ || !ch_->svc_region || !SmallService::Enabled() ||
+        share_max_ > SmallService::ShareMax())
         return false;
     KernelSet ks;
     if (!get_kernels(dtype, op, &ks))
@@ -1161,7 +1162,7 @@ bool Communicator::SmallHostAllreduce(void* host, size_t count, int dtype, int o
     {
         std::lock_guard<std::mutex> lk(ch_->mu);
         if (!ch_->svc)
-            ch_->svc.reset(new SmallService(rank_, n_, device_, ch_->peer_svc_region, ch_->peer_svc_flags, err_ + 56,
+            ch_->svc.reset(new SmallService(rank_, n_, device_, ch_->peer_svc_region, err_ + 56,
                                             tree_len_, tree_dst_, tree_src_, cfg_.timeout_s, wall_khz_));
         svc = ch_->svc.get();
     }

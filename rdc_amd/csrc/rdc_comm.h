@@ -85,12 +85,10 @@ struct Channel {
     char* peer_ag[RDC_MAX_RANKS] = {};
     uint32_t* peer_flags[RDC_MAX_RANKS] = {};
     // small-allreduce service (rdc_service.h): its own uncached slots
-    // [2][n] x RDC_SVC_MAX_BYTES followed by arrival words [n] per rank (one
-    // allocation), IPC-mapped
+    // small-allreduce service slots (rdc_service.h): [2 halves][n] x
+    // RDC_SVC_SLOT_BYTES of LL words per rank, IPC-mapped
     char* svc_region = nullptr;
-    uint32_t* svc_flags = nullptr;  // = svc_region + 2 n RDC_SVC_MAX_BYTES
     char* peer_svc_region[RDC_MAX_RANKS] = {};
-    uint32_t* peer_svc_flags[RDC_MAX_RANKS] = {};
     std::unique_ptr<SmallService> svc;  // started on first use
     std::mutex mu;
     int users = 0;                     // communicators attached

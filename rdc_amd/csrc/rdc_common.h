@@ -114,24 +114,31 @@ struct CollArgs {
 // HOST-buffer allreduces from a pinned mailbox without a kernel launch per
 // call; it exits after RDC_HOST_SERVICE_IDLE_US of idleness (rdc_service.h).
 #define RDC_SVC_MAX_BYTES (64u << 10)  // largest buffer it serves
+#define RDC_SVC_SLOT_BYTES (2u * RDC_SVC_MAX_BYTES)  // one rank's LL words (4 payload bytes per 8)
+#define RDC_SVC_LL_MAX (16u << 10)  // largest input sent over PCIe as LL words
 enum { RDC_SVC_NEVER = 0, RDC_SVC_RUNNING = 1, RDC_SVC_EXITING = 2, RDC_SVC_EXITED = 3 };
 
 struct SvcBox {  // pinned host memory, hipHostMallocUncached; one per rank
-    alignas(64) uint64_t req;     // host: (seq << 32) | tree << 31 | bytes — the whole request in one word
+    // request header, itself an LL word: (seq << 32) | tree << 31 | ll << 30 | bytes
+    alignas(64) uint64_t hdr;
     alignas(64) uint32_t done;    // device: last completed request
     alignas(64) uint32_t state;   // device: RDC_SVC_*
     alignas(64) uint32_t stop;    // host: exit now
     alignas(64) uint32_t err;     // device: RDC_KERR_* of a failed request (sticky)
-    alignas(256) char data[RDC_SVC_MAX_BYTES];  // the rank's input in, the result out
+    alignas(64) uint64_t trace[4];  // RDC_SVC_TRACE: wall clock at request seen / input sent / peers in / result out
+    // LL mode: the input as LL words {4 payload bytes, seq}; plain mode: the input
+    alignas(256) char data[RDC_SVC_MAX_BYTES];
+    alignas(256) char out[RDC_SVC_MAX_BYTES];  // the result
 };
 
 struct SvcArgs {
     SvcBox* box;                    // device address of this rank's mailbox
-    char* region[RDC_MAX_RANKS];    // rank p's service slots: [2 halves][n] x RDC_SVC_MAX_BYTES (uncached)
-    uint32_t* sflags[RDC_MAX_RANKS];  // rank p's arrival words: [n], word w set by rank w
+    char* region[RDC_MAX_RANKS];    // rank p's service slots: [2 halves][n] x RDC_SVC_SLOT_BYTES (uncached)
     uint32_t* derr;                 // device error word of the service (the mailbox gets a copy)
     int n, rank;
     int strict;                     // RDC_STRICT_FENCES: system fence before `done`
+    int trace;                      // RDC_SVC_TRACE: stamp SvcBox::trace per request
+    int eager;                      // threads that read their LL input vector while polling the header
     uint64_t idle_ticks;            // wall_clock64 ticks without a request before exiting
     uint64_t timeout_ticks;         // waiting for a peer's contribution
     int tree_len;

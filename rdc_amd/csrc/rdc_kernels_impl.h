@@ -21,6 +21,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rdc_device.h"
 #include "rdc_kernels.h"
 
@@ -163,12 +165,13 @@ __device__ void mesh_reduce_range(const CollArgs& a, char* own, const char* slot
         for (int u = 0; u < U; ++u) live[u] = i + u * stride < nvec;
 #pragma unroll
         for (int k = 1; k <= NMAX; ++k) {
-            if (k > n) break;
-            const int q = (r - k + n) % n;  // k-th value in ring order: x[r-1], x[r-2], ..., x[r]
-            const char* src = (q == r ? (const char*)own : slot0 + q * a.slot_bytes) + head;
+            if (k <= n) {  // (a `break` here stops full unrolling: v would live in scratch)
+                const int q = (r - k + n) % n;  // k-th value in ring order: x[r-1], x[r-2], ..., x[r]
+                const char* src = (q == r ? (const char*)own : slot0 + q * a.slot_bytes) + head;
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (live[u]) v[u][k - 1] = ld16_nt(src + (i + u * stride) * 16);
+                for (int u = 0; u < U; ++u)
+                    if (live[u]) v[u][k - 1] = ld16_nt(src + (i + u * stride) * 16);
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -475,11 +478,12 @@ __device__ void oneshot_fold_range(const FoldView& a, int c, uint64_t lo, uint64
         for (int u = 0; u < U; ++u) live[u] = i + u * kBlock < nvec;
 #pragma unroll
         for (int k = 1; k <= NMAX; ++k) {
-            if (k > n) break;
-            const char* p = src((c - k + n) % n) + vlo;
+            if (k <= n) {
+                const char* p = src((c - k + n) % n) + vlo;
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (live[u]) v[u][k - 1] = ld16_nt(p + (i + u * kBlock) * 16);
+                for (int u = 0; u < U; ++u)
+                    if (live[u]) v[u][k - 1] = ld16_nt(p + (i + u * kBlock) * 16);
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -497,25 +501,11 @@ __device__ void oneshot_fold_range(const FoldView& a, int c, uint64_t lo, uint64
 // of [lo, hi) folded over the n ranks' values with the host-planned program
 // acc[d] = OP(acc[d], acc[s]) (rdc_plan.h PlanTreeProgram), result acc[0] —
 // the reference root's bits, which its broadcast hands to every rank.  The
-// program indices are uniform (kernel arguments), so pick / put compile to
-// selects over registers instead of a private-memory array.
-template <int NMAX, typename V>
-__device__ __forceinline__ V tree_pick(const V (&v)[NMAX], int i) {
-    V x = v[0];
-#pragma unroll
-    for (int k = 1; k < NMAX; ++k)
-        if (k == i) x = v[k];
-    return x;
-}
-template <int NMAX, typename V>
-__device__ __forceinline__ void tree_put(V (&v)[NMAX], int i, V x) {
-#pragma unroll
-    for (int k = 0; k < NMAX; ++k)
-        if (k == i) v[k] = x;
-}
-
+// program's indices are run-time values, so the n values live in LDS as
+// [rank][thread] (a register array indexed that way becomes scratch memory).
 template <int OP, typename T, int NMAX>
 __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
+    __shared__ v4u s_acc[NMAX * kBlock];
     const int n = a.n, r = a.r;
     const char* own = a.own;
     char* out = a.out;
@@ -523,16 +513,15 @@ __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
     const unsigned tid = threadIdx.x;
     auto src = [&](int q) -> const char* { return q == r ? own : slots + (uint64_t)q * a.slot_bytes; };
     auto fold_elem = [&](uint64_t x) {
-        T v[NMAX];
+        T* v = reinterpret_cast<T*>(s_acc + tid);  // v[q * 16 / sizeof(T) * kBlock]: rank q's value
+        constexpr int S = 16 / sizeof(T) * kBlock;
 #pragma unroll
         for (int k = 0; k < NMAX; ++k)
-            if (k < n) v[k] = *reinterpret_cast<const T*>(src(k) + x);
-#pragma unroll
-        for (int i = 0; i < NMAX - 1; ++i)
-            if (i < a.tree_len) {
-                const int d = a.tree_dst[i], s = a.tree_src[i];
-                tree_put<NMAX, T>(v, d, OpF<OP>::apply(tree_pick<NMAX, T>(v, d), tree_pick<NMAX, T>(v, s)));
-            }
+            if (k < n) v[k * S] = *reinterpret_cast<const T*>(src(k) + x);
+        for (int i = 0; i < a.tree_len; ++i) {
+            const int d = a.tree_dst[i], s = a.tree_src[i];
+            v[d * S] = OpF<OP>::apply(v[d * S], v[s * S]);
+        }
         *reinterpret_cast<T*>(out + x) = v[0];
     };
     if (((((uintptr_t)own ^ (uintptr_t)slots) | ((uintptr_t)out ^ (uintptr_t)slots)) & 15) != 0) {  // not 16-B aligned
@@ -548,17 +537,19 @@ __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
         else if (tid >= 64 && tid - 64 < nt) fold_elem(vhi + (tid - 64) * sizeof(T));
     }
     const uint64_t nvec = (vhi - vlo) >> 4;
+    v4u* v = s_acc + tid;  // v[q * kBlock]: rank q's vector
     for (uint64_t i = tid; i < nvec; i += kBlock) {
-        v4u v[NMAX];
+        v4u x[NMAX];
 #pragma unroll
         for (int k = 0; k < NMAX; ++k)
-            if (k < n) v[k] = ld16_nt(src(k) + vlo + i * 16);
+            if (k < n) x[k] = ld16_nt(src(k) + vlo + i * 16);
 #pragma unroll
-        for (int j = 0; j < NMAX - 1; ++j)
-            if (j < a.tree_len) {
-                const int d = a.tree_dst[j], s = a.tree_src[j];
-                tree_put<NMAX, v4u>(v, d, reduce16<OP, T>(tree_pick<NMAX, v4u>(v, d), tree_pick<NMAX, v4u>(v, s)));
-            }
+        for (int k = 0; k < NMAX; ++k)
+            if (k < n) v[k * kBlock] = x[k];
+        for (int j = 0; j < a.tree_len; ++j) {
+            const int d = a.tree_dst[j], s = a.tree_src[j];
+            v[d * kBlock] = reduce16<OP, T>(v[d * kBlock], v[s * kBlock]);
+        }
         st16(out + vlo + i * 16, v[0]);
     }
 }
@@ -792,117 +783,250 @@ __device__ __forceinline__ void box_store(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// src[0, bytes) read once (16-byte lanes, rounded up: both sides are 64 KiB
-// areas aligned to 256 B) and stored to every dst[k], k < ndst
-__device__ __forceinline__ void block_scatter(char* const* dst, int ndst, const char* src, uint64_t bytes) {
-    const uint64_t nvec = (bytes + 15) >> 4;
-    constexpr int U = 4;
-    for (uint64_t i = threadIdx.x; i < nvec; i += U * kBlock) {
-        v4u v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (i + u * kBlock < nvec) v[u] = ld16_nt(src + (i + u * kBlock) * 16);
-        for (int k = 0; k < ndst; ++k)
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (i + u * kBlock < nvec) st16_nt(dst[k] + (i + u * kBlock) * 16, v[u]);
-    }
+// ---- exchange between the ranks' service blocks: LL words.  Each 16-byte
+// vector i of a rank's input travels as two 16-byte stores {x, seq, y, seq}
+// {z, seq, w, seq} into its slot of every peer's region (half next & 1): the
+// receiver polls the words themselves, so a vector is complete when its four
+// sequence words match — no write drain before a flag, no flag poll, no
+// second read of the payload.  8-byte {data, seq} pairs inside a 16-byte
+// store are written whole.  A peer is at most one request ahead (it needs
+// this rank's next contribution to finish its own), so it never overwrites
+// the half this rank is still reading.
+__device__ __forceinline__ v4u vload16(const char* p) { return *reinterpret_cast<const volatile v4u*>(p); }
+
+// chunk of element e under utils::Split (rdc_plan.cpp SplitRanges): the
+// first m chunks hold k + 1 elements; positions past `count` (the vector
+// round-up) map to the last chunk
+__device__ __forceinline__ int split_chunk(uint64_t e, uint64_t k, uint64_t m, int n) {
+    const uint64_t big = m * (k + 1);
+    uint64_t c = e < big ? e / (k + 1) : (k ? m + (e - big) / k : (uint64_t)n - 1);
+    return c < (uint64_t)n ? (int)c : n - 1;
 }
 
-template <int OP, typename T, int NMAX>
-__global__ __launch_bounds__(kBlock) void k_svc(SvcArgs a) {
+__device__ __forceinline__ bool ll_match(const v4u& lo, const v4u& hi, uint32_t seq) {
+    return lo.y == seq && lo.w == seq && hi.y == seq && hi.w == seq;
+}
+
+// Two input modes (header bit 30), chosen by the host by size:
+//   LL (<= RDC_HOST_SERVICE_LL_BYTES): the host writes its input as LL words,
+//     so the poll that finds the header can already hold the data (the first
+//     `eager` threads read their vector every round): one PCIe round trip
+//     fewer;
+//   plain: the input as is, read after the header is seen.
+// The result goes to `out` as is, drained, then `done` (measured: LL result
+// words polled by the host landed tens of microseconds late).
+template <int OP, typename T, int NMAX, int BS>
+__global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
+    constexpr int L = 16 / sizeof(T);  // elements per vector
+    constexpr int U = 4;               // input vectors in flight per thread
+    typedef typename std::conditional<sizeof(T) == 1, uint8_t,
+            typename std::conditional<sizeof(T) == 2, uint16_t,
+            typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type>::type>::type UT;
     const int n = a.n, r = a.rank;
+    const unsigned tid = threadIdx.x;
     SvcBox* box = a.box;
+    __shared__ v4u s_in[RDC_SVC_MAX_BYTES / 16];  // this rank's input, read once over PCIe
+    __shared__ v4u s_pv[NMAX * BS];               // [q][thread]: rank q's vector being folded
     __shared__ uint32_t s_next;
-    __shared__ int s_go;
+    __shared__ int s_go, s_err;
     __shared__ uint64_t s_req;
-    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
-    __shared__ char* s_dst[RDC_MAX_RANKS];
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         s_next = box_load(&box->done) + 1u;
+        s_err = 0;
         box_store(&box->state, RDC_SVC_RUNNING);
     }
     __syncthreads();
     for (;;) {
-        if (threadIdx.x == 0) {
-            const uint32_t next = s_next;
-            const uint64_t t0 = wall_clock64();
-            int go = 0;
-            uint64_t q = 0;
-            for (;;) {
-                q = box_load64(&box->req);  // (seq << 32) | tree << 31 | bytes: one word, one PCIe read
-                if (seq_reached((uint32_t)(q >> 32), next)) {
-                    go = 1;
-                    break;
-                }
-                if (box_load(&box->stop)) break;
-                if (wall_clock64() - t0 > a.idle_ticks) {
-                    // leaving: EXITING, then one more look at `req` (the host
-                    // posts `req` and then reads `state`; seq_cst on both sides)
+        // ---- wait for a request (rounds: every thread's loads, one barrier)
+        const uint32_t seq = s_next;
+        const uint64_t t0 = wall_clock64();
+        const bool eager = tid < (unsigned)a.eager;
+        v4u elo = {0, 0, 0, 0}, ehi = {0, 0, 0, 0};
+        int go;
+        for (;;) {
+            if (eager) {
+                elo = ld16_nt(box->data + 32 * tid);
+                ehi = ld16_nt(box->data + 32 * tid + 16);
+            }
+            if (tid == 0) {
+                uint64_t q = box_load64(&box->hdr);
+                const uint32_t stop = box_load(&box->stop);  // issued with the header read: one round trip
+                int g = 0;  // 0 poll again, 1 request, -1 leave
+                if ((uint32_t)(q >> 32) == seq) {
+                    g = 1;
+                } else if (stop) {
+                    g = -1;
+                } else if (wall_clock64() - t0 > a.idle_ticks) {
+                    // leaving: EXITING, then one more look at the header (the
+                    // host posts it and then reads `state`; seq_cst both sides)
                     box_store(&box->state, RDC_SVC_EXITING);
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-                    q = box_load64(&box->req);
-                    if (seq_reached((uint32_t)(q >> 32), next)) {
+                    g = -1;
+                    q = box_load64(&box->hdr);
+                    if ((uint32_t)(q >> 32) == seq) {
                         box_store(&box->state, RDC_SVC_RUNNING);
-                        go = 1;
+                        g = 1;
                     }
+                }
+                s_req = q;
+                s_go = g;
+            }
+            __syncthreads();
+            go = s_go;
+            __syncthreads();  // s_go is rewritten by the next round
+            if (go != 0) break;
+            if (tid == 0) __builtin_amdgcn_s_sleep(1);
+        }
+        if (go < 0) break;
+        uint64_t ts[4];
+        if (a.trace) ts[0] = wall_clock64();
+        const uint64_t req = s_req;
+        const uint64_t bytes = req & 0x3fffffffu;
+        const bool tree = (req >> 31) & 1u, ll = (req >> 30) & 1u;
+        const uint64_t nvec = (bytes + 15) >> 4;  // rounded up: the mailbox and slots have room
+        const uint64_t half = (uint64_t)(seq & 1u) * (uint64_t)n * RDC_SVC_SLOT_BYTES;
+        const uint64_t deadline = wall_clock64() + a.timeout_ticks;
+        bool ok = true;
+        // 1) my input (U vectors in flight per thread), kept in LDS and sent as
+        //    LL words into my slot of every peer's region
+        auto send = [&](uint64_t i, const v4u& x) {
+            s_in[i] = x;
+            for (int k = 1; k < n; ++k) {
+                char* d = a.region[(r + k) % n] + half + (uint64_t)r * RDC_SVC_SLOT_BYTES + 32 * i;
+                st16_nt(d, v4u{x.x, seq, x.y, seq});
+                st16_nt(d + 16, v4u{x.z, seq, x.w, seq});
+            }
+        };
+        if (ll) {
+            const bool have0 = eager && ll_match(elo, ehi, seq);
+            for (uint64_t i0 = tid; i0 < nvec && ok; i0 += (uint64_t)U * BS) {
+                v4u lo[U], hi[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint64_t i = i0 + (uint64_t)u * BS;
+                    if (u == 0 && i0 == tid && have0) {
+                        lo[u] = elo;
+                        hi[u] = ehi;
+                    } else if (i < nvec) {
+                        lo[u] = ld16_nt(box->data + 32 * i);
+                        hi[u] = ld16_nt(box->data + 32 * i + 16);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint64_t i = i0 + (uint64_t)u * BS;
+                    if (i >= nvec || !ok) continue;
+                    uint32_t spins = 0;
+                    while (!ll_match(lo[u], hi[u], seq)) {  // written before the header, so rarely taken
+                        if ((++spins & 63) == 0 && wall_clock64() > deadline) {
+                            ok = false;
+                            break;
+                        }
+                        asm volatile("" ::: "memory");
+                        lo[u] = ld16_nt(box->data + 32 * i);
+                        hi[u] = ld16_nt(box->data + 32 * i + 16);
+                    }
+                    if (ok) send(i, v4u{lo[u].x, lo[u].z, hi[u].x, hi[u].z});
+                }
+            }
+        } else {
+            for (uint64_t i0 = tid; i0 < nvec; i0 += (uint64_t)U * BS) {
+                v4u x[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (i0 + (uint64_t)u * BS < nvec) x[u] = ld16_nt(box->data + 16 * (i0 + (uint64_t)u * BS));
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (i0 + (uint64_t)u * BS < nvec) send(i0 + (uint64_t)u * BS, x[u]);
+            }
+        }
+        if (a.trace) ts[1] = wall_clock64();
+        // 2) per vector: every peer's words (polled together), folded in the
+        //    reference's order in registers, written straight to the mailbox
+        const char* mine = a.region[r] + half;
+        const uint64_t count = bytes / sizeof(T), ck = count / (uint64_t)n, cm = count % (uint64_t)n;
+#pragma unroll 1
+        for (uint64_t i = tid; i < nvec && ok; i += BS) {
+            v4u* pv = s_pv + tid;  // pv[q * BS]
+            const v4u own = s_in[i];
+            uint32_t pending = ((1u << n) - 1u) & ~(1u << r);
+            uint32_t spins = 0;
+            while (pending) {
+                asm volatile("" ::: "memory");  // a fresh load of every pending word per pass
+#pragma unroll
+                for (int q = 0; q < NMAX; ++q)
+                    if ((pending >> q) & 1u) {
+                        const char* p = mine + (uint64_t)q * RDC_SVC_SLOT_BYTES + 32 * i;
+                        const v4u lo = ld16_nt(p), hi = ld16_nt(p + 16);
+                        if (ll_match(lo, hi, seq)) {
+                            pv[q * BS] = v4u{lo.x, lo.z, hi.x, hi.z};
+                            pending &= ~(1u << q);
+                        }
+                    }
+                if (pending && (++spins & 63) == 0 && wall_clock64() > deadline) {
+                    ok = false;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
             }
-            s_go = go;
-            s_req = q;
-        }
-        __syncthreads();
-        if (!s_go) break;
-        const uint32_t next = s_next;
-        const uint64_t bytes = s_req & 0x7fffffffu;
-        const bool tree = (s_req >> 31) & 1u;
-        const uint64_t half = (uint64_t)(next & 1u) * (uint64_t)n * RDC_SVC_MAX_BYTES;
-        char* own = a.region[r] + half + (uint64_t)r * RDC_SVC_MAX_BYTES;
-        // 1) the input, read once over PCIe, into slot r of every rank's half
-        if (threadIdx.x < (unsigned)n) s_dst[threadIdx.x] = a.region[(r + threadIdx.x) % n] + half + (uint64_t)r * RDC_SVC_MAX_BYTES;
-        if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.sflags[(r + 1 + threadIdx.x) % n] + r;
-        __syncthreads();
-        block_scatter(s_dst, n, box->data, bytes);
-        block_publish(s_flags, n - 1, next, 1);
-        __syncthreads();
-        // 2) every peer's copy
-        if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.sflags[r] + (r + 1 + threadIdx.x) % n;
-        __syncthreads();
-        const Abort ab{a.derr, wall_clock64() + a.timeout_ticks};
-        if (!block_wait(s_flags, n - 1, next, ab, RDC_KERR_TIMEOUT_RS, 1)) {
-            if (threadIdx.x == 0) {
-                box_store(&box->err, __hip_atomic_load(a.derr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                box_store(&box->done, next);  // the host reads err
+            if (!ok) break;
+            if (a.trace && i == tid) ts[2] = wall_clock64();
+            pv[r * BS] = own;
+            v4u res;
+            if (tree) {  // acc[d] = OP(acc[d], acc[s]) over the host-planned program; result acc[0]
+                for (int j = 0; j < a.tree_len; ++j) {
+                    const int d = a.tree_dst[j], sidx = a.tree_src[j];
+                    pv[d * BS] = reduce16<OP, T>(pv[d * BS], pv[sidx * BS]);
+                }
+                res = pv[0];
+            } else {
+                const uint64_t e0 = i * (uint64_t)L;
+                const int c0 = split_chunk(e0, ck, cm, n), c1 = split_chunk(e0 + L - 1, ck, cm, n);
+                res = own;
+                for (int c = c0; c <= c1; ++c) {  // ring order of chunk c: x[c-1], then x[c-2] ... x[c]
+                    v4u acc = pv[((c - 1 + n) % n) * BS];
+                    for (int kk = 2; kk <= n; ++kk) acc = reduce16<OP, T>(pv[((c - kk + n) % n) * BS], acc);
+                    if (c0 == c1) {
+                        res = acc;
+                    } else {  // a vector across chunk boundaries: each lane from its own chunk's fold
+                        UT rl[L], al[L];
+                        __builtin_memcpy(rl, &res, 16);
+                        __builtin_memcpy(al, &acc, 16);
+#pragma unroll
+                        for (int l = 0; l < L; ++l)
+                            if (split_chunk(e0 + l, ck, cm, n) == c) rl[l] = al[l];
+                        __builtin_memcpy(&res, rl, 16);
+                    }
+                }
             }
-            break;
+            st16(box->out + 16 * i, res);
         }
-        // 3) fold in the reference's order, straight into the mailbox
-        const FoldView fv{n, r, own, box->data, a.region[r] + half, RDC_SVC_MAX_BYTES, a.tree_len, a.tree_dst,
-                          a.tree_src};
-        if (tree) {
-            tree_fold_range<OP, T, NMAX>(fv, 0, bytes);
-        } else {  // utils::Split chunks (rdc_plan.cpp SplitRanges), in bytes
-            const uint64_t count = bytes / sizeof(T), k = count / (uint64_t)n, m = count % (uint64_t)n;
-            for (int c = 0; c < n; ++c) {
-                const uint64_t b = (uint64_t)c * k + ((uint64_t)c < m ? (uint64_t)c : m);
-                const uint64_t e = (uint64_t)(c + 1) * k + ((uint64_t)(c + 1) < m ? (uint64_t)(c + 1) : m);
-                if (e > b) oneshot_fold_range<OP, T, NMAX>(fv, c, b * sizeof(T), e * sizeof(T));
-            }
-        }
+        if (!ok) s_err = 1;
         // every wave's result stores performed at host memory before `done`
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (s_err) {
+            if (tid == 0) {
+                __hip_atomic_store(a.derr, (uint32_t)RDC_KERR_TIMEOUT_RS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                box_store(&box->err, RDC_KERR_TIMEOUT_RS);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                box_store(&box->done, seq);  // the host reads err
+            }
+            break;
+        }
+        if (tid == 0) {
+            if (a.trace) {
+                ts[3] = wall_clock64();
+                for (int t = 0; t < 4; ++t)
+                    __hip_atomic_store(&box->trace[t], ts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stamps before `done`
+            }
             if (a.strict) __threadfence_system();
-            box_store(&box->done, next);
-            s_next = next + 1u;
+            box_store(&box->done, seq);
+            s_next = seq + 1u;
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) box_store(&box->state, RDC_SVC_EXITED);
+    if (tid == 0) box_store(&box->state, RDC_SVC_EXITED);
 }
 
 // ============================================================ dispatch ===
@@ -937,9 +1061,9 @@ struct Kernels {
     }
     static hipError_t svc(const SvcArgs& a, hipStream_t s) {
         if (a.n <= 8)
-            hipLaunchKernelGGL((k_svc<OP, T, 8>), dim3(1), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_svc<OP, T, 8, 512>), dim3(1), dim3(512), 0, s, a);
         else
-            hipLaunchKernelGGL((k_svc<OP, T, 16>), dim3(1), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_svc<OP, T, 16, 256>), dim3(1), dim3(256), 0, s, a);
         return hipGetLastError();
     }
     static hipError_t tree(const CollArgs& a, int grid, hipStream_t s) {

@@ -1,9 +1,11 @@
 // Small-allreduce service (see rdc_service.h).
 #include "rdc_service.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <stdexcept>
 #include <string>
@@ -30,18 +32,22 @@ bool SmallService::Enabled() {
     return on;
 }
 
-SmallService::SmallService(int rank, int n, int device, char* const* region, uint32_t* const* sflags, uint32_t* derr,
+SmallService::SmallService(int rank, int n, int device, char* const* region, uint32_t* derr,
                            int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz)
     : rank_(rank), device_(device), timeout_s_(timeout_s) {
     memset(&args_, 0, sizeof(args_));
-    for (int p = 0; p < n; ++p) {
-        args_.region[p] = region[p];
-        args_.sflags[p] = sflags[p];
-    }
+    for (int p = 0; p < n; ++p) args_.region[p] = region[p];
     args_.derr = derr;
     args_.n = n;
     args_.rank = rank;
     args_.strict = getenv("RDC_STRICT_FENCES") && atoi(getenv("RDC_STRICT_FENCES")) != 0;
+    args_.trace = getenv("RDC_SVC_TRACE") && atoi(getenv("RDC_SVC_TRACE")) != 0;
+    // LL mode up to RDC_HOST_SERVICE_LL_BYTES (default and most RDC_SVC_LL_MAX);
+    // RDC_HOST_SERVICE_EAGER_BYTES of LL input (default 4 KiB) read by every poll round
+    ll_bytes_ = (uint64_t)std::min(env_double("RDC_HOST_SERVICE_LL_BYTES", RDC_SVC_LL_MAX), (double)RDC_SVC_LL_MAX);
+    const int block = n <= 8 ? 512 : 256;  // Kernels::svc's block size
+    args_.eager = std::max(0, std::min(block, (int)(env_double("RDC_HOST_SERVICE_EAGER_BYTES", 4096) / 16)));
+    wall_khz_ = wall_khz;
     args_.idle_ticks = (uint64_t)(env_double("RDC_HOST_SERVICE_IDLE_US", 1000.0) * (double)wall_khz / 1000.0);
     args_.timeout_ticks = (uint64_t)(timeout_s * (double)wall_khz * 1000.0);
     args_.tree_len = tree_len;
@@ -65,9 +71,26 @@ SmallService::SmallService(int rank, int n, int device, char* const* region, uin
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "service stream");
 }
 
+int SmallService::ShareMax() {
+    static const int v = [] {
+        const char* e = getenv("RDC_HOST_SERVICE_SHARE_MAX");
+        return e && *e ? atoi(e) : 4;
+    }();
+    return v;
+}
+
 bool SmallService::Usable() const { return box_ != nullptr; }
 
 SmallService::~SmallService() {
+    if (args_.trace && traced_ > 0) {
+        const double us = 1000.0 / (double)wall_khz_, k = 1.0 / (double)traced_;
+        fprintf(stderr,
+                "[rdc service] rank %d: %ld requests: host post->done %.2f us; device: seen->sent %.2f, "
+                "sent->peers in %.2f, peers in->result out %.2f us; poll + done visibility %.2f us\n",
+                rank_, traced_, tr_[0] * k, tr_[1] * k * us, tr_[2] * k * us, tr_[3] * k * us,
+                (tr_[0] - (tr_[1] + tr_[2] + tr_[3]) * us) * k);
+        fprintf(stderr, "[rdc service] rank %d host: LL encode + copy in %.2f us\n", rank_, ht_[0] * k);
+    }
     try {
         Stop();
     } catch (...) {
@@ -111,21 +134,63 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
     if (bytes > RDC_SVC_MAX_BYTES) throw std::logic_error("rdc service: buffer too large");
     hip_check(hipSetDevice(device_), "hipSetDevice");
     if (launched_ && kind != kind_) Stop();  // another (dtype, op) needs another kernel
-    memcpy(box_->data, host, bytes);
     const uint32_t r = ++req_;
-    // the whole request in one word, stored after the data (x86 stores stay in order)
-    __atomic_store_n(&box_->req, ((uint64_t)r << 32) | (tree ? 1ull << 31 : 0ull) | bytes, __ATOMIC_SEQ_CST);
-    EnsureRunning(ks, kind);
+    const bool ll = bytes <= ll_bytes_;
+    const uint64_t nwords = ((bytes + 15) / 16) * 4;  // whole 16-byte vectors of 4-byte LL payloads
     const auto t0 = std::chrono::steady_clock::now();
+    if (ll) {
+        // LL words {4 payload bytes, r}, built in host memory and copied in
+        // whole; the device takes a word once it carries r, so the order in
+        // which they land does not matter
+        const uint64_t tag = (uint64_t)r << 32, full = bytes / 4;
+        for (uint64_t j = 0; j < full; ++j) {
+            uint32_t v;
+            memcpy(&v, host + 4 * j, 4);
+            stage_[j] = tag | v;
+        }
+        for (uint64_t j = full; j < nwords; ++j) {
+            uint32_t v = 0;
+            if (4 * j < bytes) memcpy(&v, host + 4 * j, bytes - 4 * j);
+            stage_[j] = tag | v;
+        }
+        memcpy(box_->data, stage_.data(), nwords * 8);
+        if (args_.trace) ht_[0] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    } else {
+        memcpy(box_->data, host, bytes);
+    }
+    // the header, after the data (x86 stores stay in order)
+    __atomic_store_n(&box_->hdr, ((uint64_t)r << 32) | (tree ? 1ull << 31 : 0ull) | (ll ? 1ull << 30 : 0ull) | bytes,
+                     __ATOMIC_SEQ_CST);
+    EnsureRunning(ks, kind);
     const double limit = timeout_s_ * 2 + 10;
-    for (uint32_t spins = 0; (int32_t)(host_load(&box_->done) - r) < 0;) {
-        __builtin_ia32_pause();
-        if ((++spins & 4095) == 0 &&
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+    auto check = [&](uint32_t spins) {
+        if ((spins & 4095) != 0) return;
+        if (host_load(&box_->err) != 0) {
+            broken_ = true;
+            (void)hipStreamSynchronize(stream_);
+            launched_ = false;
+            throw std::runtime_error("rdc service: a peer did not join request " + std::to_string(r) + " on rank " +
+                                     std::to_string(rank_) + " (communicator is now unusable)");
+        }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
             broken_ = true;
             throw std::runtime_error("rdc service: request " + std::to_string(r) + " did not complete on rank " +
                                      std::to_string(rank_));
         }
+    };
+    uint32_t spins = 0;
+    while ((int32_t)(host_load(&box_->done) - r) < 0) {
+        __builtin_ia32_pause();
+        check(++spins);
+    }
+    if (args_.trace) {
+        const double host_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        const uint64_t* t = box_->trace;
+        tr_[0] += host_us;
+        tr_[1] += (double)(t[1] - t[0]);
+        tr_[2] += (double)(t[2] - t[1]);
+        tr_[3] += (double)(t[3] - t[2]);
+        ++traced_;
     }
     if (host_load(&box_->err) != 0) {
         broken_ = true;
@@ -134,7 +199,7 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
         throw std::runtime_error("rdc service: a peer did not join request " + std::to_string(r) + " on rank " +
                                  std::to_string(rank_) + " (communicator is now unusable)");
     }
-    memcpy(host, box_->data, bytes);
+    memcpy(host, box_->out, bytes);
 }
 
 }  // namespace rdc_amd

@@ -8,11 +8,12 @@
 // memory).  Here each rank keeps ONE resident block (k_svc) while calls keep
 // coming: the host copies its input into a pinned, GPU-uncached mailbox and
 // posts one request word (seq, bytes, tree); the block, polling that word,
-// reads the input once over PCIe and stores it into its slot of every rank's
-// service region (xGMI), waits for the peers' arrival words, folds every
-// element in the reference's order (Split chunk ring order, or the tree's
-// order below rdc_reduce_ring_mincount — the one-shot's fold code) straight
-// into the mailbox and bumps `done`.
+// reads the input once over PCIe and stores it as LL words (4 payload bytes +
+// the request's sequence number per 8) into its slot of every peer's service
+// region (xGMI); each thread then polls the peers' words for its own vectors,
+// folds every element in the reference's order (Split chunk ring order, or
+// the tree's order below rdc_reduce_ring_mincount) in registers, writes the
+// result straight into the mailbox, and the block bumps `done`.
 //
 // The block exits after RDC_HOST_SERVICE_IDLE_US (default 1000) without a
 // request, when the host sets `stop` (another (dtype, op), teardown) or when
@@ -20,11 +21,14 @@
 // device-wide synchronisation waits at most the idle time.  The next call
 // relaunches it.  Its slots and arrival words are its own (not the channel's
 // scratch), so it never races the channel's stream-ordered launches.
-// RDC_HOST_SERVICE=0 disables it.
+// RDC_HOST_SERVICE=0 disables it; with more than RDC_HOST_SERVICE_SHARE_MAX
+// (default 4) ranks on one GPU it is not used (their persistent blocks'
+// queues get time-sliced by the hardware scheduler).
 #pragma once
 #include <hip/hip_runtime_api.h>
 
 #include <mutex>
+#include <vector>
 
 #include "rdc_common.h"
 #include "rdc_kernels.h"
@@ -33,12 +37,14 @@ namespace rdc_amd {
 
 class SmallService {
 public:
-    // region / sflags: every rank's service slots and arrival words (peers'
-    // IPC-mapped or direct); derr: a device word for the kernel's errors
-    SmallService(int rank, int n, int device, char* const* region, uint32_t* const* sflags, uint32_t* derr,
+    // region: every rank's service slots (peers' IPC-mapped or direct); derr:
+    // a device word for the kernel's errors
+    SmallService(int rank, int n, int device, char* const* region, uint32_t* derr,
                  int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz);
     ~SmallService();
     static bool Enabled();
+    // most ranks per GPU it runs with (RDC_HOST_SERVICE_SHARE_MAX, default 4)
+    static int ShareMax();
     // false when the uncached mailbox could not be allocated (no service then)
     bool Usable() const;
     // in place on `host` (bytes <= RDC_SVC_MAX_BYTES); the kernel derives the
@@ -59,6 +65,12 @@ private:
     bool launched_ = false;
     bool broken_ = false;
     uint32_t req_ = 0;
+    int wall_khz_ = 100000;
+    uint64_t ll_bytes_ = RDC_SVC_LL_MAX;  // LL mode up to this many bytes
+    std::vector<uint64_t> stage_ = std::vector<uint64_t>(RDC_SVC_LL_MAX / 4);  // LL input words, built here
+    double tr_[4] = {0, 0, 0, 0};  // RDC_SVC_TRACE sums: host us, device ticks per phase
+    long traced_ = 0;
+    double ht_[1] = {0};  // RDC_SVC_TRACE: LL encode time
     std::mutex mu_;
 };
 

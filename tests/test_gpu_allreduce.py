@@ -422,14 +422,20 @@ def expected_host_mix(world, mincount=1):
 
 
 @pytest.mark.parametrize("world,env", [(2, {}), (3, {"rdc_reduce_ring_mincount": "8K"}), (2, {"RDC_HOST_SERVICE": "0"}),
-                                       (4, {"RDC_HOST_SERVICE_IDLE_US": "50"})])
+                                       (4, {"RDC_HOST_SERVICE_IDLE_US": "50"}),
+                                       (2, {"RDC_HOST_SERVICE_LL_BYTES": "0"}),
+                                       (3, {"RDC_HOST_SERVICE_EAGER_BYTES": "0", "rdc_reduce_ring_mincount": "8K"}),
+                                       (8, {"RDC_HOST_SERVICE_SHARE_MAX": "8"})])
 def test_mp_host_small_service(world, env):
     """Small synchronous HOST allreduces (cfg1's path) through the resident
     service block (rdc_service.h): 12 calls of 1 B - 64 KiB over 8 (dtype, op)
     pairs (each switch restarts the kernel), sleeps of 3-5 ms longer than its
     idle time (it exits and is relaunched), device collectives in between,
-    the tree order below rdc_reduce_ring_mincount; and the launch path with
-    RDC_HOST_SERVICE=0.  Every result bit-exact against the oracle."""
+    the tree order below rdc_reduce_ring_mincount; LL and plain input modes
+    (RDC_HOST_SERVICE_LL_BYTES=0), no eager polling, 8 ranks (the 8-wide
+    kernel; RDC_HOST_SERVICE_SHARE_MAX lifts the one-GPU cap); and the
+    launch path with RDC_HOST_SERVICE=0.  Every result bit-exact against the
+    oracle."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cases = [{"count": 0, "dtype": 6, "op": 2, "kind": "host_mix", "ops": HOST_MIX}]
