@@ -114,21 +114,22 @@ struct CollArgs {
 // HOST-buffer allreduces from a pinned mailbox without a kernel launch per
 // call; it exits after RDC_HOST_SERVICE_IDLE_US of idleness (rdc_service.h).
 #define RDC_SVC_MAX_BYTES (64u << 10)  // largest buffer it serves
-#define RDC_SVC_SLOT_BYTES (2u * RDC_SVC_MAX_BYTES)  // one rank's LL words (4 payload bytes per 8)
+#define RDC_SVC_SLOT_BYTES (2u * RDC_SVC_MAX_BYTES)  // one rank's LL words: two planes of RDC_SVC_MAX_BYTES
 #define RDC_SVC_LL_MAX (16u << 10)  // largest input sent over PCIe as LL words
 enum { RDC_SVC_NEVER = 0, RDC_SVC_RUNNING = 1, RDC_SVC_EXITING = 2, RDC_SVC_EXITED = 3 };
 
 struct SvcBox {  // pinned host memory, hipHostMallocUncached; one per rank
-    // request header, itself an LL word: (seq << 32) | tree << 31 | ll << 30 | bytes
+    // request header, itself an LL word: (seq << 32) | tree << 31 | LL input << 30 | LL result << 29 | bytes
     alignas(64) uint64_t hdr;
     alignas(64) uint32_t done;    // device: last completed request
     alignas(64) uint32_t state;   // device: RDC_SVC_*
     alignas(64) uint32_t stop;    // host: exit now
     alignas(64) uint32_t err;     // device: RDC_KERR_* of a failed request (sticky)
     alignas(64) uint64_t trace[4];  // RDC_SVC_TRACE: wall clock at request seen / input sent / peers in / result out
-    // LL mode: the input as LL words {4 payload bytes, seq}; plain mode: the input
+    // the input: LL words {4 payload bytes, seq} in two planes of RDC_SVC_LL_MAX
+    // (k_svc), or as is
     alignas(256) char data[RDC_SVC_MAX_BYTES];
-    alignas(256) char out[RDC_SVC_MAX_BYTES];  // the result
+    alignas(256) char out[RDC_SVC_MAX_BYTES];  // the result: LL words (two planes) or as is
 };
 
 struct SvcArgs {

@@ -807,14 +807,17 @@ __device__ __forceinline__ bool ll_match(const v4u& lo, const v4u& hi, uint32_t 
     return lo.y == seq && lo.w == seq && hi.y == seq && hi.w == seq;
 }
 
-// Two input modes (header bit 30), chosen by the host by size:
-//   LL (<= RDC_HOST_SERVICE_LL_BYTES): the host writes its input as LL words,
-//     so the poll that finds the header can already hold the data (the first
-//     `eager` threads read their vector every round): one PCIe round trip
-//     fewer;
-//   plain: the input as is, read after the header is seen.
-// The result goes to `out` as is, drained, then `done` (measured: LL result
-// words polled by the host landed tens of microseconds late).
+// Header bits: 31 tree order, 30 LL input, 29 LL result, 0-28 bytes.
+//   LL input (<= RDC_HOST_SERVICE_LL_BYTES): the host writes its input as LL
+//     words, so the poll that finds the header can already hold the data (the
+//     first `eager` threads read their vector every round): one PCIe round
+//     trip fewer; otherwise the input as is, read after the header is seen.
+//   LL result: the result as LL words the host polls (no drain, no `done`
+//     wait on the host); otherwise as is, drained, then `done`.
+// LL words are PLANAR: vector i's {w0, seq, w1, seq} at plane 0 + 16 i and
+// {w2, seq, w3, seq} at plane 1 + 16 i, so the 64 lanes of one instruction
+// touch 1 KiB of contiguous memory (an interleaved 32-byte pair per lane made
+// every instruction 64 separate 16-byte requests).
 template <int OP, typename T, int NMAX, int BS>
 __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
     constexpr int L = 16 / sizeof(T);  // elements per vector
@@ -845,8 +848,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
         int go;
         for (;;) {
             if (eager) {
-                elo = ld16_nt(box->data + 32 * tid);
-                ehi = ld16_nt(box->data + 32 * tid + 16);
+                elo = ld16_nt(box->data + 16 * tid);
+                ehi = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * tid);
             }
             if (tid == 0) {
                 uint64_t q = box_load64(&box->hdr);
@@ -881,8 +884,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
         uint64_t ts[4];
         if (a.trace) ts[0] = wall_clock64();
         const uint64_t req = s_req;
-        const uint64_t bytes = req & 0x3fffffffu;
-        const bool tree = (req >> 31) & 1u, ll = (req >> 30) & 1u;
+        const uint64_t bytes = req & 0x1fffffffu;
+        const bool tree = (req >> 31) & 1u, ll = (req >> 30) & 1u, ll_out = (req >> 29) & 1u;
         const uint64_t nvec = (bytes + 15) >> 4;  // rounded up: the mailbox and slots have room
         const uint64_t half = (uint64_t)(seq & 1u) * (uint64_t)n * RDC_SVC_SLOT_BYTES;
         const uint64_t deadline = wall_clock64() + a.timeout_ticks;
@@ -892,9 +895,9 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
         auto send = [&](uint64_t i, const v4u& x) {
             s_in[i] = x;
             for (int k = 1; k < n; ++k) {
-                char* d = a.region[(r + k) % n] + half + (uint64_t)r * RDC_SVC_SLOT_BYTES + 32 * i;
+                char* d = a.region[(r + k) % n] + half + (uint64_t)r * RDC_SVC_SLOT_BYTES + 16 * i;
                 st16_nt(d, v4u{x.x, seq, x.y, seq});
-                st16_nt(d + 16, v4u{x.z, seq, x.w, seq});
+                st16_nt(d + RDC_SVC_MAX_BYTES, v4u{x.z, seq, x.w, seq});
             }
         };
         if (ll) {
@@ -908,8 +911,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                         lo[u] = elo;
                         hi[u] = ehi;
                     } else if (i < nvec) {
-                        lo[u] = ld16_nt(box->data + 32 * i);
-                        hi[u] = ld16_nt(box->data + 32 * i + 16);
+                        lo[u] = ld16_nt(box->data + 16 * i);
+                        hi[u] = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * i);
                     }
                 }
 #pragma unroll
@@ -923,8 +926,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                             break;
                         }
                         asm volatile("" ::: "memory");
-                        lo[u] = ld16_nt(box->data + 32 * i);
-                        hi[u] = ld16_nt(box->data + 32 * i + 16);
+                        lo[u] = ld16_nt(box->data + 16 * i);
+                        hi[u] = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * i);
                     }
                     if (ok) send(i, v4u{lo[u].x, lo[u].z, hi[u].x, hi[u].z});
                 }
@@ -956,8 +959,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
 #pragma unroll
                 for (int q = 0; q < NMAX; ++q)
                     if ((pending >> q) & 1u) {
-                        const char* p = mine + (uint64_t)q * RDC_SVC_SLOT_BYTES + 32 * i;
-                        const v4u lo = ld16_nt(p), hi = ld16_nt(p + 16);
+                        const char* p = mine + (uint64_t)q * RDC_SVC_SLOT_BYTES + 16 * i;
+                        const v4u lo = ld16_nt(p), hi = ld16_nt(p + RDC_SVC_MAX_BYTES);
                         if (ll_match(lo, hi, seq)) {
                             pv[q * BS] = v4u{lo.x, lo.z, hi.x, hi.z};
                             pending &= ~(1u << q);
@@ -998,11 +1001,17 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                     }
                 }
             }
-            st16(box->out + 16 * i, res);
+            if (ll_out) {  // LL result words, planar like the input; the host polls them
+                st16(box->out + 16 * i, v4u{res.x, seq, res.y, seq});
+                st16(box->out + RDC_SVC_LL_MAX + 16 * i, v4u{res.z, seq, res.w, seq});
+            } else {
+                st16(box->out + 16 * i, res);
+            }
         }
         if (!ok) s_err = 1;
-        // every wave's result stores performed at host memory before `done`
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // plain result: every wave's stores performed at host memory before
+        // `done` (LL result words carry their own sequence number)
+        if (!ll_out) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (s_err) {
             if (tid == 0) {

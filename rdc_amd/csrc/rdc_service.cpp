@@ -45,6 +45,9 @@ SmallService::SmallService(int rank, int n, int device, char* const* region, uin
     // LL mode up to RDC_HOST_SERVICE_LL_BYTES (default and most RDC_SVC_LL_MAX);
     // RDC_HOST_SERVICE_EAGER_BYTES of LL input (default 4 KiB) read by every poll round
     ll_bytes_ = (uint64_t)std::min(env_double("RDC_HOST_SERVICE_LL_BYTES", RDC_SVC_LL_MAX), (double)RDC_SVC_LL_MAX);
+    // LL result up to RDC_HOST_SERVICE_LL_OUT_BYTES (default 256: measured faster
+    // than a drained result + `done` up to 256 B, slower from 1 KiB)
+    ll_out_bytes_ = (uint64_t)std::min(env_double("RDC_HOST_SERVICE_LL_OUT_BYTES", 256), (double)RDC_SVC_LL_MAX);
     const int block = n <= 8 ? 512 : 256;  // Kernels::svc's block size
     args_.eager = std::max(0, std::min(block, (int)(env_double("RDC_HOST_SERVICE_EAGER_BYTES", 4096) / 16)));
     wall_khz_ = wall_khz;
@@ -141,25 +144,32 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
     if (ll) {
         // LL words {4 payload bytes, r}, built in host memory and copied in
         // whole; the device takes a word once it carries r, so the order in
-        // which they land does not matter
+        // which they land does not matter.  Planar (k_svc): payload word j of
+        // vector j / 4 goes to plane (j / 2) % 2.
         const uint64_t tag = (uint64_t)r << 32, full = bytes / 4;
+        auto put = [&](uint64_t j, uint32_t v) { stage_[ll_index(j)] = tag | v; };
         for (uint64_t j = 0; j < full; ++j) {
             uint32_t v;
             memcpy(&v, host + 4 * j, 4);
-            stage_[j] = tag | v;
+            put(j, v);
         }
         for (uint64_t j = full; j < nwords; ++j) {
             uint32_t v = 0;
             if (4 * j < bytes) memcpy(&v, host + 4 * j, bytes - 4 * j);
-            stage_[j] = tag | v;
+            put(j, v);
         }
-        memcpy(box_->data, stage_.data(), nwords * 8);
+        const uint64_t plane_words = nwords / 2;  // nwords is a multiple of 4
+        memcpy(box_->data, stage_.data(), plane_words * 8);
+        memcpy(box_->data + RDC_SVC_LL_MAX, stage_.data() + RDC_SVC_LL_MAX / 8, plane_words * 8);
         if (args_.trace) ht_[0] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     } else {
         memcpy(box_->data, host, bytes);
     }
     // the header, after the data (x86 stores stay in order)
-    __atomic_store_n(&box_->hdr, ((uint64_t)r << 32) | (tree ? 1ull << 31 : 0ull) | (ll ? 1ull << 30 : 0ull) | bytes,
+    const bool ll_out = bytes <= ll_out_bytes_;
+    __atomic_store_n(&box_->hdr,
+                     ((uint64_t)r << 32) | (tree ? 1ull << 31 : 0ull) | (ll ? 1ull << 30 : 0ull) |
+                         (ll_out ? 1ull << 29 : 0ull) | bytes,
                      __ATOMIC_SEQ_CST);
     EnsureRunning(ks, kind);
     const double limit = timeout_s_ * 2 + 10;
@@ -179,11 +189,26 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
         }
     };
     uint32_t spins = 0;
-    while ((int32_t)(host_load(&box_->done) - r) < 0) {
-        __builtin_ia32_pause();
-        check(++spins);
+    if (ll_out) {  // every result word as it lands, decoded in place
+        const uint64_t* o = reinterpret_cast<const uint64_t*>(box_->out);
+        const uint64_t used = (bytes + 3) / 4;
+        for (uint64_t j = 0; j < used; ++j) {
+            uint64_t v;
+            while ((uint32_t)((v = __atomic_load_n(o + ll_index(j), __ATOMIC_ACQUIRE)) >> 32) != r) {
+                __builtin_ia32_pause();
+                check(++spins);
+            }
+            const uint32_t x = (uint32_t)v;
+            memcpy(host + 4 * j, &x, std::min<uint64_t>(4, bytes - 4 * j));
+        }
+    } else {
+        while ((int32_t)(host_load(&box_->done) - r) < 0) {
+            __builtin_ia32_pause();
+            check(++spins);
+        }
     }
     if (args_.trace) {
+        while ((int32_t)(host_load(&box_->done) - r) < 0) __builtin_ia32_pause();  // the stamps
         const double host_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         const uint64_t* t = box_->trace;
         tr_[0] += host_us;
@@ -199,7 +224,7 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
         throw std::runtime_error("rdc service: a peer did not join request " + std::to_string(r) + " on rank " +
                                  std::to_string(rank_) + " (communicator is now unusable)");
     }
-    memcpy(host, box_->out, bytes);
+    if (!ll_out) memcpy(host, box_->out, bytes);
 }
 
 }  // namespace rdc_amd

@@ -66,7 +66,10 @@ private:
     bool broken_ = false;
     uint32_t req_ = 0;
     int wall_khz_ = 100000;
-    uint64_t ll_bytes_ = RDC_SVC_LL_MAX;  // LL mode up to this many bytes
+    uint64_t ll_bytes_ = RDC_SVC_LL_MAX;  // LL input up to this many bytes
+    uint64_t ll_out_bytes_ = 0;           // LL result up to this many bytes
+    // 8-byte LL word of payload word j in the planar layout (k_svc)
+    static uint64_t ll_index(uint64_t j) { return ((j >> 1) & 1) * (RDC_SVC_LL_MAX / 8) + 2 * (j >> 2) + (j & 1); }
     std::vector<uint64_t> stage_ = std::vector<uint64_t>(RDC_SVC_LL_MAX / 4);  // LL input words, built here
     double tr_[4] = {0, 0, 0, 0};  // RDC_SVC_TRACE sums: host us, device ticks per phase
     long traced_ = 0;

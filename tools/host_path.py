@@ -50,17 +50,24 @@ def main():
     call()
     if world > 1:
         dist.barrier()
+    per = []
     t0 = time.perf_counter()
     for _ in range(iters):
+        t1 = time.perf_counter()
         call()
+        per.append(time.perf_counter() - t1)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
+    per.sort()
+    med_us, max_us = per[len(per) // 2] * 1e6, per[-1] * 1e6
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t[0])
     if rank == 0:
-        print(json.dumps({"host_path": True, "n": world, "bytes": S, "ms_per_call": round(dt * 1e3, 3),
+        print(json.dumps({"host_path": True, "n": world, "bytes": S, "ms_per_call": round(dt * 1e3, 4),
+                          "us_per_call_mean": round(dt * 1e6, 2), "us_per_call_median_rank0": round(med_us, 2),
+                          "us_per_call_max_rank0": round(max_us, 1),
                           "GBps": round(S / dt / 1e9, 3), "memory": "pageable numpy"}), flush=True)
     if world > 1:
         dist.barrier()
