@@ -223,7 +223,6 @@ void HostPath::DrainLoop() {
 // error word needs no copy (the kernel mirrors it into pinned memory).
 void HostPath::AllreduceSmall(Communicator* c, char* h, size_t count, size_t S, int dtype, int op,
                               hipStream_t comm_stream) {
-    if (c->SmallHostAllreduce(h, count, dtype, op)) return;  // the resident service (rdc_service.h)
     if (!pin_small_) {
         hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_small_), kSmall + 64, hipHostMallocCoherent),
                   "hipHostMalloc");
@@ -260,6 +259,8 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
     const size_t esz = rdc_dtype_size(dtype);
     const size_t S = count * esz;
     char* h = static_cast<char*>(host);
+    // the resident service (rdc_service.h) needs no HIP call per request
+    if (S <= kSmall && c->SmallHostAllreduce(h, count, dtype, op)) return;
     hip_check(hipSetDevice(device_), "hipSetDevice");
     if (S <= kSmall) {
         AllreduceSmall(c, h, count, S, dtype, op, comm_stream);

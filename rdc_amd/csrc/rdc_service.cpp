@@ -126,6 +126,7 @@ void SmallService::EnsureRunning(const KernelSet& ks, int kind) {
         launched_ = false;
     }
     host_store(&box_->state, RDC_SVC_NEVER);
+    hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(ks.svc(args_, stream_), "launch service");
     launched_ = true;
     kind_ = kind;
@@ -135,7 +136,6 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
     std::lock_guard<std::mutex> lk(mu_);
     if (broken_) throw std::runtime_error("rdc service: unusable after an earlier failure");
     if (bytes > RDC_SVC_MAX_BYTES) throw std::logic_error("rdc service: buffer too large");
-    hip_check(hipSetDevice(device_), "hipSetDevice");
     if (launched_ && kind != kind_) Stop();  // another (dtype, op) needs another kernel
     const uint32_t r = ++req_;
     const bool ll = bytes <= ll_bytes_;
