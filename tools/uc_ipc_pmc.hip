@@ -4,7 +4,10 @@
 //   hipcc --offload-arch=gfx950 -O3 -o tools/uc_ipc_pmc tools/uc_ipc_pmc.hip
 //   tools/uc_ipc_pmc owner DIR &                      # exports 256 MiB, waits for DIR/done
 //   rocprofv3 --pmc WRITE_SIZE -d OUT -o run --output-format csv -- tools/uc_ipc_pmc writer DIR
+//   tools/uc_ipc_pmc busy SECONDS        # an unprofiled process storing into its own memory meanwhile
 // Kernels: k_ipc_store (256 MiB into the owner's memory), k_local_store (256 MiB local).
+// TCC counters are device-wide: with `busy` running, the profiled dispatches
+// also count its stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -42,6 +45,31 @@ int main(int argc, char** argv) {
         return 2;
     }
     const std::string mode = argv[1], dir = argv[2];
+    if (mode == "busy") {  // store into own uncached memory for `dir` seconds
+        void* p = nullptr;
+        CK(hipExtMallocWithFlags(&p, kBytes, hipDeviceMallocUncached));
+        const double secs = atof(dir.c_str());
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        CK(hipEventRecord(e0));
+        int launches = 0;
+        for (float el = 0; el < secs * 1000; ++launches) {
+            for (int k = 0; k < 20; ++k) {
+                hipLaunchKernelGGL(k_local_store, dim3(1024), dim3(256), 0, 0, (v4u*)p, kBytes / 16);
+                CK(hipGetLastError());
+            }
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&el, e0, e1));
+        }
+        float el = 0;
+        CK(hipEventElapsedTime(&el, e0, e1));
+        printf("{\"busy_launches\": %d, \"busy_GBps\": %.1f}\n", launches * 20,
+               (double)launches * 20 * kBytes / (el * 1e-3) / 1e9);
+        CK(hipFree(p));
+        return 0;
+    }
     const std::string hfile = dir + "/handle", dfile = dir + "/done";
     if (mode == "owner") {
         void* p = nullptr;
