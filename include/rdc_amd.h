@@ -99,7 +99,14 @@ int RdcAllreduceCoalescedOn(void* comm, void** bufs, const size_t* counts, int n
 
 /* rdc::NewCommunicator / GetCommunicator (include/rdc.h:62-71;
  * rdc/comm.py:398-427 calls RdcNewCommunicator(byref(handle), name)).
- * NewCommunicator is collective over all ranks. */
+ * NewCommunicator is collective over all ranks.  Named communicators over the
+ * same ranks share one scratch channel (one pool of uncached HBM per rank):
+ * every rank must then issue the collectives of ALL those communicators in
+ * the same order (the SPMD order rdc programs follow; the reference's
+ * Allreduce is not thread-safe either, communicator.h:87).  Ranks that
+ * interleave two communicators differently — e.g. from two threads — need
+ * RDC_SHARE_SCRATCH=0 (a channel per communicator, as the reference's
+ * independent TCP meshes behave). */
 int RdcNewCommunicator(void** out, const char* name);
 int RdcGetCommunicator(void** out, const char* name);
 /* rdc::CreateGroup / ICommunicator::CreateGroup (include/api.h:124-125,
