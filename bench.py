@@ -121,8 +121,11 @@ def sync_check(comm, sp, dist, torch):
         raise RuntimeError(err or "failed on another rank")
 
 
-def timed_ms(one, comm, sp, dist, torch, steps, warm=2):
-    """ms per call of one(), max over ranks, after `warm` checked calls."""
+def timed_ms(one, comm, sp, dist, torch, steps, warm=2, synchronous=False):
+    """ms per call of one(), max over ranks, after `warm` checked calls.
+    synchronous: one() has completed when it returns (host-buffer calls), so
+    the clock stops at the end of the loop; otherwise after a device sync and
+    a barrier (stream-ordered launches)."""
     for _ in range(warm):
         one()
     sync_check(comm, sp, dist, torch)
@@ -130,8 +133,9 @@ def timed_ms(one, comm, sp, dist, torch, steps, warm=2):
     t0 = time.perf_counter()
     for _ in range(steps):
         one()
-    torch.cuda.synchronize()
-    dist.barrier()
+    if not synchronous:
+        torch.cuda.synchronize()
+        dist.barrier()
     t = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     sync_check(comm, sp, dist, torch)
@@ -218,10 +222,11 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out):
     # cfg1 on the real path: 4 KiB of fp32 in pageable host memory through
     # RdcAllreduce (rdc/core.py's entry point), synchronous per call
     a = np.ones(1024, dtype=np.float32)
-    ms = timed(lambda: check_call(lib.RdcAllreduce(ctypes.c_void_p(a.ctypes.data), 1024, 6, 2, None, None)),
-               max(steps, 200))
-    e = entry(ms, 4096, "4 KiB float32 allreduce of HOST memory via RdcAllreduce (cfg1 shape, synchronous)",
-              max(steps, 200))
+    pa = ctypes.c_void_p(a.ctypes.data)
+    ms = timed_ms(lambda: check_call(lib.RdcAllreduce(pa, 1024, 6, 2, None, None)), comm, sp, dist, torch,
+                  max(steps, 2000), warm=20, synchronous=True)
+    e = entry(ms, 4096, "4 KiB float32 allreduce of HOST memory via RdcAllreduce (cfg1 shape, synchronous; "
+              "clock stops when the last call returns, max over ranks)", max(steps, 2000))
     e["us_per_call"] = round(ms * 1e3, 2)
     out["cfg1_host_4KiB"] = e
     # cfg2's 256 MiB fp32 buffer and the sizes below it (prefixes of one
@@ -235,7 +240,9 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out):
     for nb in (4 << 10, 64 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, big):
         if nb > big:
             continue
-        ns = max(steps, 50) if nb <= (16 << 20) else steps  # small calls: more of them
+        # small calls: enough of them that the closing device sync + barrier
+        # (~1 ms with gloo) is noise (50 calls made it 20 us of a 4 KiB call)
+        ns = max(steps, 2000 if nb <= (64 << 10) else 400 if nb <= (1 << 20) else 50 if nb <= (16 << 20) else 0)
         ms = timed(lambda: check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(f.data_ptr()),
                                                              nb // 4, 6, 2, 0, sp)), ns)
         e = entry(ms, nb, "in-place allreduce(sum) of %d KiB float32" % (nb >> 10), ns)
