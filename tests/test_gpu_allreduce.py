@@ -425,7 +425,10 @@ def expected_host_mix(world, mincount=1):
                                        (4, {"RDC_HOST_SERVICE_IDLE_US": "50"}),
                                        (2, {"RDC_HOST_SERVICE_LL_BYTES": "0"}),
                                        (3, {"RDC_HOST_SERVICE_EAGER_BYTES": "0", "rdc_reduce_ring_mincount": "8K"}),
-                                       (8, {"RDC_HOST_SERVICE_SHARE_MAX": "8"})])
+                                       (8, {"RDC_HOST_SERVICE_SHARE_MAX": "8"}),
+                                       (5, {"RDC_HOST_SERVICE_SHARE_MAX": "8"}),
+                                       (7, {"RDC_HOST_SERVICE_SHARE_MAX": "8",
+                                            "rdc_reduce_ring_mincount": "2K"})])
 def test_mp_host_small_service(world, env):
     """Small synchronous HOST allreduces (cfg1's path) through the resident
     service block (rdc_service.h): 12 calls of 1 B - 64 KiB over 8 (dtype, op)
@@ -440,7 +443,8 @@ def test_mp_host_small_service(world, env):
         pytest.skip("no GPU")
     cases = [{"count": 0, "dtype": 6, "op": 2, "kind": "host_mix", "ops": HOST_MIX}]
     tmp = run_mp(world, cases, env_extra=env)
-    mincount = 8 << 10 if "rdc_reduce_ring_mincount" in env else 1
+    mc = env.get("rdc_reduce_ring_mincount", "1")
+    mincount = int(mc[:-1]) << 10 if mc.endswith("K") else int(mc)
     want = expected_host_mix(world, mincount)
     for r in range(world):
         got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
