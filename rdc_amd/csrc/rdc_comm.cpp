@@ -77,7 +77,7 @@ struct PeerInfo {
     uint64_t p2p_slot_bytes;
     int32_t num_cus;
     int32_t pad2;
-    uint64_t plan[12];  // PlanKey: the parameters that shape a launch plan (must agree)
+    uint64_t plan[14];  // PlanKey: the parameters that shape a launch plan (must agree)
     char host[64];
     char pci[32];  // physical GPU (ranks may share one: tests, emulation)
 };
@@ -94,17 +94,23 @@ struct Handles {  // round 2 of Create: IPC handles (scratch ones only for a new
 // data lands by byte offset, so ranks that planned differently would read
 // contributions that have not landed (silent wrong bits, not a timeout).
 // Every parameter a plan depends on is exchanged at creation and compared.
+// The small-allreduce service's switches too: a rank that serves a small host
+// buffer through it while a peer launches a kernel would wait out RDC_TIMEOUT.
+constexpr int kPlanKeys = 14;
 void PlanKey(const CommConfig& c, uint64_t* k) {
-    const uint64_t v[12] = {(uint64_t)c.algo, (uint64_t)c.max_blocks, (uint64_t)c.tile_bytes,
-                            (uint64_t)c.oneshot_push_max, (uint64_t)c.fuse_bytes, (uint64_t)c.coalesce_fused,
-                            (uint64_t)c.fuse_bytes_direct, (uint64_t)c.bcast_split_bytes, (uint64_t)c.mesh_split.s16,
-                            (uint64_t)c.mesh_split.r16, (uint64_t)c.ring_mincount, (uint64_t)c.scratch_bytes};
+    const uint64_t v[kPlanKeys] = {(uint64_t)c.algo, (uint64_t)c.max_blocks, (uint64_t)c.tile_bytes,
+                                   (uint64_t)c.oneshot_push_max, (uint64_t)c.fuse_bytes, (uint64_t)c.coalesce_fused,
+                                   (uint64_t)c.fuse_bytes_direct, (uint64_t)c.bcast_split_bytes,
+                                   (uint64_t)c.mesh_split.s16, (uint64_t)c.mesh_split.r16, (uint64_t)c.ring_mincount,
+                                   (uint64_t)c.scratch_bytes, (uint64_t)SmallService::Enabled(),
+                                   (uint64_t)SmallService::ShareMax()};
     memcpy(k, v, sizeof(v));
 }
-const char* kPlanKeyNames[12] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES",
-                                 "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT", "RDC_BCAST_SPLIT_BYTES",
-                                 "RDC_MESH_SPLIT", "RDC_MESH_SPLIT", "rdc_reduce_ring_mincount",
-                                 "RDC_SCRATCH_BYTES"};
+const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_ONESHOT_BYTES",
+                                        "RDC_FUSE_BYTES", "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT",
+                                        "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "RDC_MESH_SPLIT",
+                                        "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES", "RDC_HOST_SERVICE",
+                                        "RDC_HOST_SERVICE_SHARE_MAX"};
 
 // The point-to-point control block (rdc_p2p.h) in POSIX shared memory: rank 0
 // creates it, every rank maps it, rank 0 unlinks the name once all mapped.
@@ -402,7 +408,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         if (q.slot_bytes != mine.slot_bytes || q.max_tiles != mine.max_tiles ||
             q.p2p_slot_bytes != mine.p2p_slot_bytes)
             throw std::runtime_error("rdc: ranks disagree on scratch size (set RDC_SCRATCH_BYTES identically)");
-        for (int k = 0; k < 12; ++k)
+        for (int k = 0; k < kPlanKeys; ++k)
             if (q.plan[k] != mine.plan[k])
                 throw std::runtime_error(std::string("rdc: rank ") + std::to_string(p) + " and rank " +
                                          std::to_string(c->rank_) + " disagree on " + kPlanKeyNames[k] + " (" +

@@ -816,3 +816,42 @@ def test_missing_peer_times_out_instead_of_hanging(algo):
     finally:
         for c in g:
             c.destroy()
+
+
+_PLAN_SNIPPET = r"""
+import os, sys
+sys.path.insert(0, %r)
+import rdc_amd
+rank, world, port = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+rdc_amd.init(["RDC_RANK=%%d" %% rank, "RDC_WORLD_SIZE=%%d" %% world, "RDC_TRACKER_PORT=%%d" %% port,
+              "RDC_TRACKER_URI=127.0.0.1"])
+try:
+    rdc_amd.get_comm("main")
+    print("NOERROR", flush=True)
+except Exception as e:  # the expected path
+    print("ERR:", e, flush=True)
+"""
+
+
+@pytest.mark.parametrize("key,value", [("RDC_TILE_BYTES", "1M"), ("RDC_HOST_SERVICE", "0"),
+                                       ("RDC_HOST_SERVICE_SHARE_MAX", "2")])
+def test_mp_plan_disagreement_is_refused(key, value):
+    """Ranks whose launch-plan parameters differ (one rank's env) are refused
+    at communicator creation with the parameter named, on every rank: a
+    mismatch would otherwise read contributions that never landed, or leave a
+    rank waiting in the small-allreduce service while its peer launched a
+    kernel (rdc_comm.cpp PlanKey)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    port = free_port()
+    base = dict(os.environ, RDC_DEVICE="0", RDC_SCRATCH_BYTES="64M")
+    procs = []
+    for r in range(2):
+        env = dict(base)
+        if r == 1:
+            env[key] = value
+        procs.append(subprocess.Popen([sys.executable, "-c", _PLAN_SNIPPET % ROOT, str(r), "2", str(port)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = [p.communicate(timeout=120)[0].decode(errors="replace") for p in procs]
+    for r, o in enumerate(outs):
+        assert "ERR:" in o and ("disagree on " + key) in o, "rank %d:\n%s" % (r, o[-2000:])
