@@ -6,21 +6,26 @@
 // kernel's completion before the caller sees its result (DESIGN.md §5.3:
 // 14.6 us for a 4 KiB allreduce of device memory at n = 2, 17.4 us from host
 // memory).  Here each rank keeps ONE resident block (k_svc) while calls keep
-// coming: the host copies its input into a pinned, GPU-uncached mailbox and
-// posts one request word (seq, bytes, tree); the block, polling that word,
-// reads the input once over PCIe and stores it as LL words (4 payload bytes +
-// the request's sequence number per 8) into its slot of every peer's service
-// region (xGMI); each thread then polls the peers' words for its own vectors,
-// folds every element in the reference's order (Split chunk ring order, or
-// the tree's order below rdc_reduce_ring_mincount) in registers, writes the
-// result straight into the mailbox, and the block bumps `done`.
+// coming.  The host writes its input into a pinned, GPU-uncached mailbox —
+// up to RDC_HOST_SERVICE_LL_BYTES as LL words (4 payload bytes + the request's
+// sequence number per 8, planar) — and then one header word (seq, tree order,
+// LL input, LL result, bytes).  The block polls the header together with the
+// first 4 KiB of LL input (so a small request's data usually arrives with the
+// poll that finds it), stores its input as LL words into its slot of every
+// peer's service region (xGMI), then each thread polls the peers' words for
+// its own vectors, folds every element in the reference's order (Split chunk
+// ring order, or the tree's order at or below rdc_reduce_ring_mincount)
+// through LDS, and writes the result into the mailbox: as LL words the host
+// polls (<= 256 B), or as is, drained, followed by `done`.
 //
 // The block exits after RDC_HOST_SERVICE_IDLE_US (default 1000) without a
 // request, when the host sets `stop` (another (dtype, op), teardown) or when
 // a peer never arrives (RDC_TIMEOUT): nothing stays resident, and a
 // device-wide synchronisation waits at most the idle time.  The next call
-// relaunches it.  Its slots and arrival words are its own (not the channel's
-// scratch), so it never races the channel's stream-ordered launches.
+// relaunches it (state EXITING closes the race with a request posted while it
+// leaves: host store header / load state, device store state / fence / load
+// header).  Its slots are its own, not the channel's scratch, so it never
+// races the channel's stream-ordered launches.
 // RDC_HOST_SERVICE=0 disables it; with more than RDC_HOST_SERVICE_SHARE_MAX
 // (default 4) ranks on one GPU it is not used (their persistent blocks'
 // queues get time-sliced by the hardware scheduler).
@@ -67,7 +72,7 @@ private:
     uint32_t req_ = 0;
     int wall_khz_ = 100000;
     uint64_t ll_bytes_ = RDC_SVC_LL_MAX;  // LL input up to this many bytes
-    uint64_t ll_out_bytes_ = 0;           // LL result up to this many bytes
+    uint64_t ll_out_bytes_ = 0;           // LL result up to this many bytes (set from the env in the ctor)
     // 8-byte LL word of payload word j in the planar layout (k_svc)
     static uint64_t ll_index(uint64_t j) { return ((j >> 1) & 1) * (RDC_SVC_LL_MAX / 8) + 2 * (j >> 2) + (j & 1); }
     std::vector<uint64_t> stage_ = std::vector<uint64_t>(RDC_SVC_LL_MAX / 4);  // LL input words, built here
