@@ -14,7 +14,7 @@ def make_plan(seed, nops, world):
     rng = random.Random(seed)
     plan = []
     for k in range(nops):
-        kind = rng.choice(["allreduce", "allreduce", "bcast", "allgather", "coalesced"])
+        kind = rng.choice(["allreduce", "allreduce", "bcast", "allgather", "coalesced", "host"])
         s = 0x5EED0000 + 1000 * k
         if kind == "allreduce":
             dt, op = rng.choice(PAIRS)
@@ -26,6 +26,10 @@ def make_plan(seed, nops, world):
                          "root": rng.randrange(world), "seed": s})
         elif kind == "allgather":
             plan.append({"kind": kind, "sizes": [rng.choice([0, 3, 64, 5000, 70001]) for _ in range(world)],
+                         "seed": s})
+        elif kind == "host":  # synchronous, host buffer: the small-allreduce service or the launch path
+            dt, op = rng.choice(PAIRS)
+            plan.append({"kind": kind, "count": rng.choice([1, 7, 1000, 4099, 16384, 20000]), "dtype": dt, "op": op,
                          "seed": s})
         else:
             dt, op = rng.choice([(6, 2), (2, 0), (10, 2)])
@@ -39,7 +43,7 @@ def output_bytes(plan):
     """Total bytes of every op's outputs, in the worker's order."""
     tot = 0
     for op in plan:
-        if op["kind"] == "allreduce":
+        if op["kind"] in ("allreduce", "host"):
             tot += op["count"] * ESZ[op["dtype"]]
         elif op["kind"] == "bcast":
             tot += op["bytes"]
@@ -58,7 +62,7 @@ def expected(plan, world):
     parts = []
     for op in plan:
         kind = op["kind"]
-        if kind == "allreduce":
+        if kind in ("allreduce", "host"):
             xs = [O.fill(op["count"], op["dtype"], op["seed"], r) for r in range(world)]
             parts.append(np.frombuffer(O.expected_allreduce(xs, op["dtype"], op["op"]).tobytes(), np.uint8))
         elif kind == "bcast":

@@ -3,7 +3,9 @@ tests/test_gpu_mixed.py): a seeded sequence of allreduce (every schedule),
 broadcast (rotating roots, direct and forwarded), variable-size allgather and
 coalesced allreduce launches on ONE communicator and ONE stream with no host
 synchronisation in between, so consecutive launches of different kinds
-overlap across ranks the way a training step issues them.  Every op has its
+overlap across ranks the way a training step issues them; synchronous
+host-buffer allreduces (the small-allreduce service, or the launch path above
+64 KiB) run in between while earlier launches may still be in flight.  Every op has its
 own output buffers; all are saved at the end for the parent to check against
 the CPU oracle.
 
@@ -49,6 +51,11 @@ def main():
             check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(t.data_ptr()), n, dt, op["op"],
                                                op["algo"], sp))
             outs.append((t, n * ESZ[dt]))
+        elif kind == "host":
+            from oracle import oracle as O  # the checker's generator (same bits as RdcFill)
+            h = O.fill(op["count"], op["dtype"], op["seed"], rank).copy()
+            check_call(_LIB.RdcAllreduce(ctypes.c_void_p(h.ctypes.data), op["count"], op["dtype"], op["op"], None, None))
+            outs.append((h, h.nbytes))
         elif kind == "bcast":
             nb = op["bytes"]
             t = dev(nb)
@@ -74,7 +81,8 @@ def main():
                                                       sp))
             outs.extend((x, c * ESZ[dt]) for x, c in zip(ts, counts))
     comm.check(sp)
-    blob = np.concatenate([t[:nb].cpu().numpy() for t, nb in outs]) if outs else np.zeros(0, np.uint8)
+    blob = np.concatenate([np.frombuffer(t.tobytes(), np.uint8) if isinstance(t, np.ndarray) else t[:nb].cpu().numpy()
+                           for t, nb in outs]) if outs else np.zeros(0, np.uint8)
     np.save(os.path.join(outdir, "mixed_rank%d.npy" % rank), blob)
     print("rank %d: mixed OK" % rank, flush=True)
     rdc_amd.finalize()
