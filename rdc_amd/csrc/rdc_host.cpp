@@ -24,7 +24,7 @@ int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 constexpr size_t kPieceTarget = (size_t)16 << 20;  // bytes of all chunks' slices per piece
-constexpr size_t kParallelMin = (size_t)1 << 20;   // below this a copy runs on the caller alone
+constexpr size_t kParallelMin = (size_t)512 << 10;  // below this a copy runs on the caller alone (waking the pool costs more)
 // RDC_HOST_TRACE=1: per-piece timeline on stderr (diagnostics)
 double trace_now() {
     timespec t;
@@ -36,76 +36,6 @@ bool tracing() {
     return on;
 }
 }  // namespace
-
-// ---------------------------------------------------------------- CopyPool --
-CopyPool::CopyPool(int threads) {
-    for (int i = 0; i < threads; ++i) th_.emplace_back([this] { Loop(); });
-}
-
-CopyPool::~CopyPool() {
-    {
-        std::lock_guard<std::mutex> lk(mu_);
-        stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-}
-
-void CopyPool::Loop() {
-    uint64_t seen = 0;
-    for (;;) {
-        const std::function<void(int)>* job;
-        {
-            std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-            if (stop_) return;
-            seen = gen_;
-            job = job_;
-        }
-        for (;;) {
-            int i;
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                if (next_ >= total_) break;
-                i = next_++;
-            }
-            (*job)(i);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (++finished_ == total_) done_cv_.notify_all();
-        }
-    }
-}
-
-void CopyPool::Run(int n, const std::function<void(int)>& f) {
-    if (n <= 0) return;
-    if (th_.empty() || n == 1) {
-        for (int i = 0; i < n; ++i) f(i);
-        return;
-    }
-    {
-        std::lock_guard<std::mutex> lk(mu_);
-        job_ = &f;
-        next_ = 0;
-        total_ = n;
-        finished_ = 0;
-        ++gen_;
-    }
-    cv_.notify_all();
-    for (;;) {  // the caller works too
-        int i;
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            if (next_ >= total_) break;
-            i = next_++;
-        }
-        f(i);
-        std::lock_guard<std::mutex> lk(mu_);
-        if (++finished_ == total_) done_cv_.notify_all();
-    }
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return finished_ == total_; });
-    job_ = nullptr;
-}
 
 // ---------------------------------------------------------------- HostPath --
 HostPath::HostPath(int device, size_t zc_max)
@@ -132,6 +62,7 @@ HostPath::~HostPath() {
     }
     for (hipEvent_t e : ar_done_) (void)hipEventDestroy(e);
     if (pin_small_) (void)hipHostFree(pin_small_);
+    if (small_done_) (void)hipEventDestroy(small_done_);
     if (dev_small_) (void)hipFree(dev_small_);
     if (dev_) (void)hipFree(dev_);
     if (h2d_) (void)hipStreamDestroy(h2d_);
@@ -230,7 +161,7 @@ void HostPath::AllreduceSmall(Communicator* c, char* h, size_t count, size_t S, 
                   "hipHostGetDevicePointer");
         hip_check(hipMalloc(reinterpret_cast<void**>(&dev_small_), kSmall), "hipMalloc");
     }
-    memcpy(pin_small_, h, S);
+    Copy(pin_small_, h, S);
     if (S <= zc_max_) {
         // the launch's last block stores a token into pinned memory: spin on
         // it instead of a stream sync (Communicator::ArmNotify / WaitNotify)
@@ -242,15 +173,24 @@ void HostPath::AllreduceSmall(Communicator* c, char* h, size_t count, size_t S, 
             throw;
         }
         c->WaitNotify(token, comm_stream);
-        memcpy(h, pin_small_, S);
+        Copy(h, pin_small_, S);
         return;
     }
     hip_check(hipMemcpyAsync(dev_small_, pin_small_, S, hipMemcpyHostToDevice, comm_stream), "H2D");
     c->Allreduce(dev_small_, count, dtype, op, comm_stream);
     hip_check(hipMemcpyAsync(pin_small_, dev_small_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
-    hip_check(hipStreamSynchronize(comm_stream), "sync");
+    // spin on the D2H's completion (a blocking synchronisation may sleep and
+    // pay a wake-up per call)
+    if (!small_done_) hip_check(hipEventCreateWithFlags(&small_done_, hipEventDisableTiming), "event");
+    hip_check(hipEventRecord(small_done_, comm_stream), "record");
+    for (;;) {
+        const hipError_t q = hipEventQuery(small_done_);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) hip_check(q, "D2H completion");
+        __builtin_ia32_pause();
+    }
     c->RaiseIfError(c->HostErrorWord());
-    memcpy(h, pin_small_, S);
+    Copy(h, pin_small_, S);
 }
 
 void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, int op, hipStream_t comm_stream) {

@@ -25,27 +25,12 @@
 #include <vector>
 
 #include "rdc_comm.h"
+#include "rdc_copypool.h"
 
 namespace rdc_amd {
 
 // fixed pool of memcpy threads; Run(n, f) calls f(0..n-1) across the pool
 // and the caller, returning when all are done
-class CopyPool {
-public:
-    explicit CopyPool(int threads);
-    ~CopyPool();
-    void Run(int n, const std::function<void(int)>& f);
-
-private:
-    void Loop();
-    std::vector<std::thread> th_;
-    std::mutex mu_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(int)>* job_ = nullptr;
-    int next_ = 0, total_ = 0, finished_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
 
 class HostPath {
 public:
@@ -74,6 +59,7 @@ private:
     int device_;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
     char* pin_small_ = nullptr;      // kSmall bytes + the error word
+    hipEvent_t small_done_ = nullptr;  // the staged small path's D2H
     char* pin_small_dev_ = nullptr;  // its device address
     size_t zc_max_ = 0;
     char* dev_small_ = nullptr;
