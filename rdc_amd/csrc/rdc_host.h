@@ -60,6 +60,7 @@ private:
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
     char* pin_small_ = nullptr;      // kSmall bytes + the error word
     hipEvent_t small_done_ = nullptr;  // the staged small path's D2H
+    static void SpinEvent(hipEvent_t e, const char* what);
     char* pin_small_dev_ = nullptr;  // its device address
     size_t zc_max_ = 0;
     char* dev_small_ = nullptr;
