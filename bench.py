@@ -528,6 +528,11 @@ def main():
         sync_check(comm, sp, dist, torch)
     wall = t1 - t0
     kern_ms = e0.elapsed_time(e1) / args.steps
+    timed_algo = None
+    if world > 1:  # the schedule the library chose for the timed launches
+        ll = (ctypes.c_uint64 * 6)()
+        if _LIB.RdcCommLastLaunch(comm.handle, ll) == 0:
+            timed_algo = {1: "ring", 2: "mesh", 3: "oneshot", 4: "tree"}.get(int(ll[5]))
     if world > 1:
         tt = torch.tensor([wall, kern_ms], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -627,9 +632,8 @@ def main():
         value = S / (wall / args.steps) / 1e9 * 2 * (world - 1) / world
         busbw = algbw * 2 * (world - 1) / world
         algo_name = args.algo
-        if algo_name == "auto":  # the library's own choice (rdc_plan.cpp OneshotEligible, 1 MiB push budget)
-            unit = S // args.buckets if args.unfused else min(S, 256 << 20)
-            algo_name = "oneshot" if unit * (world - 1) <= (1 << 20) else "mesh"
+        if algo_name == "auto":  # the schedule the library launched in the timed region (RdcCommLastLaunch)
+            algo_name = timed_algo or "mesh"
         peak = XGMI_LINK_DIR_GBPS * (1 if algo_name == "ring" else (world - 1))
         roof = {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 1), "unit": "GB/s",
                 "frac": round(busbw / peak, 4), "traffic": None,

@@ -157,7 +157,10 @@ int RdcCommIRecv(void** wc, void* comm, void* buf, size_t bytes, int src, void* 
 int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op, void* stream);
 /* algo: 0 auto, 1 ring (the reference schedule), 2 mesh (all links), 3 one-shot (small buffers:
  * every rank pushes the whole buffer to every peer, one hand-off); auto = one-shot when
- * (n-1) x bytes <= RDC_ONESHOT_BYTES (default 1 MiB), else mesh.  All bit-identical.
+ * the one-shot while bytes <= 8 MiB and its extra egress over the mesh,
+ * (n-1)(n-2)/n x bytes, is <= 4 MiB (n = 2: 8 MiB, n = 8: 0.76 MiB; with
+ * RDC_ONESHOT_BYTES set: while (n-1) x bytes <= it), else the ring at n = 2
+ * and the mesh from n = 3.  All bit-identical.
  * Whatever the algo, a buffer of at most rdc_reduce_ring_mincount bytes (default 1) takes
  * the reference's TREE order (TryAllreduce, src/comm/communicator_collective.cc:6-13: the
  * fold of TryReduceTree to rank 0, every rank receiving the root's bits) as one one-shot
@@ -256,6 +259,11 @@ int RdcPlanResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu)
  * dst/src hold >= 16 ints.  Returns n-1, or -1 on bad arguments. */
 int RdcPlanTree(int n, int* dst, int* src);
 int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4);
+/* The automatic schedule for an allreduce of `bytes` over n ranks: returns
+ * RDC_ALGO_ONESHOT (3), RDC_ALGO_RING (1, n = 2 beyond the one-shot) or
+ * RDC_ALGO_MESH (2) (negative on bad arguments).
+ * oneshot_bytes = RDC_ONESHOT_BYTES (0 = the default size / rank-aware rule). */
+int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_bytes);
 int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int algo, size_t tile_bytes,
                      int max_blocks, uint64_t* out, int max_pieces, int* out_pieces);
 

@@ -73,6 +73,7 @@ def _load():
         "RdcFill": (i, [vp, sz, i, u64, i, vp]),
         "RdcMemcpy": (i, [vp, vp, sz]),
         "RdcPlanLayout": (i, [i, sz, ctypes.POINTER(u64)]),
+        "RdcPlanAutoAlgo": (i, [i, sz, sz, sz]),
         "RdcPlanAllreduce": (i, [i, sz, i, sz, i, sz, i, ctypes.POINTER(u64), i, ctypes.POINTER(ctypes.c_int)]),
         "RdcAllreduceCoalesced": (i, [pvp, ctypes.POINTER(sz), i, i, i]),
         "RdcAllreduceCoalescedOn": (i, [vp, pvp, ctypes.POINTER(sz), i, i, i]),

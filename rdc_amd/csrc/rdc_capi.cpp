@@ -692,6 +692,16 @@ int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4) {
     });
 }
 
+int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_bytes) {
+    int algo = -1;
+    const int rc = guard([&] {
+        if (n < 1 || n > RDC_MAX_RANKS) throw std::invalid_argument("rdc: bad argument");
+        const Layout L = MakeLayout(n, scratch_bytes ? scratch_bytes : CommConfig().scratch_bytes);
+        algo = AutoAlgo(n, bytes, L, oneshot_bytes);
+    });
+    return rc != 0 ? rc : algo;
+}
+
 int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int algo, size_t tile_bytes,
                      int max_blocks, uint64_t* out, int max_pieces, int* out_pieces) {
     return guard([&] {

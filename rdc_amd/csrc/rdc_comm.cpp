@@ -626,7 +626,7 @@ int Communicator::PickAlgo(int algo) const {
 int Communicator::PickAlgo(int algo, uint64_t bytes) const {
     if (algo == RDC_ALGO_AUTO) algo = cfg_.algo;
     if (algo == RDC_ALGO_AUTO)
-        algo = OneshotEligible(n_, bytes, layout(), cfg_.oneshot_push_max) ? RDC_ALGO_ONESHOT : RDC_ALGO_MESH;
+        algo = AutoAlgo(n_, bytes, layout(), cfg_.oneshot_push_max);
     if (algo == RDC_ALGO_ONESHOT && !OneshotEligible(n_, bytes, layout(), (uint64_t)-1))
         algo = RDC_ALGO_MESH;  // does not fit half a slot
     return algo;
@@ -976,7 +976,11 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
                 bytes += (uint64_t)counts[b] * esz;
                 live += counts[b] != 0;
             }
-            if (live >= 2 && PickAlgo(algo, bytes) == RDC_ALGO_MESH) {
+            // auto picks the ring at n = 2, but a list is faster through the
+            // unit-table mesh (no staging image) than staged through the ring
+            const int pick = PickAlgo(algo, bytes);
+            const bool automatic = algo == RDC_ALGO_AUTO && cfg_.algo == RDC_ALGO_AUTO;
+            if (live >= 2 && (pick == RDC_ALGO_MESH || (automatic && pick == RDC_ALGO_RING))) {
                 const PackEntry& e = PackTable(bufs + b0, counts + b0, b1 - b0, esz, stream);
                 LaunchRanges(ks, nullptr, e.off, e.len, e.total, esz, RDC_ALGO_MESH, stream, e.dtable, e.nunits);
             } else {

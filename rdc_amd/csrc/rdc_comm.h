@@ -31,7 +31,7 @@ struct CommConfig {
     int max_blocks = 0;                      // 0 = auto
     size_t tile_bytes = 0;                   // 0 = auto
     double timeout_s = 60.0;                 // device-side wait limit
-    size_t oneshot_push_max = (size_t)1 << 20;  // auto picks one-shot when (n-1) x bytes <= this
+    size_t oneshot_push_max = 0;  // RDC_ONESHOT_BYTES: 0 = size/rank-aware rule (rdc_plan.h OneshotAuto)
     size_t fuse_bytes = (size_t)256 << 20;      // coalesced allreduce: data bytes per fusion group
     size_t p2p_slot_bytes = (size_t)4 << 20;    // Send/Recv: piece size (2 slots per ordered rank pair)
     bool coalesce_fused = true;                 // coalesced mesh reads/writes user buffers directly (no image)

@@ -131,6 +131,24 @@ bool OneshotEligible(int n, uint64_t bytes, const Layout& L, uint64_t push_max) 
     return n > 1 && bytes > 0 && bytes <= OneshotHalfBytes(L) && bytes * (uint64_t)(n - 1) <= push_max;
 }
 
+bool OneshotAuto(int n, uint64_t bytes, const Layout& L, uint64_t push_max) {
+    if (push_max) return OneshotEligible(n, bytes, L, push_max);  // RDC_ONESHOT_BYTES given: (n-1) x S <= it
+    if (!OneshotEligible(n, bytes, L, ~(uint64_t)0)) return false;
+    // the one-shot pushes (n-1) x S per rank where the mesh pushes 2(n-1)/n x S,
+    // and hands off once instead of twice: worth it while the extra egress
+    // (n-1)(n-2)/n x S stays small, and while S is small enough that fixed
+    // costs, not bandwidth, decide (n = 2: no extra bytes at all)
+    const uint64_t extra = bytes * (uint64_t)(n - 1) * (uint64_t)(n - 2) / (uint64_t)n;
+    return bytes <= kOneshotAutoMaxBytes && extra <= kOneshotAutoExtraBytes;
+}
+
+int AutoAlgo(int n, uint64_t bytes, const Layout& L, uint64_t push_max) {
+    if (OneshotAuto(n, bytes, L, push_max)) return RDC_ALGO_ONESHOT;
+    // two ranks: one link either way, and the ring's two steps hand off less
+    // than the mesh's three roles; the mesh's all-links egress pays from n = 3
+    return n == 2 ? RDC_ALGO_RING : RDC_ALGO_MESH;
+}
+
 Piece PlanOneshot(int n, uint64_t count, size_t esz, const Layout& L, size_t cfg_tile, int max_blocks) {
     int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
     SplitRanges((int64_t)count, n, cb, ce);

@@ -68,6 +68,21 @@ std::vector<Piece> PlanAllreduce(int n, uint64_t count, size_t esz, const Layout
 // push_max.  off/len = the Split chunk byte ranges; tiles[0] tiles over the
 // whole buffer; nb_scatter = grid.
 bool OneshotEligible(int n, uint64_t bytes, const Layout& L, uint64_t push_max);
+// The automatic choice between one-shot and mesh.  push_max != 0
+// (RDC_ONESHOT_BYTES set): one-shot while (n-1) x bytes <= push_max.  0: one-
+// shot while bytes <= kOneshotAutoMaxBytes and the extra egress over the mesh,
+// (n-1)(n-2)/n x bytes, <= kOneshotAutoExtraBytes — n = 2: up to 8 MiB, n = 3:
+// 6 MiB, n = 4: 2.7 MiB, n = 8: 0.76 MiB.  Measured with 2-4 ranks on one GPU
+// (tools/algo_sweep.py, profiles/r02/algo_sweep_*.log): the one-shot is the
+// fastest schedule up to 8 MiB at n = 2 (1.6x the mesh at 2-8 MiB) and up to
+// 8-16 MiB at n = 3, 4.
+constexpr uint64_t kOneshotAutoMaxBytes = (uint64_t)8 << 20;
+constexpr uint64_t kOneshotAutoExtraBytes = (uint64_t)4 << 20;
+bool OneshotAuto(int n, uint64_t bytes, const Layout& L, uint64_t push_max);
+// RDC_ALGO=auto: the one-shot by OneshotAuto, else the ring at n = 2 (one link
+// either way; measured 16 MiB 0.028 vs 0.036 ms, 1 GiB 1.71 vs 1.74 ms with 2
+// ranks on one GPU) and the mesh from n = 3 (all n-1 links)
+int AutoAlgo(int n, uint64_t bytes, const Layout& L, uint64_t push_max);
 uint64_t OneshotHalfBytes(const Layout& L);
 Piece PlanOneshot(int n, uint64_t count, size_t esz, const Layout& L, size_t cfg_tile, int max_blocks);
 

@@ -210,3 +210,27 @@ def test_resident_grid_never_oversubscribes():
         g = _LIB.RdcPlanResidentGrid(want, per_cu, cus, share)
         assert 1 <= g <= want
         assert g == want or g * share <= per_cu * cus or g == 1
+
+
+def test_auto_schedule_oneshot_vs_mesh():
+    """rdc_plan.h OneshotAuto: one-shot while bytes <= 8 MiB and its extra
+    egress over the mesh, (n-1)(n-2)/n x bytes, is <= 4 MiB; with
+    RDC_ONESHOT_BYTES given, while (n-1) x bytes <= it."""
+    from rdc_amd._lib import _LIB
+    ONESHOT, MESH, RING = 3, 2, 1
+    M = 1 << 20
+    scratch = 4080 * M
+
+    def pick(n, b, ob=0):
+        return _LIB.RdcPlanAutoAlgo(n, b, scratch, ob)
+    # n = 2: the one-shot moves no more bytes than the mesh -> up to 8 MiB
+    assert pick(2, 4) == ONESHOT and pick(2, 8 * M) == ONESHOT and pick(2, 8 * M + 4) == RING
+    # n = 3: extra = S * 2/3 <= 4 MiB -> S <= 6 MiB
+    assert pick(3, 6 * M) == ONESHOT and pick(3, 6 * M + 3 * 4096) == MESH
+    # n = 8: extra = S * 42/8 <= 4 MiB -> S <= 798,915 bytes
+    assert pick(8, 798912) == ONESHOT and pick(8, 800 * 1024) == MESH
+    # explicit RDC_ONESHOT_BYTES keeps the push-budget rule
+    assert pick(8, 149792, M) == ONESHOT and pick(8, 150000, M) == MESH
+    assert pick(2, 2 * M, M) == RING
+    # never beyond half a slot, never for one rank; n = 2 beyond it: the ring
+    assert pick(2, 1 << 40) == RING and pick(4, 1 << 40) == MESH and pick(1, 4096) == MESH
