@@ -431,7 +431,7 @@ def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
         out[key] = round(per_target * ntarget / (float(t[0]) * 1e-3) / 1e9, 2)
         dist.barrier()
     out["bytes_per_target"] = per_target
-    out["kernel"] = "k_push (block_copy, 16-B non-temporal lanes; push = remote stores, pull = remote loads)"
+    out["kernel"] = "k_push (block_copy, 16-B lanes; push = write-through (sc0 sc1) remote stores, pull = remote loads)"
     return out
 
 

@@ -8,14 +8,18 @@
 //        BitOR: dst = dst | src
 //    f16: native v_add_f16 (correctly rounded); bf16: f32 add + RNE to bf16.
 //  * 16-byte vector reduce (v4u reinterpreted as 16/sizeof(T) lanes)
-//  * cross-GPU hand-off: payload stores -> every wave's vmcnt(0) -> barrier ->
-//    one lane: system-scope release fence, asm vmcnt(0), relaxed system-scope
-//    flag store.  Consumer: one lane per flag polls relaxed/system, then a
-//    system-scope acquire fence, vmcnt(0), barrier (MI355X_MICROARCH.md
-//    "Workgroup dispatch ... visibility"; cdna_hip_programming.md G16).
+//  * cross-GPU hand-off: write-through (sc0 sc1) payload stores into the
+//    peer's scratch -> every wave's vmcnt(0) -> barrier -> one lane: relaxed
+//    system-scope flag store (plus a system-scope release fence when the
+//    scratch is not uncached).  Consumer: one lane per flag polls
+//    relaxed/system, barrier, loads of its own uncached scratch (an acquire
+//    fence when it is not uncached) (MI355X_MICROARCH.md "Workgroup dispatch
+//    ... visibility"; cdna_hip_programming.md G16).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "rdc_common.h"
 
@@ -121,6 +125,44 @@ __device__ __forceinline__ void st16_nt(void* p, v4u v) {
     __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
 }
 
+// Write-through stores for bytes a PEER reads (its IPC-mapped scratch, over
+// xGMI on a multi-GPU node).  `sc0 sc1` (system scope) stores leave no copy in
+// this XCD's L2, so once the storing wave's vmcnt has drained they are at the
+// target's memory whatever memory type the IPC import was mapped with (MTYPE
+// UC if the driver carries the exporter's uncached flag over, NC — L2-cached,
+// written back only by a system release — if it does not).  Plain or `nt`
+// stores would depend on that mapping (MI355X_MICROARCH.md visibility table:
+// `nt` is not write-through).  16-B form: buffer store with aux = sc0|sc1 from
+// a wave-uniform base (cdna_hip_programming.md T8/T20); narrow form: relaxed
+// system-scope atomic stores (global_store_{byte,short,dword,dwordx2} sc0 sc1).
+constexpr int kWtAux = 1 | 16;  // CPol SC0 | SC1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+    const uint64_t b = (uint64_t)(uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0xffffffffu, 0x00020000);
+}
+// 16 bytes at base + off (off < 4 GiB; base wave-uniform)
+__device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, v4u v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kWtAux);
+}
+template <typename W>
+__device__ __forceinline__ void st_wt(W* p, W v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// one element of type T (any 1/2/4/8-byte type) written through
+template <typename T>
+__device__ __forceinline__ void st_elem_wt(void* p, T v) {
+    typedef typename std::conditional<sizeof(T) == 1, uint8_t,
+            typename std::conditional<sizeof(T) == 2, uint16_t,
+            typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type>::type>::type W;
+    st_wt(reinterpret_cast<W*>(p), __builtin_bit_cast(W, v));
+}
+
+// Where a block_copy writes: this GPU's own memory (user buffers, local
+// slots: streaming `nt` stores) or a peer's scratch (write-through, above).
+enum { kDstLocal = 0, kDstPeer = 1 };
+
 // ------------------------------------------------------------- hand-off ----
 __device__ __forceinline__ uint32_t flag_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -132,15 +174,16 @@ __device__ __forceinline__ bool seq_reached(uint32_t v, uint32_t seq) { return (
 
 // Called by EVERY thread of the block after its payload stores.  Lanes
 // 0..nflags-1 of wave 0 then store flags[i] = seq.
-// Every hand-off payload lives in the peers' scratch slots.  When all scratch
-// is uncached (MTYPE UC, hipDeviceMallocUncached: `uc`), those stores are
-// write-through — no XCD's L2 keeps them — and every storing wave's
-// `s_waitcnt vmcnt(0)` (before the barrier) means they have been performed
-// at memory: the write-through + drained-flag form of MI355X_MICROARCH.md
-// ("Valid forms", R1), with uncached memory in place of `sc1` stores.  The
-// system-scope release fence would only add an L2 write-back (buffer_wbl2
-// sc0 sc1, 1.7-6.5 us per call) of cached lines no peer reads, so it is
-// issued only for fine- / coarse-grained scratch (alloc fallbacks).
+// Every hand-off payload lives in the peers' scratch slots and is stored
+// write-through (st16_wt / block_copy<kDstPeer>: sc0 sc1), so every storing
+// wave's `s_waitcnt vmcnt(0)` (before the barrier) means it has been
+// performed at the owner's memory: the write-through + drained-flag form of
+// MI355X_MICROARCH.md ("Valid forms", R1) at system scope.  When the scratch
+// is uncached (MTYPE UC, hipDeviceMallocUncached: `uc`) the owner's loads
+// never hit a stale line either, and the system-scope release fence would
+// only add an L2 write-back (buffer_wbl2 sc0 sc1, 1.7-6.5 us per call) of
+// cached lines no peer reads, so it is issued only for fine- / coarse-grained
+// scratch (alloc fallbacks).
 __device__ __forceinline__ void block_publish(uint32_t* const* flags, int nflags, uint32_t seq, int uc) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -222,7 +265,16 @@ __device__ __forceinline__ bool block_wait(uint32_t* const* flags, int nflags, u
 // not 16-B aligned takes the narrow path (units of the widest common
 // alignment), still exact.
 
-// dst[i] = src[i], dst and src congruent mod 16
+template <int DST, typename W>
+__device__ __forceinline__ void put_word(W* p, W v) {
+    if (DST == kDstPeer) st_wt(p, v);
+    else *p = v;
+}
+
+// dst[i] = src[i], dst and src congruent mod 16.  The 16-B body walks windows
+// of U x blockDim vectors; the window base is wave-uniform, so a peer
+// destination gets one buffer descriptor per window (offsets < 4 GiB).
+template <int DST>
 __device__ __forceinline__ void block_copy_vec(char* __restrict__ dst, const char* __restrict__ src,
                                                uint64_t len) {
     const uint64_t mis = (uint64_t)(uintptr_t)src & 15;
@@ -231,24 +283,39 @@ __device__ __forceinline__ void block_copy_vec(char* __restrict__ dst, const cha
     const uint64_t nvec = (len - head) >> 4;
     const uint64_t tail_start = head + (nvec << 4);
     const unsigned tid = threadIdx.x;
-    if (tid < head) dst[tid] = src[tid];
-    if (tid < len - tail_start) dst[tail_start + tid] = src[tail_start + tid];
+    if (tid < head) put_word<DST, char>(dst + tid, src[tid]);
+    if (tid < len - tail_start) put_word<DST, char>(dst + tail_start + tid, src[tail_start + tid]);
     const v4u* s = reinterpret_cast<const v4u*>(src + head);
     v4u* d = reinterpret_cast<v4u*>(dst + head);
     constexpr int U = 8;  // 32 KiB in flight per 256-thread block
     const uint64_t step = (uint64_t)blockDim.x;
-    uint64_t i = tid;
-    for (; i + (U - 1) * step < nvec; i += U * step) {
-        v4u v[U];
+    for (uint64_t ib = 0; ib < nvec; ib += U * step) {
+        const uint64_t i = ib + tid;
+        if (ib + U * step <= nvec) {
+            v4u v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = ld16_nt(s + i + u * step);
+            for (int u = 0; u < U; ++u) v[u] = ld16_nt(s + i + u * step);
+            if (DST == kDstPeer) {
+                const __amdgpu_buffer_rsrc_t rs = wt_rsrc(d + ib);
 #pragma unroll
-        for (int u = 0; u < U; ++u) st16_nt(d + i + u * step, v[u]);
+                for (int u = 0; u < U; ++u) st16_wt(rs, (uint32_t)((tid + u * step) * 16), v[u]);
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) st16_nt(d + i + u * step, v[u]);
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t rs = wt_rsrc(d + ib);
+            for (int u = 0; u < U; ++u) {
+                if (i + u * step >= nvec) break;
+                const v4u v = ld16_nt(s + i + u * step);
+                if (DST == kDstPeer) st16_wt(rs, (uint32_t)((tid + u * step) * 16), v);
+                else st16_nt(d + i + u * step, v);
+            }
+        }
     }
-    for (; i < nvec; i += step) st16_nt(d + i, ld16_nt(s + i));
 }
 
-template <typename W>
+template <int DST, typename W>
 __device__ __forceinline__ void block_copy_words(char* dst, const char* src, uint64_t len) {
     const uint64_t mis = (uint64_t)(uintptr_t)src & (sizeof(W) - 1);
     uint64_t head = mis ? sizeof(W) - mis : 0;
@@ -256,20 +323,22 @@ __device__ __forceinline__ void block_copy_words(char* dst, const char* src, uin
     const uint64_t nw = (len - head) / sizeof(W);
     const uint64_t tail_start = head + nw * sizeof(W);
     const unsigned tid = threadIdx.x;
-    if (tid < head) dst[tid] = src[tid];
-    if (tid < len - tail_start) dst[tail_start + tid] = src[tail_start + tid];
+    if (tid < head) put_word<DST, char>(dst + tid, src[tid]);
+    if (tid < len - tail_start) put_word<DST, char>(dst + tail_start + tid, src[tail_start + tid]);
     const W* s = reinterpret_cast<const W*>(src + head);
     W* d = reinterpret_cast<W*>(dst + head);
-    for (uint64_t i = tid; i < nw; i += blockDim.x) d[i] = s[i];
+    for (uint64_t i = tid; i < nw; i += blockDim.x) put_word<DST, W>(d + i, s[i]);
 }
 
+// DST: kDstLocal (this GPU's memory) or kDstPeer (a peer's IPC-mapped scratch)
+template <int DST>
 __device__ __forceinline__ void block_copy(char* __restrict__ dst, const char* __restrict__ src, uint64_t len) {
     const uintptr_t x = ((uintptr_t)dst ^ (uintptr_t)src) & 15;
-    if (x == 0) block_copy_vec(dst, src, len);
-    else if ((x & 7) == 0) block_copy_words<uint64_t>(dst, src, len);
-    else if ((x & 3) == 0) block_copy_words<uint32_t>(dst, src, len);
-    else if ((x & 1) == 0) block_copy_words<uint16_t>(dst, src, len);
-    else block_copy_words<uint8_t>(dst, src, len);
+    if (x == 0) block_copy_vec<DST>(dst, src, len);
+    else if ((x & 7) == 0) block_copy_words<DST, uint64_t>(dst, src, len);
+    else if ((x & 3) == 0) block_copy_words<DST, uint32_t>(dst, src, len);
+    else if ((x & 1) == 0) block_copy_words<DST, uint16_t>(dst, src, len);
+    else block_copy_words<DST, uint8_t>(dst, src, len);
 }
 
 }  // namespace rdc_amd

@@ -38,7 +38,7 @@ __device__ void allgather_body(const CollArgs& a, uint32_t seq) {
             const uint64_t toff = (uint64_t)t * a.tile_bytes;
             uint64_t tlen = a.len[r] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-            block_copy(a.ag[p] + (uint64_t)r * a.slot_bytes + a.mis[r] + toff, a.cbuf[r] + a.off[r] + toff, tlen);
+            block_copy<kDstPeer>(a.ag[p] + (uint64_t)r * a.slot_bytes + a.mis[r] + toff, a.cbuf[r] + a.off[r] + toff, tlen);
             block_publish1(a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t, seq, a.uc);
         }
         return;
@@ -57,7 +57,7 @@ __device__ void allgather_body(const CollArgs& a, uint32_t seq) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[c] - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-        block_copy(a.cbuf[c] + a.off[c] + toff, a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c] + toff, tlen);
+        block_copy<kDstLocal>(a.cbuf[c] + a.off[c] + toff, a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c] + toff, tlen);
         __syncthreads();
     }
 }
@@ -78,8 +78,8 @@ __global__ __launch_bounds__(kBlock) void k_pack(const PackUnit* __restrict__ un
         char* usr = reinterpret_cast<char*>(units[u].buf);
         char* img = image + units[u].packed;
         const uint64_t len = units[u].len;
-        if (unpack) block_copy(usr, img, len);
-        else block_copy(img, usr, len);
+        if (unpack) block_copy<kDstLocal>(usr, img, len);
+        else block_copy<kDstLocal>(img, usr, len);
     }
 }
 
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(kBlock) void k_copy(char* __restrict__ dst, const c
                                                  uint32_t* arrive, uint64_t* word, uint64_t value) {
     constexpr uint64_t kStep = 64 << 10;
     for (uint64_t off = (uint64_t)blockIdx.x * kStep; off < bytes; off += (uint64_t)gridDim.x * kStep)
-        block_copy(dst + off, src + off, bytes - off < kStep ? bytes - off : kStep);
+        block_copy<kDstPeer>(dst + off, src + off, bytes - off < kStep ? bytes - off : kStep);
     if (word == nullptr) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kBlock) void k_push(PushTargets t, int ndst, const 
     if (b >= per) return;
     constexpr uint64_t kStep = 64 << 10;
     for (uint64_t off = (uint64_t)b * kStep; off < bytes; off += (uint64_t)per * kStep)
-        block_copy(t.dst[d] + off, (t.src[d] ? t.src[d] : src) + off, bytes - off < kStep ? bytes - off : kStep);
+        block_copy<kDstPeer>(t.dst[d] + off, (t.src[d] ? t.src[d] : src) + off, bytes - off < kStep ? bytes - off : kStep);
 }
 
 // ================================================================= fill ===

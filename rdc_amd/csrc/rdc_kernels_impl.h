@@ -127,7 +127,7 @@ __device__ __forceinline__ void mesh_fold_elem(const CollArgs& a, char* own, con
     }
     *reinterpret_cast<T*>(own + e) = acc;
     for (int p = 0; p < n; ++p)
-        if (p != r) *reinterpret_cast<T*>(a.ag[p] + soff + e) = acc;
+        if (p != r) st_elem_wt<T>(a.ag[p] + soff + e, acc);
 }
 
 // Fold `tlen` bytes: own (this rank's values, overwritten with the result),
@@ -158,7 +158,14 @@ __device__ void mesh_reduce_range(const CollArgs& a, char* own, const char* slot
     // runtime loop would leave the lane latency-bound at n = 8.
     constexpr int U = NMAX <= 8 ? 2 : 1;
     const uint64_t stride = kBlock;
-    for (uint64_t i = tid; i < nvec; i += U * stride) {
+    // peers' allgather regions at this range: one write-through descriptor
+    // each per window of U x kBlock vectors (wave-uniform bases)
+    __amdgpu_buffer_rsrc_t ag_rs[NMAX];
+    for (uint64_t ib = 0; ib < nvec; ib += U * stride) {
+        const uint64_t i = ib + tid;
+#pragma unroll
+        for (int p = 0; p < NMAX; ++p)
+            if (p < n && p != r) ag_rs[p] = wt_rsrc(a.ag[p] + soff + head + ib * 16);
         v4u v[U][NMAX];
         bool live[U];
 #pragma unroll
@@ -182,8 +189,9 @@ __device__ void mesh_reduce_range(const CollArgs& a, char* own, const char* slot
                 if (k <= n) acc = reduce16<OP, T>(v[u][k - 1], acc);
             const uint64_t b = head + (i + u * stride) * 16;
             st16(own + b, acc);
-            for (int p = 0; p < n; ++p)
-                if (p != r) st16_nt(a.ag[p] + soff + b, acc);
+#pragma unroll
+            for (int p = 0; p < NMAX; ++p)
+                if (p < n && p != r) st16_wt(ag_rs[p], (uint32_t)((tid + u * stride) * 16), acc);
         }
     }
 }
@@ -259,10 +267,10 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
             char* dst = a.rs[c] + (uint64_t)r * a.slot_bytes + a.mis[c];
             if (a.units)
                 for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
-                    block_copy(dst + (p - a.off[c]), usr, l);
+                    block_copy<kDstPeer>(dst + (p - a.off[c]), usr, l);
                 });
             else
-                block_copy(dst + toff, a.user + a.off[c] + toff, tlen);
+                block_copy<kDstPeer>(dst + toff, a.user + a.off[c] + toff, tlen);
             block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, seq, a.uc);
         }
         return;
@@ -312,10 +320,10 @@ __device__ void mesh_body(const CollArgs& a, uint32_t seq) {
         const char* src = a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c];
         if (a.units)
             for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
-                block_copy(usr, src + (p - a.off[c]), l);
+                block_copy<kDstLocal>(usr, src + (p - a.off[c]), l);
             });
         else
-            block_copy(a.user + a.off[c] + toff, src + toff, tlen);
+            block_copy<kDstLocal>(a.user + a.off[c] + toff, src + toff, tlen);
     }
 }
 
@@ -376,7 +384,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
             if (t < a.tiles[cs]) {
                 uint64_t tlen = a.len[cs] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_copy(a.rs[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
+                block_copy<kDstPeer>(a.rs[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
                            tlen);
                 block_publish1(a.flags[prev] + (uint64_t)j * a.max_tiles + t, seq, a.uc);
             }
@@ -399,7 +407,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
             if (t < a.tiles[cs]) {
                 uint64_t tlen = a.len[cs] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_copy(a.ag[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
+                block_copy<kDstPeer>(a.ag[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
                            tlen);
                 block_publish1(a.flags[prev] + (uint64_t)(n + j) * a.max_tiles + t, seq, a.uc);
             }
@@ -410,7 +418,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
                 if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING, a.uc)) return;
                 uint64_t tlen = a.len[cr] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_copy(a.user + a.off[cr] + toff, a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr] + toff,
+                block_copy<kDstLocal>(a.user + a.off[cr] + toff, a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr] + toff,
                            tlen);
                 __syncthreads();
             }
@@ -568,7 +576,7 @@ __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
         uint64_t tlen = total - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
         for (int k = 1; k < n; ++k)
-            block_copy(a.rs[(r + k) % n] + (uint64_t)r * a.slot_bytes + half + toff, a.user + toff, tlen);
+            block_copy<kDstPeer>(a.rs[(r + k) % n] + (uint64_t)r * a.slot_bytes + half + toff, a.user + toff, tlen);
         if (threadIdx.x < (unsigned)(n - 1))
             s_flags[threadIdx.x] = a.flags[(r + 1 + threadIdx.x) % n] + (uint64_t)r * a.max_tiles + t;
         block_publish(s_flags, n - 1, seq, a.uc);
@@ -642,10 +650,10 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
         if (r == root) {
             if (split) {
                 const int f = bcast_forwarder(n, root, t);
-                block_copy(a.ag[f] + soff, mine, tlen);
+                block_copy<kDstPeer>(a.ag[f] + soff, mine, tlen);
                 block_publish1(a.flags[f] + frow, seq, a.uc);
             } else {
-                for (int k = 1; k < n; ++k) block_copy(a.ag[(root + k) % n] + soff, mine, tlen);
+                for (int k = 1; k < n; ++k) block_copy<kDstPeer>(a.ag[(root + k) % n] + soff, mine, tlen);
                 if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.flags[(root + 1 + threadIdx.x) % n] + frow;
                 block_publish(s_flags, n - 1, seq, a.uc);
             }
@@ -658,7 +666,7 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
             if (split && bcast_forwarder(n, root, t) == r) {
                 for (int k = 1; k < n; ++k) {
                     const int q = (r + k) % n;
-                    if (q != root) block_copy(a.ag[q] + soff, land, tlen);
+                    if (q != root) block_copy<kDstPeer>(a.ag[q] + soff, land, tlen);
                 }
                 if (threadIdx.x == 0) {
                     int k = 0;
@@ -667,7 +675,7 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
                 }
                 block_publish(s_flags, n - 2, seq, a.uc);  // its barrier orders thread 0's list before use
             }
-            block_copy(mine, land, tlen);
+            block_copy<kDstLocal>(mine, land, tlen);
             __syncthreads();
         }
     }
@@ -895,9 +903,10 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
         auto send = [&](uint64_t i, const v4u& x) {
             s_in[i] = x;
             for (int k = 1; k < n; ++k) {
-                char* d = a.region[(r + k) % n] + half + (uint64_t)r * RDC_SVC_SLOT_BYTES + 16 * i;
-                st16_nt(d, v4u{x.x, seq, x.y, seq});
-                st16_nt(d + RDC_SVC_MAX_BYTES, v4u{x.z, seq, x.w, seq});
+                const __amdgpu_buffer_rsrc_t rs =
+                    wt_rsrc(a.region[(r + k) % n] + half + (uint64_t)r * RDC_SVC_SLOT_BYTES);
+                st16_wt(rs, (uint32_t)(16 * i), v4u{x.x, seq, x.y, seq});
+                st16_wt(rs, (uint32_t)(16 * i + RDC_SVC_MAX_BYTES), v4u{x.z, seq, x.w, seq});
             }
         };
         if (ll) {
