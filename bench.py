@@ -59,6 +59,9 @@ def parse():
                     help="N>1: also time cfg4 (fp16) and cfg5 (1024 buckets) this many steps after the timed region")
     ap.add_argument("--ring-steps", type=int, default=5,
                     help="N>1: also time the reference's ring schedule this many steps after the timed region")
+    ap.add_argument("--autotune-reps", type=int, default=3,
+                    help="N>1: before the warm-up, RdcCommAutotune times the launch shapes (role split, grid, "
+                         "tile) for this buffer size on this node and keeps the fastest (0 = library defaults)")
     return ap.parse_args()
 
 
@@ -150,34 +153,6 @@ def time_ring(lib, comm, buf, count, dt_enum, sp, dist, torch, steps):
     def one():
         check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), count, dt_enum, 2, 1, sp))
     return timed_ms(one, comm, sp, dist, torch, steps)
-
-
-def mesh_tuning(lib, comm, S, dt_enum, esz, world, rank, sp, dist, torch, steps, out):
-    """ms per S-byte allreduce for a few mesh role splits and grids
-    (RdcCommTune), max over ranks: which knobs the next round should move on
-    THIS node (the defaults were tuned with every rank on one HBM).  Grids
-    are clamped to what stays resident (ResidentGrid).  Runs last: the
-    communicator keeps the last shape.  Fills `out` as it goes (a failure
-    keeps the shapes measured so far)."""
-    from rdc_amd._lib import check_call
-    import rdc_amd
-    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    shapes = [(4, 8, 0), (3, 9, 0), (5, 8, 0), (6, 6, 0), (3, 10, 0), (4, 8, cus), (4, 8, 3 * cus)]
-    buf = torch.empty(S // esz, dtype=torch.float32 if esz == 4 else torch.float16, device="cuda")
-    rdc_amd.fill_(buf, 0x5EED0000, rank)
-    for s16, r16, grid in shapes:
-        check_call(lib.RdcCommTune(comm.handle, s16, r16, grid, 0))
-
-        def one():
-            check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(buf.data_ptr()), buf.numel(), dt_enum,
-                                              2, 2, sp))
-        ms = timed_ms(one, comm, sp, dist, torch, steps)
-        ll = (ctypes.c_uint64 * 6)()
-        check_call(lib.RdcCommLastLaunch(comm.handle, ll))
-        out["split %d,%d grid %s" % (s16, r16, grid or "auto")] = {"ms": round(ms, 4), "launched_grid": int(ll[0])}
-    check_call(lib.RdcCommTune(comm.handle, 4, 8, 0, 0))
-    del buf
-    return out
 
 
 def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out):
@@ -505,6 +480,24 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         sync_check(comm, sp, dist, torch)
+    tuned = None
+    if world > 1 and args.autotune_reps > 0:
+        # launch-shape autotuning on THIS node (outside the timed region; the
+        # defaults were tuned where every rank shares one HBM).  Every rank
+        # keeps the same winner (times agreed by a MAX allreduce in the
+        # library); a failure is recorded and the defaults kept.
+        try:
+            tuned = comm.autotune(S, dt_enum, reps=args.autotune_reps, stream=sp)
+            failed = 0.0
+        except Exception as e:  # noqa: BLE001 - recorded in the line
+            tuned, failed = {"error": str(e)[:300]}, 1.0
+        f = torch.tensor([failed], dtype=torch.float64)
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        if float(f[0]) > 0:
+            comm.tune(4, 8, 0, 0)
+            if "error" not in tuned:
+                tuned = {"error": "failed on another rank"}
+        sync_check(comm, sp, dist, torch)
     for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
@@ -566,7 +559,7 @@ def main():
 
     multi = world > 1 and args.buckets == 1 and args.algo == "auto"
     f32 = args.dtype == "float32"
-    roles = ring_cmp = extra = rccl = tuning = tcp = checks = None
+    roles = ring_cmp = extra = rccl = tcp = checks = None
     if multi:
         roles = guarded("role_timeline", lambda: trace_roles(_LIB, comm, buf, count, dt_enum, sp, dist, torch))
     if multi and args.ring_steps > 0:
@@ -588,11 +581,6 @@ def main():
                          partial=part_c)
     if multi and f32 and args.rccl_steps > 0:
         rccl = guarded("rccl_comparison", lambda: rccl_compare(S, world, rank, local, dist, torch, args.rccl_steps))
-    if multi and f32 and args.extra_steps > 0:
-        torch.cuda.empty_cache()
-        part_t = {}
-        tuning = guarded("mesh_tuning_ms", lambda: mesh_tuning(_LIB, comm, S, dt_enum, esz, world, rank, sp, dist,
-                                                               torch, args.extra_steps, part_t), partial=part_t)
     if world > 1 and args.cpu_seconds > 0:
         tcp = guarded("cpu_tcp_ring", lambda: cpu_tcp_ring(S, world, rank, dist), needs_comm=False)
 
@@ -688,10 +676,10 @@ def main():
                                 "frac_of_one_link_peak": None if shared else round(rb / XGMI_LINK_DIR_GBPS, 4),
                                 "note": "reference ring schedule (k_ring) on the same buffer, timed after the "
                                         "main region; bit-identical result"}
+    if tuned is not None:
+        out["autotune"] = tuned
     if roles is not None:
         out["role_timeline"] = roles
-    if tuning is not None:
-        out["mesh_tuning_ms"] = tuning
     if extra is not None:
         out["extra_configs"] = extra
     if checks is not None:

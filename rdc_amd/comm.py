@@ -12,6 +12,12 @@ from .buffer import Buffer
 WS_PENDING, WS_RUNNING, WS_FINISHED, WS_ERROR = 1 << 1, 1 << 2, 1 << 3, 1 << 6
 
 
+class TuneCand(ctypes.Structure):
+    """RdcTuneCand (include/rdc_amd.h): one launch shape timed by RdcCommAutotune."""
+    _fields_ = [("mesh_s16", ctypes.c_int), ("mesh_r16", ctypes.c_int), ("max_blocks", ctypes.c_int),
+                ("tiles_per_block", ctypes.c_int), ("ms", ctypes.c_double)]
+
+
 class WorkComp(object):
     """Completion of an isend / irecv (rdc/comm.py:11-33).  Holds the buffer
     alive until the handle is dropped."""
@@ -177,6 +183,33 @@ class Comm(object):
         bytes (0 = auto) for the following collectives (RdcCommTune); every
         rank must pass the same values.  Results stay bit-identical."""
         check_call(_LIB.RdcCommTune(self.handle, int(mesh_s16), int(mesh_r16), int(max_blocks), int(tile_bytes)))
+
+    def autotune(self, nbytes, dtype=None, reps=3, stream=None):
+        """Collective (every rank, same arguments): time the launch shapes the
+        automatic schedule can take for allreduces of `nbytes` (mesh role
+        split, grid, tiles per block), agree on the slowest rank's times and keep the
+        fastest (RdcCommAutotune).  Returns {"chosen": {...} or None,
+        "candidates": [{...,"ms"}]}; None chosen = the size takes the one-shot
+        or tree path and nothing changed.  Results stay bit-identical."""
+        if dtype is None:
+            dtype = 6  # mpi::kFloat32
+        elif not isinstance(dtype, int):
+            dtype = _dev.dtype_enum(dtype)
+        if stream is None:
+            import torch
+            stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        room = 32
+        cand = (TuneCand * room)()
+        nc, best = ctypes.c_int(0), ctypes.c_int(-1)
+        check_call(_LIB.RdcCommAutotune(self.handle, int(nbytes), int(dtype), int(reps), stream,
+                                        ctypes.cast(cand, ctypes.c_void_p), room, ctypes.byref(nc),
+                                        ctypes.byref(best)))
+
+        def row(c):
+            return {"split": [c.mesh_s16, c.mesh_r16], "grid": c.max_blocks or "auto",
+                    "tiles_per_block": c.tiles_per_block or "auto", "ms": round(c.ms, 4)}
+        rows = [row(cand[k]) for k in range(nc.value)]
+        return {"chosen": rows[best.value] if best.value >= 0 else None, "candidates": rows}
 
     def check(self, stream=None):
         """Synchronise the stream and raise if a device-side wait failed."""

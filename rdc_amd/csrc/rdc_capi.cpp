@@ -565,6 +565,20 @@ int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t t
     return guard([&] { as_comm(comm)->Tune(mesh_s16, mesh_r16, max_blocks, tile_bytes); });
 }
 
+int RdcCommAutotune(void* comm, size_t bytes, int dtype, int reps, void* stream, RdcTuneCand* cand, int max_cand,
+                    int* ncand, int* best) {
+    return guard([&] {
+        if (!cand || !ncand || !best || max_cand <= 0) throw std::invalid_argument("rdc: null argument");
+        std::vector<rdc_amd::Communicator::TuneCand> c((size_t)max_cand);
+        int b = -1;
+        const int k = as_comm(comm)->Autotune(bytes, dtype, reps, static_cast<hipStream_t>(stream), c.data(),
+                                              max_cand, &b);
+        for (int i = 0; i < k; ++i) cand[i] = RdcTuneCand{c[i].s16, c[i].r16, c[i].grid, c[i].tpb, c[i].ms};
+        *ncand = k;
+        *best = b;
+    });
+}
+
 int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, double* ms_out, size_t* bytes_out) {
     return guard([&] {
         if (!ms_out) throw std::invalid_argument("rdc: null argument");

@@ -664,6 +664,22 @@ Layout Communicator::layout() const {
 
 int Communicator::max_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_blocks : cus_min_; }
 
+int Communicator::SizeClass(uint64_t bytes) {
+    int k = 0;
+    while (k < 63 && (bytes >> (k + 1)) != 0) ++k;
+    return k;
+}
+
+Communicator::Shape Communicator::ShapeFor(uint64_t total) const {
+    const auto it = tuned_.find(SizeClass(total));
+    if (it != tuned_.end()) return it->second;
+    Shape s;
+    s.split = cfg_.mesh_split;
+    s.max_blocks = cfg_.max_blocks;
+    s.tile_bytes = cfg_.tile_bytes;
+    return s;
+}
+
 // The mesh keeps more remote stores in flight with two blocks per CU (k_mesh:
 // 100 VGPRs, 4 blocks per CU fit): 1 GiB on 2 ranks 1.86 -> 1.65-1.69 ms at
 // 384-512 blocks (tools/mesh_sweep*.sh).  Ranks sharing a GPU get their share
@@ -797,11 +813,14 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         hip_check(ks.oneshot(a, p.nb_scatter, stream), "launch one-shot allreduce");
         return;
     }
+    const Shape sh = ShapeFor(total);
     const int grid_cap =
-        algo == RDC_ALGO_MESH ? LaunchGrid(mesh_blocks(), ks.occupancy(RDC_KIND_MESH, n_))
-                              : LaunchGrid(max_blocks(), ks.occupancy(RDC_KIND_RING, n_));
+        algo == RDC_ALGO_MESH ? LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : 2 * cus_min_,
+                                           ks.occupancy(RDC_KIND_MESH, n_))
+                              : LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : cus_min_,
+                                           ks.occupancy(RDC_KIND_RING, n_));
     const std::vector<Piece> plan =
-        PlanAllreduceRanges(n_, off, len, esz, layout(), algo, cfg_.tile_bytes, grid_cap, cfg_.mesh_split);
+        PlanAllreduceRanges(n_, off, len, esz, layout(), algo, sh.tile_bytes, grid_cap, sh.split);
     for (const Piece& p : plan) {
         CollArgs a;
         FillArgsCommon(&a);
@@ -1080,8 +1099,129 @@ void Communicator::Tune(int s16, int r16, int max_blocks, size_t tile_bytes) {
     if (tile_bytes % RDC_SLOT_ALIGN) throw std::invalid_argument("rdc: tile bytes must be a multiple of 256");
     cfg_.mesh_split.s16 = s16;
     cfg_.mesh_split.r16 = r16;
+    cfg_.mesh_split.tpb = 0;
     cfg_.max_blocks = max_blocks;
     cfg_.tile_bytes = tile_bytes;
+    tuned_.clear();  // an explicit shape replaces every autotuned one
+}
+
+// Launch-shape autotuning for one buffer size (rdc_comm.h).  The defaults
+// (4 / 8 / 4 split, 2 blocks per CU, ~2 tiles per reduce block) were tuned on
+// one GPU where HBM is the bound; over xGMI the balance between the copy
+// roles and the reduce role, the number of remote stores in flight and the
+// tile granularity (the ring: 2(n-1) hand-offs per tile) can differ, so a
+// node measures its own.  Coordinate descent, every stage
+// agreed across ranks before the next one is built from its winner.
+int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream, TuneCand* cand, int max_cand,
+                           int* best) {
+    if (!cand || !best || max_cand <= 0 || reps <= 0) throw std::invalid_argument("rdc: autotune needs reps and room");
+    *best = -1;
+    const size_t esz = rdc_dtype_size(dtype);
+    if (esz == 0) throw std::invalid_argument("rdc: unsupported dtype");
+    const size_t count = bytes / esz;
+    if (n_ == 1 || count == 0 || (uint64_t)count * esz <= cfg_.ring_mincount) return 0;
+    const int algo = PickAlgo(RDC_ALGO_AUTO, (uint64_t)count * esz);
+    if (algo != RDC_ALGO_MESH && algo != RDC_ALGO_RING) return 0;  // one-shot: a single hand-off, no roles
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    void* buf = nullptr;
+    double* dms = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const int cls = SizeClass((uint64_t)count * esz);
+    const auto had = tuned_.find(cls);
+    const bool had_shape = had != tuned_.end();
+    const Shape saved = had_shape ? had->second : Shape();
+    int nc = 0;
+    auto release = [&] {
+        if (buf) (void)hipFreeAsync(buf, stream);
+        if (dms) (void)hipFreeAsync(dms, stream);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        (void)hipStreamSynchronize(stream);
+    };
+    try {
+        hip_check(hipMallocAsync(&buf, count * esz, stream), "autotune buffer");
+        hip_check(hipMallocAsync(reinterpret_cast<void**>(&dms), sizeof(double) * (size_t)max_cand, stream),
+                  "autotune times");
+        hip_check(hipMemsetAsync(buf, 0, count * esz, stream), "autotune memset");
+        hip_check(hipEventCreate(&e0), "event");
+        hip_check(hipEventCreate(&e1), "event");
+        auto set_shape = [&](int s16, int r16, int grid, int tpb) {
+            Shape s;
+            s.split.s16 = s16;
+            s.split.r16 = r16;
+            s.split.tpb = tpb;
+            s.max_blocks = grid;
+            tuned_[cls] = s;
+        };
+        auto time_one = [&](int s16, int r16, int grid, int tpb) {
+            if (nc >= max_cand) return;
+            set_shape(s16, r16, grid, tpb);
+            Allreduce(buf, count, dtype, RDC_OP_SUM, stream, RDC_ALGO_AUTO);  // warm (and first-use work)
+            hip_check(hipEventRecord(e0, stream), "record");
+            for (int i = 0; i < reps; ++i) Allreduce(buf, count, dtype, RDC_OP_SUM, stream, RDC_ALGO_AUTO);
+            hip_check(hipEventRecord(e1, stream), "record");
+            hip_check(hipEventSynchronize(e1), "sync");
+            float ms = 0;
+            hip_check(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+            cand[nc++] = TuneCand{s16, r16, grid, tpb, (double)ms / reps};
+        };
+        // the slowest rank's time per candidate, identical on every rank;
+        // returns the stage's winner (lowest index among equal times)
+        auto agree = [&](int lo) {
+            const int k = nc - lo;
+            if (k <= 0) throw std::runtime_error("rdc: autotune ran out of candidate room");
+            double h[64];
+            if (k > 64) throw std::logic_error("rdc: autotune stage too large");
+            for (int i = 0; i < k; ++i) h[i] = cand[lo + i].ms;
+            hip_check(hipMemcpyAsync(dms, h, sizeof(double) * k, hipMemcpyHostToDevice, stream), "H2D");
+            Allreduce(dms, (size_t)k, RDC_DT_FLOAT64, RDC_OP_MAX, stream, RDC_ALGO_AUTO);
+            hip_check(hipMemcpyAsync(h, dms, sizeof(double) * k, hipMemcpyDeviceToHost, stream), "D2H");
+            Check(stream);
+            int w = lo;
+            for (int i = 0; i < k; ++i) {
+                cand[lo + i].ms = h[i];
+                if (h[i] < cand[w].ms) w = lo + i;
+            }
+            return w;
+        };
+        const int cus = cus_min_;
+        int w;
+        if (algo == RDC_ALGO_MESH) {
+            static const int kSplits[][2] = {{4, 8}, {3, 9}, {5, 8}, {6, 6}, {3, 10}, {2, 10}, {5, 7}};
+            int lo = nc;
+            for (const auto& s : kSplits) time_one(s[0], s[1], 0, 0);
+            w = agree(lo);
+            const int s16 = cand[w].s16, r16 = cand[w].r16;
+            lo = nc;
+            for (int bpc : {1, 3, 4}) time_one(s16, r16, bpc * cus, 0);
+            if (nc < max_cand) cand[nc++] = cand[w];  // the auto grid (2 per CU), timed: kept in the stage
+            w = agree(lo);
+            const int grid = cand[w].grid;
+            lo = nc;
+            for (int tpb : {1, 4, 8}) time_one(s16, r16, grid, tpb);
+            if (nc < max_cand) cand[nc++] = cand[w];
+            w = agree(lo);
+        } else {
+            const int s16 = cfg_.mesh_split.s16, r16 = cfg_.mesh_split.r16;  // unused by the ring
+            int lo = nc;
+            for (int bpc : {1, 2}) time_one(s16, r16, bpc * cus, 0);
+            w = agree(lo);
+            const int grid = cand[w].grid;
+            lo = nc;
+            for (int tpb : {4, 8, 16, 32}) time_one(s16, r16, grid, tpb);
+            if (nc < max_cand) cand[nc++] = cand[w];
+            w = agree(lo);
+        }
+        set_shape(cand[w].s16, cand[w].r16, cand[w].grid, cand[w].tpb);
+        *best = w;
+    } catch (...) {
+        if (had_shape) tuned_[cls] = saved;
+        else tuned_.erase(cls);
+        release();
+        throw;
+    }
+    release();
+    return nc;
 }
 
 double Communicator::Probe(int mode, size_t* bytes_io, int reps, hipStream_t stream) {

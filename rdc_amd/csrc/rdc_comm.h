@@ -163,6 +163,23 @@ public:
     // bytes (0 = auto).  Throws std::invalid_argument on a bad split.
     void Tune(int s16, int r16, int max_blocks, size_t tile_bytes);
 
+    // Collective (every rank, same arguments, no collective in flight): time
+    // the launch shapes the automatic schedule for `bytes` of `dtype` can take
+    // (mesh: role split, then grid, then tiles per reduce block; ring: grid,
+    // then tiles per block — granularity that scales with the buffer), `reps`
+    // Sum allreduces each on a scratch buffer, agree on the per-candidate
+    // times by a MAX allreduce over this communicator (every rank gets the
+    // same bits, so the same winner), and keep the fastest for allreduces of
+    // the same size class ([2^k, 2^(k+1)) bytes: tuned_; Tune clears them).
+    // Candidates in cand[] ({s16, r16, grid, tpb, ms}; up to max_cand);
+    // returns their count and *best = the chosen index (-1: nothing to tune,
+    // e.g. a one-shot / tree size).  Results stay bit-identical whatever wins.
+    struct TuneCand {
+        int s16, r16, grid, tpb;  // tpb: automatic tiles per block (MeshSplit::tpb), 0 = default
+        double ms;
+    };
+    int Autotune(size_t bytes, int dtype, int reps, hipStream_t stream, TuneCand* cand, int max_cand, int* best);
+
     // diagnostics: the next allreduce's launches (mesh or ring) record per
     // block {start, end} wall_clock64 ticks into dev_words (>= 2 x grid words);
     // LastLaunch() = {grid, nb_scatter, nb_reduce, nb_gather, tile_bytes, algo}
@@ -190,6 +207,17 @@ public:
     // (LaunchGrid, rdc_plan.h ResidentGrid)
     int max_blocks() const;
     int mesh_blocks() const;
+    // Launch shape of a mesh / ring allreduce of `total` bytes: the shape
+    // Autotune recorded for its size class (floor(log2(total))), else the
+    // communicator's configuration (defaults, RDC_* env, Tune).
+    struct Shape {
+        MeshSplit split;
+        int max_blocks = 0;
+        size_t tile_bytes = 0;
+    };
+    Shape ShapeFor(uint64_t total) const;
+    static int SizeClass(uint64_t bytes);
+    std::map<int, Shape> tuned_;  // Autotune results per size class; cleared by Tune
     int LaunchGrid(int want, int blocks_per_cu) const;
     bool shared_gpu() const { return share_max_ > 1; }
     int ranks_per_gpu() const { return share_max_; }

@@ -56,9 +56,9 @@ void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blo
         const size_t G = (size_t)std::max(1, max_blocks);
         size_t want, lo = RDC_MIN_TILE;
         if (algo == RDC_ALGO_RING) {
-            want = chunk_bytes / G;
+            want = chunk_bytes / (G * (size_t)(split.tpb > 0 ? split.tpb : 1));
         } else {
-            want = chunk_bytes / (2 * std::max<size_t>(1, G * (size_t)r16 / 16));
+            want = chunk_bytes / ((size_t)(split.tpb > 0 ? split.tpb : 2) * std::max<size_t>(1, G * (size_t)r16 / 16));
             lo = (size_t)64 << 10;
         }
         t = std::min<size_t>(std::max<size_t>(want, lo), (size_t)1 << 20);

@@ -44,6 +44,10 @@ struct Piece {
 // the most work per byte: n loads, n stores).
 struct MeshSplit {
     int s16 = 4, r16 = 8;
+    // automatic tiles per block (0 = default: 2 per mesh reduce block, 1 per
+    // ring block); bounded to [64 KiB (mesh) / RDC_MIN_TILE (ring), 1 MiB].
+    // Set by Communicator::Autotune; scales with the buffer like the default.
+    int tpb = 0;
 };
 // Grid of a launch whose blocks wait on peers' blocks.  Every waiting block of
 // every rank must be resident at once, or a rank's waiters can occupy the CUs

@@ -170,6 +170,9 @@ def main():
             del bufs
             print("rank %d case %d ok" % (rank, i), flush=True)
             continue
+        if c.get("autotune"):  # RdcCommAutotune for this many bytes, then the case runs on the chosen shape
+            res = comm.autotune(c["autotune"], dtype, reps=2, stream=sp)
+            open(os.path.join(outdir, "case%d_rank%d.tune" % (i, rank)), "w").write(json.dumps(res))
         if c.get("last_launch"):  # record the launch shape the library chose (grid clamp checks)
             ll = (ctypes.c_uint64 * 6)()
         reps = c.get("reps", 1)

@@ -575,6 +575,36 @@ def test_mp_forced_oversized_grid_four_ranks():
     assert (16 << 20) * 4 // 4 // ll[4] >= 256, ll  # ring: >= 256 tiles per chunk
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_mp_autotune_agrees_and_stays_bit_exact(world):
+    """RdcCommAutotune (bench.py runs it before the timed region at N > 1):
+    every rank keeps the same winner (times agreed by a MAX allreduce), the
+    stages cover the schedule the size takes (n = 2 above 8 MiB: ring grid /
+    tiles per block; n = 3: mesh split / grid / tiles per reduce block), a
+    one-shot size changes nothing,
+    and the allreduces on the chosen shape stay bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    big = 8 << 20  # fp32 elements: 32 MiB
+    cases = [{"count": 16384, "dtype": 6, "op": 2, "autotune": 65536},
+             {"count": big, "dtype": 6, "op": 2, "autotune": big * 4, "reps": 2},
+             {"count": 100003, "dtype": 11, "op": 2, "algo": 2}]
+    tmp = run_mp(world, cases, timeout=400)
+    for i, c in enumerate(cases):
+        want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
+    small = [json.load(open(os.path.join(tmp, "case0_rank%d.tune" % r))) for r in range(world)]
+    assert all(t == {"chosen": None, "candidates": []} for t in small), small
+    tunes = [json.load(open(os.path.join(tmp, "case1_rank%d.tune" % r))) for r in range(world)]
+    assert all(t == tunes[0] for t in tunes), tunes  # identical bits on every rank
+    t = tunes[0]
+    assert t["chosen"] is not None and t["chosen"] in t["candidates"], t
+    assert t["chosen"]["ms"] == min(c["ms"] for c in t["candidates"]), t
+    assert len(t["candidates"]) == (7 if world == 2 else 15), t
+
+
 def test_mp_many_small_buckets_cfg5_shape():
     """test/mallreduce.cc shape: back-to-back 1 MiB fp32 allreduces on one buffer."""
     if not torch.cuda.is_available():
