@@ -686,8 +686,14 @@ Communicator::Shape Communicator::ShapeFor(uint64_t total) const {
 // of the resident blocks through LaunchGrid.
 int Communicator::mesh_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_blocks : 2 * cus_min_; }
 
+// One CU per rank on the GPU is left out of the resident budget: the
+// small-allreduce service (rdc_service.h) keeps one persistent block per rank
+// resident, and its registers (k_svc: 512 threads, ~208 VGPRs) leave no room
+// for a collective block on its CU.  A grid sized to every CU would then not
+// be co-resident while the service runs (RDC_NBLOCKS / Tune / Autotune can
+// ask for 4 blocks per CU) and its waits would time out.
 int Communicator::LaunchGrid(int want, int blocks_per_cu) const {
-    return ResidentGrid(want, blocks_per_cu, cus_min_, share_max_);
+    return ResidentGrid(want, blocks_per_cu, std::max(1, cus_min_ - share_max_), share_max_);
 }
 
 void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStream_t stream, int algo) {

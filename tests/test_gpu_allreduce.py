@@ -575,6 +575,35 @@ def test_mp_forced_oversized_grid_four_ranks():
     assert (16 << 20) * 4 // 4 // ll[4] >= 256, ll  # ring: >= 256 tiles per chunk
 
 
+def test_mp_full_grid_beside_resident_service():
+    """The small-allreduce service keeps one persistent block per rank resident
+    (a host allreduce starts it); a collective forced to the largest grid
+    (RDC_NBLOCKS=4096 -> clamped to 4 blocks per CU) must still be wholly
+    co-resident beside it, so LaunchGrid leaves one CU per rank out of the
+    budget.  Host calls, full-grid mesh / ring / broadcast launches and host
+    calls again, interleaved, all bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [{"count": 1024, "dtype": 6, "op": 2, "kind": "host_allreduce"},
+             {"count": 4 << 20, "dtype": 6, "op": 2, "algo": 2, "last_launch": True},
+             {"count": 1000, "dtype": 2, "op": 2, "kind": "host_allreduce"},
+             {"count": 4 << 20, "dtype": 6, "op": 2, "algo": 1},
+             {"count": 999, "dtype": 6, "op": 0, "kind": "host_allreduce"},
+             {"count": (3 << 20) + 1, "dtype": 0, "kind": "broadcast", "root": 1},
+             {"count": 16, "dtype": 7, "op": 2, "kind": "host_allreduce"}]
+    # the service stays resident for 30 s after its last request (default 1 ms)
+    tmp = run_mp(2, cases, timeout=300, env_extra={"RDC_NBLOCKS": "4096", "RDC_TIMEOUT": "20",
+                                                   "RDC_HOST_SERVICE_IDLE_US": "30000000"})
+    for i, c in enumerate(cases):
+        want = expected_for(c, 2)
+        for r in range(2):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    ll = json.load(open(os.path.join(tmp, "case1_rank0.launch")))
+    assert ll[0] <= 4 * (cus - 2) // 2, ll
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_mp_autotune_agrees_and_stays_bit_exact(world):
     """RdcCommAutotune (bench.py runs it before the timed region at N > 1):
