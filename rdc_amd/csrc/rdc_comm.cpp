@@ -670,8 +670,8 @@ int Communicator::SizeClass(uint64_t bytes) {
     return k;
 }
 
-Communicator::Shape Communicator::ShapeFor(uint64_t total) const {
-    const auto it = tuned_.find(SizeClass(total));
+Communicator::Shape Communicator::ShapeFor(uint64_t total, int algo) const {
+    const auto it = tuned_.find(SizeClass(total) * 8 + algo);
     if (it != tuned_.end()) return it->second;
     Shape s;
     s.split = cfg_.mesh_split;
@@ -819,7 +819,7 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         hip_check(ks.oneshot(a, p.nb_scatter, stream), "launch one-shot allreduce");
         return;
     }
-    const Shape sh = ShapeFor(total);
+    const Shape sh = ShapeFor(total, algo);
     const int grid_cap =
         algo == RDC_ALGO_MESH ? LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : 2 * cus_min_,
                                            ks.occupancy(RDC_KIND_MESH, n_))
@@ -1132,7 +1132,7 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     void* buf = nullptr;
     double* dms = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    const int cls = SizeClass((uint64_t)count * esz);
+    const int cls = SizeClass((uint64_t)count * esz) * 8 + algo;  // the key ShapeFor looks up
     const auto had = tuned_.find(cls);
     const bool had_shape = had != tuned_.end();
     const Shape saved = had_shape ? had->second : Shape();

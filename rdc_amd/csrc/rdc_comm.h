@@ -208,16 +208,18 @@ public:
     int max_blocks() const;
     int mesh_blocks() const;
     // Launch shape of a mesh / ring allreduce of `total` bytes: the shape
-    // Autotune recorded for its size class (floor(log2(total))), else the
-    // communicator's configuration (defaults, RDC_* env, Tune).
+    // Autotune recorded for its size class (floor(log2(total))) and schedule,
+    // else the communicator's configuration (defaults, RDC_* env, Tune).
+    // (A coalesced list of the same size class takes the unit-table mesh: it
+    // uses a mesh shape tuned for that class, never a ring one.)
     struct Shape {
         MeshSplit split;
         int max_blocks = 0;
         size_t tile_bytes = 0;
     };
-    Shape ShapeFor(uint64_t total) const;
+    Shape ShapeFor(uint64_t total, int algo) const;
     static int SizeClass(uint64_t bytes);
-    std::map<int, Shape> tuned_;  // Autotune results per size class; cleared by Tune
+    std::map<int, Shape> tuned_;  // Autotune results by size class * 8 + algo; cleared by Tune
     int LaunchGrid(int want, int blocks_per_cu) const;
     bool shared_gpu() const { return share_max_ > 1; }
     int ranks_per_gpu() const { return share_max_; }

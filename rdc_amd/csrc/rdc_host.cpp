@@ -80,9 +80,19 @@ HostPath::~HostPath() {
     if (d2h_) (void)hipStreamDestroy(d2h_);
 }
 
-void HostPath::Reserve(size_t piece_bytes, size_t total_bytes, int pieces) {
+// Growing waits only for this path's own streams and the communicator's
+// stream (the previous call's copies and launches that may still use the old
+// buffers), never for the whole device: in a single-process group the other
+// ranks' launches may be waiting on this rank's next one.
+void HostPath::QuiesceForRegrow(hipStream_t comm_stream) {
+    hip_check(hipStreamSynchronize(h2d_), "sync before regrow");
+    hip_check(hipStreamSynchronize(d2h_), "sync before regrow");
+    hip_check(hipStreamSynchronize(comm_stream), "sync before regrow");
+}
+
+void HostPath::Reserve(size_t piece_bytes, size_t total_bytes, int pieces, hipStream_t comm_stream) {
     if (piece_bytes > slot_bytes_) {
-        hip_check(hipDeviceSynchronize(), "sync before regrow");
+        QuiesceForRegrow(comm_stream);
         for (int i = 0; i < kSlots; ++i) {
             if (pin_in_[i]) (void)hipHostFree(pin_in_[i]);
             pin_in_[i] = nullptr;
@@ -95,7 +105,7 @@ void HostPath::Reserve(size_t piece_bytes, size_t total_bytes, int pieces) {
     }
     if (total_bytes > dev_bytes_) {
         if (dev_) {
-            hip_check(hipDeviceSynchronize(), "sync before regrow");
+            QuiesceForRegrow(comm_stream);
             (void)hipFree(dev_);
             dev_ = nullptr;
             dev_bytes_ = 0;
@@ -218,7 +228,7 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
         // the tree's order (rdc_reduce_ring_mincount) is per element, but the
         // pipeline below cuts the buffer by Split chunk for the ring: stage
         // the whole buffer instead (raised thresholds are for small buffers)
-        Reserve(0, S, 0);
+        Reserve(0, S, 0, comm_stream);
         hip_check(hipMemcpyAsync(dev_, h, S, hipMemcpyHostToDevice, comm_stream), "H2D");
         c->Allreduce(dev_, count, dtype, op, comm_stream);
         hip_check(hipMemcpyAsync(h, dev_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
@@ -233,7 +243,7 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
     const uint64_t K0 = std::max<uint64_t>(1, (S + kPieceTarget - 1) / kPieceTarget);
     const uint64_t sl = std::max<uint64_t>(4096, ((maxlen + K0 - 1) / K0 + 4095) & ~(uint64_t)4095);
     const int K = (int)((maxlen + sl - 1) / sl);
-    Reserve((size_t)sl * (size_t)n, S, K);
+    Reserve((size_t)sl * (size_t)n, S, K, comm_stream);
     {
         std::lock_guard<std::mutex> lk(dmu_);
         queue_.clear();

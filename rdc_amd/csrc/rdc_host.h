@@ -47,7 +47,8 @@ private:
         int nslice;
         uint64_t off[RDC_MAX_RANKS], len[RDC_MAX_RANKS];
     };
-    void Reserve(size_t piece_bytes, size_t total_bytes, int pieces);
+    void Reserve(size_t piece_bytes, size_t total_bytes, int pieces, hipStream_t comm_stream);
+    void QuiesceForRegrow(hipStream_t comm_stream);
     void Copy(char* dst, const char* src, size_t bytes);  // parallel memcpy
     void DrainLoop();
 

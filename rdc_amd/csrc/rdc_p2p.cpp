@@ -114,8 +114,15 @@ P2PEngine::P2PEngine(int rank, int n, int device, size_t slot_bytes, char* local
     hip_check(hipSetDevice(device_), "hipSetDevice");
     ctl_dev_ = checked_ctl_mapping(ctl_);
     hip_check(hipMalloc(&arrive_, 2 * RDC_MAX_RANKS * sizeof(uint32_t)), "hipMalloc arrival counters");
-    hip_check(hipMemset(arrive_, 0, 2 * RDC_MAX_RANKS * sizeof(uint32_t)), "memset arrival counters");
-    hip_check(hipDeviceSynchronize(), "sync");
+    // zeroed on a private stream: the engine starts on first use, possibly
+    // while collectives of other ranks of a single-process group are waiting
+    // on this one, so nothing here may wait for the whole device
+    hipStream_t s = nullptr;
+    hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream");
+    const hipError_t e = hipMemsetAsync(arrive_, 0, 2 * RDC_MAX_RANKS * sizeof(uint32_t), s);
+    const hipError_t w = e == hipSuccess ? hipStreamSynchronize(s) : e;
+    (void)hipStreamDestroy(s);
+    hip_check(w, "memset arrival counters");
     th_ = std::thread([this] { Loop(); });
 }
 
