@@ -244,6 +244,26 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
     const uint64_t sl = std::max<uint64_t>(4096, ((maxlen + K0 - 1) / K0 + 4095) & ~(uint64_t)4095);
     const int K = (int)((maxlen + sl - 1) / sl);
     Reserve((size_t)sl * (size_t)n, S, K, comm_stream);
+    if (K == 1) {
+        // one piece (up to kPieceTarget): nothing to overlap, so no drain
+        // thread hand-off either — the slices of one piece are the chunks in
+        // order, i.e. the whole buffer: pool copy into a pinned slot, H2D,
+        // allreduce, pageable D2H straight into the caller's buffer, all on
+        // the communicator's stream, and the caller spins on the end
+        const double t0 = tracing() ? trace_now() : 0;
+        Copy(pin_in_[0], h, S);
+        const double t1 = tracing() ? trace_now() : 0;
+        hip_check(hipMemcpyAsync(dev_, pin_in_[0], S, hipMemcpyHostToDevice, comm_stream), "H2D");
+        c->Allreduce(dev_, count, dtype, op, comm_stream);
+        hip_check(hipMemcpyAsync(h, dev_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
+        hip_check(hipEventRecord(in_done_[0], comm_stream), "record");
+        SpinEvent(in_done_[0], "host allreduce");
+        if (tracing())
+            fprintf(stderr, "[host %.3f] one piece: copy-in %.3f ms, H2D+allreduce+D2H %.3f ms (%llu B)\n", t0,
+                    t1 - t0, trace_now() - t1, (unsigned long long)S);
+        c->RaiseIfError(c->HostErrorWord());
+        return;
+    }
     {
         std::lock_guard<std::mutex> lk(dmu_);
         queue_.clear();
