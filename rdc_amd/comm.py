@@ -14,7 +14,8 @@ WS_PENDING, WS_RUNNING, WS_FINISHED, WS_ERROR = 1 << 1, 1 << 2, 1 << 3, 1 << 6
 
 class TuneCand(ctypes.Structure):
     """RdcTuneCand (include/rdc_amd.h): one launch shape timed by RdcCommAutotune."""
-    _fields_ = [("mesh_s16", ctypes.c_int), ("mesh_r16", ctypes.c_int), ("max_blocks", ctypes.c_int),
+    _fields_ = [("algo", ctypes.c_int), ("mesh_s16", ctypes.c_int), ("mesh_r16", ctypes.c_int),
+                ("max_blocks", ctypes.c_int),
                 ("tiles_per_block", ctypes.c_int), ("ms", ctypes.c_double)]
 
 
@@ -185,9 +186,9 @@ class Comm(object):
         check_call(_LIB.RdcCommTune(self.handle, int(mesh_s16), int(mesh_r16), int(max_blocks), int(tile_bytes)))
 
     def autotune(self, nbytes, dtype=None, reps=3, stream=None):
-        """Collective (every rank, same arguments): time the launch shapes the
-        automatic schedule can take for allreduces of `nbytes` (mesh role
-        split, grid, tiles per block), agree on the slowest rank's times and keep the
+        """Collective (every rank, same arguments): time the ring and the mesh,
+        then the launch shapes of the faster one for allreduces of `nbytes`
+        (mesh role split, grid, tiles per block), agree on the slowest rank's times and keep the
         fastest (RdcCommAutotune).  Returns {"chosen": {...} or None,
         "candidates": [{...,"ms"}]}; None chosen = the size takes the one-shot
         or tree path and nothing changed.  Results stay bit-identical."""
@@ -206,7 +207,8 @@ class Comm(object):
                                         ctypes.byref(best)))
 
         def row(c):
-            return {"split": [c.mesh_s16, c.mesh_r16], "grid": c.max_blocks or "auto",
+            return {"schedule": {1: "ring", 2: "mesh"}.get(c.algo, c.algo),
+                    "split": [c.mesh_s16, c.mesh_r16], "grid": c.max_blocks or "auto",
                     "tiles_per_block": c.tiles_per_block or "auto", "ms": round(c.ms, 4)}
         rows = [row(cand[k]) for k in range(nc.value)]
         return {"chosen": rows[best.value] if best.value >= 0 else None, "candidates": rows}

@@ -625,8 +625,15 @@ int Communicator::PickAlgo(int algo) const {
 
 int Communicator::PickAlgo(int algo, uint64_t bytes) const {
     if (algo == RDC_ALGO_AUTO) algo = cfg_.algo;
-    if (algo == RDC_ALGO_AUTO)
+    if (algo == RDC_ALGO_AUTO) {
         algo = AutoAlgo(n_, bytes, layout(), cfg_.oneshot_push_max);
+        // a schedule Autotune measured for this size class replaces the
+        // rule's mesh / ring choice (never a one-shot or tree size)
+        if (algo == RDC_ALGO_MESH || algo == RDC_ALGO_RING) {
+            const auto it = tuned_algo_.find(SizeClass(bytes));
+            if (it != tuned_algo_.end()) algo = it->second;
+        }
+    }
     if (algo == RDC_ALGO_ONESHOT && !OneshotEligible(n_, bytes, layout(), (uint64_t)-1))
         algo = RDC_ALGO_MESH;  // does not fit half a slot
     return algo;
@@ -1108,10 +1115,13 @@ void Communicator::Tune(int s16, int r16, int max_blocks, size_t tile_bytes) {
     cfg_.mesh_split.tpb = 0;
     cfg_.max_blocks = max_blocks;
     cfg_.tile_bytes = tile_bytes;
-    tuned_.clear();  // an explicit shape replaces every autotuned one
+    tuned_.clear();  // an explicit shape replaces every autotuned one (and schedule)
+    tuned_algo_.clear();
 }
 
-// Launch-shape autotuning for one buffer size (rdc_comm.h).  The defaults
+// Schedule and launch-shape autotuning for one buffer size (rdc_comm.h).
+// Stage 0 times the ring and the mesh (bit-identical; the rule picks the ring
+// at n = 2 and the mesh from n = 3 on byte counts alone).  The defaults
 // (4 / 8 / 4 split, 2 blocks per CU, ~2 tiles per reduce block) were tuned on
 // one GPU where HBM is the bound; over xGMI the balance between the copy
 // roles and the reduce role, the number of remote stores in flight and the
@@ -1125,17 +1135,18 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     const size_t esz = rdc_dtype_size(dtype);
     if (esz == 0) throw std::invalid_argument("rdc: unsupported dtype");
     const size_t count = bytes / esz;
-    if (n_ == 1 || count == 0 || (uint64_t)count * esz <= cfg_.ring_mincount) return 0;
-    const int algo = PickAlgo(RDC_ALGO_AUTO, (uint64_t)count * esz);
-    if (algo != RDC_ALGO_MESH && algo != RDC_ALGO_RING) return 0;  // one-shot: a single hand-off, no roles
+    const uint64_t total = (uint64_t)count * esz;
+    if (n_ == 1 || count == 0 || total <= cfg_.ring_mincount || cfg_.algo != RDC_ALGO_AUTO) return 0;
+    const int rule = AutoAlgo(n_, total, layout(), cfg_.oneshot_push_max);
+    if (rule != RDC_ALGO_MESH && rule != RDC_ALGO_RING) return 0;  // one-shot: a single hand-off, no roles
     hip_check(hipSetDevice(device_), "hipSetDevice");
     void* buf = nullptr;
     double* dms = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    const int cls = SizeClass((uint64_t)count * esz) * 8 + algo;  // the key ShapeFor looks up
-    const auto had = tuned_.find(cls);
-    const bool had_shape = had != tuned_.end();
-    const Shape saved = had_shape ? had->second : Shape();
+    const int cls = SizeClass(total);
+    // state to restore on failure: the class's schedule and both shapes
+    const std::map<int, Shape> saved_shapes = tuned_;
+    const std::map<int, int> saved_algos = tuned_algo_;
     int nc = 0;
     auto release = [&] {
         if (buf) (void)hipFreeAsync(buf, stream);
@@ -1151,17 +1162,21 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
         hip_check(hipMemsetAsync(buf, 0, count * esz, stream), "autotune memset");
         hip_check(hipEventCreate(&e0), "event");
         hip_check(hipEventCreate(&e1), "event");
-        auto set_shape = [&](int s16, int r16, int grid, int tpb) {
+        // a candidate = schedule + shape, installed where PickAlgo / ShapeFor
+        // look them up for this size class
+        auto set_shape = [&](const TuneCand& c) {
             Shape s;
-            s.split.s16 = s16;
-            s.split.r16 = r16;
-            s.split.tpb = tpb;
-            s.max_blocks = grid;
-            tuned_[cls] = s;
+            s.split.s16 = c.s16;
+            s.split.r16 = c.r16;
+            s.split.tpb = c.tpb;
+            s.max_blocks = c.grid;
+            tuned_[cls * 8 + c.algo] = s;
+            tuned_algo_[cls] = c.algo;
         };
-        auto time_one = [&](int s16, int r16, int grid, int tpb) {
+        auto time_one = [&](int algo, int s16, int r16, int grid, int tpb) {
             if (nc >= max_cand) return;
-            set_shape(s16, r16, grid, tpb);
+            const TuneCand c{algo, s16, r16, grid, tpb, 0.0};
+            set_shape(c);
             Allreduce(buf, count, dtype, RDC_OP_SUM, stream, RDC_ALGO_AUTO);  // warm (and first-use work)
             hip_check(hipEventRecord(e0, stream), "record");
             for (int i = 0; i < reps; ++i) Allreduce(buf, count, dtype, RDC_OP_SUM, stream, RDC_ALGO_AUTO);
@@ -1169,7 +1184,8 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
             hip_check(hipEventSynchronize(e1), "sync");
             float ms = 0;
             hip_check(hipEventElapsedTime(&ms, e0, e1), "elapsed");
-            cand[nc++] = TuneCand{s16, r16, grid, tpb, (double)ms / reps};
+            cand[nc] = c;
+            cand[nc++].ms = (double)ms / reps;
         };
         // the slowest rank's time per candidate, identical on every rank;
         // returns the stage's winner (lowest index among equal times)
@@ -1190,39 +1206,51 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
             }
             return w;
         };
+        auto keep = [&](int w) {  // a stage's winner, already timed, carried into the next stage
+            if (nc < max_cand) cand[nc++] = cand[w];
+        };
         const int cus = cus_min_;
-        int w;
-        if (algo == RDC_ALGO_MESH) {
+        const int s0 = cfg_.mesh_split.s16, r0 = cfg_.mesh_split.r16;
+        // stage 0: the schedule (both bit-identical) with the configured shape
+        int lo = nc;
+        time_one(RDC_ALGO_RING, s0, r0, cfg_.max_blocks, cfg_.mesh_split.tpb);
+        time_one(RDC_ALGO_MESH, s0, r0, cfg_.max_blocks, cfg_.mesh_split.tpb);
+        int w = agree(lo);
+        if (cand[w].algo == RDC_ALGO_MESH) {
             static const int kSplits[][2] = {{4, 8}, {3, 9}, {5, 8}, {6, 6}, {3, 10}, {2, 10}, {5, 7}};
-            int lo = nc;
-            for (const auto& s : kSplits) time_one(s[0], s[1], 0, 0);
+            lo = nc;
+            keep(w);
+            for (const auto& sp : kSplits)
+                if (sp[0] != cand[w].s16 || sp[1] != cand[w].r16) time_one(RDC_ALGO_MESH, sp[0], sp[1], 0, 0);
             w = agree(lo);
             const int s16 = cand[w].s16, r16 = cand[w].r16;
             lo = nc;
-            for (int bpc : {1, 3, 4}) time_one(s16, r16, bpc * cus, 0);
-            if (nc < max_cand) cand[nc++] = cand[w];  // the auto grid (2 per CU), timed: kept in the stage
+            keep(w);
+            for (int bpc : {1, 2, 3, 4})  // (grid 0 = automatic = 2 per CU)
+                if (bpc * cus != (cand[w].grid ? cand[w].grid : 2 * cus)) time_one(RDC_ALGO_MESH, s16, r16, bpc * cus, 0);
             w = agree(lo);
             const int grid = cand[w].grid;
             lo = nc;
-            for (int tpb : {1, 4, 8}) time_one(s16, r16, grid, tpb);
-            if (nc < max_cand) cand[nc++] = cand[w];
+            keep(w);
+            for (int tpb : {1, 4, 8}) time_one(RDC_ALGO_MESH, s16, r16, grid, tpb);
             w = agree(lo);
         } else {
-            const int s16 = cfg_.mesh_split.s16, r16 = cfg_.mesh_split.r16;  // unused by the ring
-            int lo = nc;
-            for (int bpc : {1, 2}) time_one(s16, r16, bpc * cus, 0);
+            lo = nc;
+            keep(w);
+            for (int bpc : {1, 2})  // (grid 0 = automatic = 1 per CU)
+                if (bpc * cus != (cand[w].grid ? cand[w].grid : cus)) time_one(RDC_ALGO_RING, s0, r0, bpc * cus, 0);
             w = agree(lo);
             const int grid = cand[w].grid;
             lo = nc;
-            for (int tpb : {4, 8, 16, 32}) time_one(s16, r16, grid, tpb);
-            if (nc < max_cand) cand[nc++] = cand[w];
+            keep(w);
+            for (int tpb : {4, 8, 16, 32}) time_one(RDC_ALGO_RING, s0, r0, grid, tpb);
             w = agree(lo);
         }
-        set_shape(cand[w].s16, cand[w].r16, cand[w].grid, cand[w].tpb);
+        set_shape(cand[w]);
         *best = w;
     } catch (...) {
-        if (had_shape) tuned_[cls] = saved;
-        else tuned_.erase(cls);
+        tuned_ = saved_shapes;
+        tuned_algo_ = saved_algos;
         release();
         throw;
     }

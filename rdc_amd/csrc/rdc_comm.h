@@ -164,17 +164,20 @@ public:
     void Tune(int s16, int r16, int max_blocks, size_t tile_bytes);
 
     // Collective (every rank, same arguments, no collective in flight): time
-    // the launch shapes the automatic schedule for `bytes` of `dtype` can take
-    // (mesh: role split, then grid, then tiles per reduce block; ring: grid,
-    // then tiles per block — granularity that scales with the buffer), `reps`
+    // the schedules (ring vs mesh) and then the launch shapes of the faster one
+    // for `bytes` of `dtype` (mesh: role split, then grid, then tiles per
+    // reduce block; ring: grid, then tiles per block — granularity that scales
+    // with the buffer), `reps`
     // Sum allreduces each on a scratch buffer, agree on the per-candidate
     // times by a MAX allreduce over this communicator (every rank gets the
     // same bits, so the same winner), and keep the fastest for allreduces of
-    // the same size class ([2^k, 2^(k+1)) bytes: tuned_; Tune clears them).
-    // Candidates in cand[] ({s16, r16, grid, tpb, ms}; up to max_cand);
+    // the same size class ([2^k, 2^(k+1)) bytes: tuned_algo_ / tuned_; Tune
+    // clears them; nothing is tuned while RDC_ALGO forces a schedule).
+    // Candidates in cand[] ({algo, s16, r16, grid, tpb, ms}; up to max_cand);
     // returns their count and *best = the chosen index (-1: nothing to tune,
     // e.g. a one-shot / tree size).  Results stay bit-identical whatever wins.
     struct TuneCand {
+        int algo;                 // RDC_ALGO_MESH / RDC_ALGO_RING
         int s16, r16, grid, tpb;  // tpb: automatic tiles per block (MeshSplit::tpb), 0 = default
         double ms;
     };
@@ -219,7 +222,8 @@ public:
     };
     Shape ShapeFor(uint64_t total, int algo) const;
     static int SizeClass(uint64_t bytes);
-    std::map<int, Shape> tuned_;  // Autotune results by size class * 8 + algo; cleared by Tune
+    std::map<int, Shape> tuned_;     // Autotune results by size class * 8 + algo; cleared by Tune
+    std::map<int, int> tuned_algo_;  // Autotune's schedule by size class (PickAlgo); cleared by Tune
     int LaunchGrid(int want, int blocks_per_cu) const;
     bool shared_gpu() const { return share_max_ > 1; }
     int ranks_per_gpu() const { return share_max_; }

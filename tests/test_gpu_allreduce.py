@@ -608,9 +608,9 @@ def test_mp_full_grid_beside_resident_service():
 def test_mp_autotune_agrees_and_stays_bit_exact(world):
     """RdcCommAutotune (bench.py runs it before the timed region at N > 1):
     every rank keeps the same winner (times agreed by a MAX allreduce), the
-    stages cover the schedule the size takes (n = 2 above 8 MiB: ring grid /
-    tiles per block; n = 3: mesh split / grid / tiles per reduce block), a
-    one-shot size changes nothing,
+    stages cover the schedules (ring vs mesh) and then the winner's shape
+    (mesh split / grid / tiles per reduce block, or ring grid / tiles per
+    block), a one-shot size changes nothing,
     and the allreduces on the chosen shape stay bit-exact."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -631,7 +631,11 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
     t = tunes[0]
     assert t["chosen"] is not None and t["chosen"] in t["candidates"], t
     assert t["chosen"]["ms"] == min(c["ms"] for c in t["candidates"]), t
-    assert len(t["candidates"]) == (7 if world == 2 else 15), t
+    # stage 0 ring vs mesh, then (mesh) 7 splits, 4 grids, 4 tilings or (ring) 2 grids, 5 tilings,
+    # every later stage carrying its predecessor's winner
+    assert t["candidates"][0]["schedule"] == "ring" and t["candidates"][1]["schedule"] == "mesh", t
+    assert len(t["candidates"]) == (17 if t["chosen"]["schedule"] == "mesh" else 9), t
+    assert all(c["schedule"] == t["chosen"]["schedule"] for c in t["candidates"][2:]), t
 
 
 def test_mp_many_small_buckets_cfg5_shape():
