@@ -617,7 +617,13 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
     big = 8 << 20  # fp32 elements: 32 MiB
     cases = [{"count": 16384, "dtype": 6, "op": 2, "autotune": 65536},
              {"count": big, "dtype": 6, "op": 2, "autotune": big * 4, "reps": 2},
-             {"count": 100003, "dtype": 11, "op": 2, "algo": 2}]
+             {"count": 100003, "dtype": 11, "op": 2, "algo": 2},
+             # the tuned schedule / shape serve every dtype and op of the size class
+             {"count": 2 * big, "dtype": 10, "op": 2},
+             {"count": big + 12345, "dtype": 2, "op": 0},
+             {"count": big // 2 - 7, "dtype": 7, "op": 1},
+             # a coalesced list of the tuned size class keeps the unit-table mesh whichever schedule won
+             {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1 << 20] * 8}]
     tmp = run_mp(world, cases, timeout=400)
     for i, c in enumerate(cases):
         want = expected_for(c, world)
