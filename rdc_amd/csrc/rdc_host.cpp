@@ -23,7 +23,20 @@ int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
 }
-constexpr size_t kPieceTarget = (size_t)16 << 20;  // bytes of all chunks' slices per piece
+// Buffers up to kOnePieceMax go as ONE piece on the caller's thread; larger
+// ones through the pipeline in pieces of piece_target() bytes of all chunks'
+// slices (RDC_HOST_PIECE_BYTES, default 8 MiB: n = 2 on one GPU, 64 MiB
+// 4.7-4.9 ms vs 6.3-7.6 ms with 16 MiB pieces, 256 MiB 15-20 vs 19-23 ms;
+// profiles/r02/host_pieces/)
+constexpr size_t kOnePieceMax = (size_t)16 << 20;
+size_t piece_target() {
+    static const size_t v = [] {
+        const char* e = getenv("RDC_HOST_PIECE_BYTES");
+        const long long x = e ? atoll(e) : 0;
+        return x >= (1 << 20) ? (size_t)x : (size_t)8 << 20;
+    }();
+    return v;
+}
 constexpr size_t kParallelMin = (size_t)512 << 10;  // below this a copy runs on the caller alone (waking the pool costs more)
 // RDC_HOST_TRACE=1: per-piece timeline on stderr (diagnostics)
 double trace_now() {
@@ -240,12 +253,12 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
     SplitRanges((int64_t)count, n, cb, ce);
     const uint64_t maxlen = (uint64_t)(ce[0] - cb[0]) * esz;  // the first chunk is never shorter
     // slice length per chunk and piece: a multiple of 4 KiB (hence of esz)
-    const uint64_t K0 = std::max<uint64_t>(1, (S + kPieceTarget - 1) / kPieceTarget);
+    const uint64_t K0 = S <= kOnePieceMax ? 1 : std::max<uint64_t>(1, (S + piece_target() - 1) / piece_target());
     const uint64_t sl = std::max<uint64_t>(4096, ((maxlen + K0 - 1) / K0 + 4095) & ~(uint64_t)4095);
     const int K = (int)((maxlen + sl - 1) / sl);
     Reserve((size_t)sl * (size_t)n, S, K, comm_stream);
     if (K == 1) {
-        // one piece (up to kPieceTarget): nothing to overlap, so no drain
+        // one piece (up to the piece target): nothing to overlap, so no drain
         // thread hand-off either — the slices of one piece are the chunks in
         // order, i.e. the whole buffer: pool copy into a pinned slot, H2D,
         // allreduce, pageable D2H straight into the caller's buffer, all on
