@@ -19,6 +19,7 @@
 #include "rdc_kernels.h"
 #include "rdc_p2p.h"
 #include "rdc_plan.h"
+#include "rdc_host.h"
 #include "rdc_service.h"
 
 namespace rdc_amd {
@@ -66,6 +67,8 @@ void dbg(const char* fmt, int rank, const char* what) {
     }
 }
 
+constexpr int kPlanKeys = 15;  // PlanKey below; sizes PeerInfo::plan
+
 struct PeerInfo {
     uint64_t channel;   // id of the live channel this rank would share (0 = none)
     int32_t device;
@@ -77,7 +80,7 @@ struct PeerInfo {
     uint64_t p2p_slot_bytes;
     int32_t num_cus;
     int32_t pad2;
-    uint64_t plan[14];  // PlanKey: the parameters that shape a launch plan (must agree)
+    uint64_t plan[kPlanKeys];  // PlanKey: the parameters that shape a launch plan (must agree)
     char host[64];
     char pci[32];  // physical GPU (ranks may share one: tests, emulation)
 };
@@ -96,21 +99,20 @@ struct Handles {  // round 2 of Create: IPC handles (scratch ones only for a new
 // Every parameter a plan depends on is exchanged at creation and compared.
 // The small-allreduce service's switches too: a rank that serves a small host
 // buffer through it while a peer launches a kernel would wait out RDC_TIMEOUT.
-constexpr int kPlanKeys = 14;
-void PlanKey(const CommConfig& c, uint64_t* k) {
+void PlanKey(const CommConfig& c, uint64_t (&k)[kPlanKeys]) {
     const uint64_t v[kPlanKeys] = {(uint64_t)c.algo, (uint64_t)c.max_blocks, (uint64_t)c.tile_bytes,
                                    (uint64_t)c.oneshot_push_max, (uint64_t)c.fuse_bytes, (uint64_t)c.coalesce_fused,
                                    (uint64_t)c.fuse_bytes_direct, (uint64_t)c.bcast_split_bytes,
                                    (uint64_t)c.mesh_split.s16, (uint64_t)c.mesh_split.r16, (uint64_t)c.ring_mincount,
                                    (uint64_t)c.scratch_bytes, (uint64_t)SmallService::Enabled(),
-                                   (uint64_t)SmallService::ShareMax()};
+                                   (uint64_t)SmallService::ShareMax(), (uint64_t)HostPieceBytes()};
     memcpy(k, v, sizeof(v));
 }
 const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_ONESHOT_BYTES",
                                         "RDC_FUSE_BYTES", "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT",
                                         "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "RDC_MESH_SPLIT",
                                         "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES", "RDC_HOST_SERVICE",
-                                        "RDC_HOST_SERVICE_SHARE_MAX"};
+                                        "RDC_HOST_SERVICE_SHARE_MAX", "RDC_HOST_PIECE_BYTES"};
 
 // The point-to-point control block (rdc_p2p.h) in POSIX shared memory: rank 0
 // creates it, every rank maps it, rank 0 unlinks the name once all mapped.

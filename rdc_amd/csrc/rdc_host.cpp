@@ -29,14 +29,7 @@ int env_int(const char* name, int dflt) {
 // 4.7-4.9 ms vs 6.3-7.6 ms with 16 MiB pieces, 256 MiB 15-20 vs 19-23 ms;
 // profiles/r02/host_pieces/)
 constexpr size_t kOnePieceMax = (size_t)16 << 20;
-size_t piece_target() {
-    static const size_t v = [] {
-        const char* e = getenv("RDC_HOST_PIECE_BYTES");
-        const long long x = e ? atoll(e) : 0;
-        return x >= (1 << 20) ? (size_t)x : (size_t)8 << 20;
-    }();
-    return v;
-}
+size_t piece_target() { return HostPieceBytes(); }
 constexpr size_t kParallelMin = (size_t)512 << 10;  // below this a copy runs on the caller alone (waking the pool costs more)
 // RDC_HOST_TRACE=1: per-piece timeline on stderr (diagnostics)
 double trace_now() {
@@ -49,6 +42,15 @@ bool tracing() {
     return on;
 }
 }  // namespace
+
+size_t HostPieceBytes() {
+    static const size_t v = [] {
+        const char* e = getenv("RDC_HOST_PIECE_BYTES");
+        const long long x = e ? atoll(e) : 0;
+        return x >= (1 << 20) ? (size_t)x : (size_t)8 << 20;
+    }();
+    return v;
+}
 
 // ---------------------------------------------------------------- HostPath --
 // wait for an event by polling it: a blocking synchronisation may sleep and

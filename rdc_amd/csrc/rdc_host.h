@@ -29,6 +29,11 @@
 
 namespace rdc_amd {
 
+// RDC_HOST_PIECE_BYTES (default 8 MiB): every rank cuts a pipelined host
+// buffer into the same pieces, so it is one of the plan keys agreed at
+// communicator creation (rdc_comm.cpp PlanKey)
+size_t HostPieceBytes();
+
 // fixed pool of memcpy threads; Run(n, f) calls f(0..n-1) across the pool
 // and the caller, returning when all are done
 

@@ -903,7 +903,7 @@ except Exception as e:  # the expected path
 
 
 @pytest.mark.parametrize("key,value", [("RDC_TILE_BYTES", "1M"), ("RDC_HOST_SERVICE", "0"),
-                                       ("RDC_HOST_SERVICE_SHARE_MAX", "2")])
+                                       ("RDC_HOST_SERVICE_SHARE_MAX", "2"), ("RDC_HOST_PIECE_BYTES", "4194304")])
 def test_mp_plan_disagreement_is_refused(key, value):
     """Ranks whose launch-plan parameters differ (one rank's env) are refused
     at communicator creation with the parameter named, on every rank: a
