@@ -155,15 +155,17 @@ def time_ring(lib, comm, buf, count, dt_enum, sp, dist, torch, steps):
     return timed_ms(one, comm, sp, dist, torch, steps)
 
 
-def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out):
+def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, autotune_reps=0):
     """The other BASELINE.json configs on the same communicator, after the
     timed region (informational): cfg4 = fp16 allreduce of a buffer of S
     bytes, cfg5 = 1024 buckets of S/1024 bytes fp32 in one coalesced call,
     cfg1 = a 4 KiB fp32 allreduce of HOST memory through the reference's own
     entry point (RdcAllreduce on a numpy array: pinned zero-copy launch, the
     real host path) and cfg2's 256 MiB fp32 buffer, with a device size curve
-    4 KiB - 256 MiB (`sizes_fp32`).  ms per step = max over ranks of the wall
-    time of `steps` calls.  Fills `out` as it goes."""
+    4 KiB - 256 MiB (`sizes_fp32`: the automatic rule's schedule and shape,
+    then, with autotune on, the same size after RdcCommAutotune for its size
+    class).  ms per step = max over ranks of the wall time of `steps` calls.
+    Fills `out` as it goes."""
     from rdc_amd._lib import check_call
     import numpy as np
     import rdc_amd
@@ -218,10 +220,20 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out):
         # small calls: enough of them that the closing device sync + barrier
         # (~1 ms with gloo) is noise (50 calls made it 20 us of a 4 KiB call)
         ns = max(steps, 2000 if nb <= (64 << 10) else 400 if nb <= (1 << 20) else 50 if nb <= (16 << 20) else 0)
-        ms = timed(lambda: check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(f.data_ptr()),
-                                                             nb // 4, 6, 2, 0, sp)), ns)
+        def one():
+            check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(f.data_ptr()), nb // 4, 6, 2, 0, sp))
+        ms = timed(one, ns)
         e = entry(ms, nb, "in-place allreduce(sum) of %d KiB float32" % (nb >> 10), ns)
         sizes[str(nb)] = {k: e[k] for k in ("ms_per_step", "busbw_GBps", "steps")}
+        if autotune_reps > 0 and nb < S:
+            t = comm.autotune(nb, 6, reps=autotune_reps, stream=sp)
+            if t["chosen"] is not None:
+                ms_t = timed(one, ns)
+                sizes[str(nb)].update({"tuned_ms_per_step": round(ms_t, 4),
+                                       "tuned_busbw_GBps": round(nb / (ms_t * 1e-3) / 1e9 * 2 * (world - 1)
+                                                                 / world, 2),
+                                       "tuned": {k: t["chosen"][k] for k in ("schedule", "split", "grid",
+                                                                             "tiles_per_block")}})
         if nb == (256 << 20):
             out["cfg2_256MiB"] = e
     del f
@@ -574,7 +586,8 @@ def main():
     if multi and f32 and args.extra_steps > 0:
         part = {}
         extra = guarded("extra_configs", lambda: time_extra_configs(_LIB, comm, S, world, rank, sp, dist, torch,
-                                                                    args.extra_steps, part), partial=part)
+                                                                    args.extra_steps, part, args.autotune_reps),
+                        partial=part)
     if multi and f32 and not args.no_check:
         part_c = {}
         checks = guarded("parity_checks", lambda: parity_checks(_LIB, comm, S, world, rank, sp, dist, torch, part_c),

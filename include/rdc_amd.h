@@ -211,8 +211,9 @@ int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, dou
 int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t tile_bytes);
 
 /* Autotune (collective: every rank of `comm`, same arguments, no collective in
- * flight; blocks the host): time the ring and the mesh schedule, then the
- * launch shapes of the faster one, for `bytes` of `dtype` on this node — mesh: role split, then grid, then
+ * flight; blocks the host): time the ring, the mesh and (where it fits half a
+ * slot) the one-shot schedule, then the launch shapes of the fastest, for
+ * `bytes` of `dtype` on this node — mesh: role split, then grid, then
  * tiles per reduce block; ring: grid, then tiles per block (a granularity, so
  * the chosen tiles scale with later buffers' sizes) — `reps` Sum allreduces each on a scratch
  * buffer; agree on the per-candidate times with a MAX allreduce over `comm`
@@ -223,10 +224,10 @@ int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t t
  * RDC_ALGO forces a schedule).  cand (room for max_cand; 16 suffices)
  * receives every timed candidate with its slowest-rank ms; *ncand their count,
  * *best the chosen index (-1 and nothing changed for sizes that take the
- * one-shot or tree path).  Results stay bit-identical whatever wins.  No
+ * tree order, rdc_reduce_ring_mincount).  Results stay bit-identical whatever wins.  No
  * reference counterpart (the reference's schedule has no launch shape). */
 typedef struct {
-    int algo;                           /* RDC_ALGO_RING (1) or RDC_ALGO_MESH (2) */
+    int algo;                           /* RDC_ALGO_RING (1), RDC_ALGO_MESH (2), RDC_ALGO_ONESHOT (3) */
     int mesh_s16, mesh_r16, max_blocks; /* max_blocks 0 = automatic grid */
     int tiles_per_block;                /* 0 = default (mesh 2 per reduce block, ring 1) */
     double ms;                          /* per allreduce, max over ranks */

@@ -186,12 +186,12 @@ class Comm(object):
         check_call(_LIB.RdcCommTune(self.handle, int(mesh_s16), int(mesh_r16), int(max_blocks), int(tile_bytes)))
 
     def autotune(self, nbytes, dtype=None, reps=3, stream=None):
-        """Collective (every rank, same arguments): time the ring and the mesh,
-        then the launch shapes of the faster one for allreduces of `nbytes`
+        """Collective (every rank, same arguments): time the ring, the mesh and
+        (where it fits) the one-shot, then the launch shapes of the fastest for allreduces of `nbytes`
         (mesh role split, grid, tiles per block), agree on the slowest rank's times and keep the
         fastest (RdcCommAutotune).  Returns {"chosen": {...} or None,
-        "candidates": [{...,"ms"}]}; None chosen = the size takes the one-shot
-        or tree path and nothing changed.  Results stay bit-identical."""
+        "candidates": [{...,"ms"}]}; None chosen = the size takes the tree
+        order and nothing changed.  Results stay bit-identical."""
         if dtype is None:
             dtype = 6  # mpi::kFloat32
         elif not isinstance(dtype, int):
@@ -207,7 +207,7 @@ class Comm(object):
                                         ctypes.byref(best)))
 
         def row(c):
-            return {"schedule": {1: "ring", 2: "mesh"}.get(c.algo, c.algo),
+            return {"schedule": {1: "ring", 2: "mesh", 3: "oneshot"}.get(c.algo, c.algo),
                     "split": [c.mesh_s16, c.mesh_r16], "grid": c.max_blocks or "auto",
                     "tiles_per_block": c.tiles_per_block or "auto", "ms": round(c.ms, 4)}
         rows = [row(cand[k]) for k in range(nc.value)]

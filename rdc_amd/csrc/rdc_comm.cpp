@@ -630,8 +630,9 @@ int Communicator::PickAlgo(int algo, uint64_t bytes) const {
     if (algo == RDC_ALGO_AUTO) {
         algo = AutoAlgo(n_, bytes, layout(), cfg_.oneshot_push_max);
         // a schedule Autotune measured for this size class replaces the
-        // rule's mesh / ring choice (never a one-shot or tree size)
-        if (algo == RDC_ALGO_MESH || algo == RDC_ALGO_RING) {
+        // rule's mesh / ring / one-shot choice (never a tree-order size; a
+        // one-shot that does not fit half a slot falls back below)
+        if (algo == RDC_ALGO_MESH || algo == RDC_ALGO_RING || algo == RDC_ALGO_ONESHOT) {
             const auto it = tuned_algo_.find(SizeClass(bytes));
             if (it != tuned_algo_.end()) algo = it->second;
         }
@@ -1122,8 +1123,8 @@ void Communicator::Tune(int s16, int r16, int max_blocks, size_t tile_bytes) {
 }
 
 // Schedule and launch-shape autotuning for one buffer size (rdc_comm.h).
-// Stage 0 times the ring and the mesh (bit-identical; the rule picks the ring
-// at n = 2 and the mesh from n = 3 on byte counts alone).  The defaults
+// Stage 0 times the ring, the mesh and (where it fits) the one-shot — all
+// bit-identical; the rule picks among them on byte counts alone.  The defaults
 // (4 / 8 / 4 split, 2 blocks per CU, ~2 tiles per reduce block) were tuned on
 // one GPU where HBM is the bound; over xGMI the balance between the copy
 // roles and the reduce role, the number of remote stores in flight and the
@@ -1140,7 +1141,8 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     const uint64_t total = (uint64_t)count * esz;
     if (n_ == 1 || count == 0 || total <= cfg_.ring_mincount || cfg_.algo != RDC_ALGO_AUTO) return 0;
     const int rule = AutoAlgo(n_, total, layout(), cfg_.oneshot_push_max);
-    if (rule != RDC_ALGO_MESH && rule != RDC_ALGO_RING) return 0;  // one-shot: a single hand-off, no roles
+    if (rule != RDC_ALGO_MESH && rule != RDC_ALGO_RING && rule != RDC_ALGO_ONESHOT) return 0;
+    const bool oneshot_fits = OneshotEligible(n_, total, layout(), (uint64_t)-1);
     hip_check(hipSetDevice(device_), "hipSetDevice");
     void* buf = nullptr;
     double* dms = nullptr;
@@ -1213,12 +1215,16 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
         };
         const int cus = cus_min_;
         const int s0 = cfg_.mesh_split.s16, r0 = cfg_.mesh_split.r16;
-        // stage 0: the schedule (both bit-identical) with the configured shape
+        // stage 0: the schedule (all bit-identical) with the configured shape;
+        // the one-shot (one hand-off, (n-1) x the egress) where it fits
         int lo = nc;
         time_one(RDC_ALGO_RING, s0, r0, cfg_.max_blocks, cfg_.mesh_split.tpb);
         time_one(RDC_ALGO_MESH, s0, r0, cfg_.max_blocks, cfg_.mesh_split.tpb);
+        if (oneshot_fits) time_one(RDC_ALGO_ONESHOT, s0, r0, cfg_.max_blocks, cfg_.mesh_split.tpb);
         int w = agree(lo);
-        if (cand[w].algo == RDC_ALGO_MESH) {
+        if (cand[w].algo == RDC_ALGO_ONESHOT) {
+            // no roles or tiles to shape: the schedule is the result
+        } else if (cand[w].algo == RDC_ALGO_MESH) {
             static const int kSplits[][2] = {{4, 8}, {3, 9}, {5, 8}, {6, 6}, {3, 10}, {2, 10}, {5, 7}};
             lo = nc;
             keep(w);

@@ -164,7 +164,8 @@ public:
     void Tune(int s16, int r16, int max_blocks, size_t tile_bytes);
 
     // Collective (every rank, same arguments, no collective in flight): time
-    // the schedules (ring vs mesh) and then the launch shapes of the faster one
+    // the schedules (ring, mesh, one-shot where it fits) and then the launch
+    // shapes of the fastest
     // for `bytes` of `dtype` (mesh: role split, then grid, then tiles per
     // reduce block; ring: grid, then tiles per block — granularity that scales
     // with the buffer), `reps`
@@ -175,9 +176,9 @@ public:
     // clears them; nothing is tuned while RDC_ALGO forces a schedule).
     // Candidates in cand[] ({algo, s16, r16, grid, tpb, ms}; up to max_cand);
     // returns their count and *best = the chosen index (-1: nothing to tune,
-    // e.g. a one-shot / tree size).  Results stay bit-identical whatever wins.
+    // a tree-order size).  Results stay bit-identical whatever wins.
     struct TuneCand {
-        int algo;                 // RDC_ALGO_MESH / RDC_ALGO_RING
+        int algo;                 // RDC_ALGO_MESH / RDC_ALGO_RING / RDC_ALGO_ONESHOT
         int s16, r16, grid, tpb;  // tpb: automatic tiles per block (MeshSplit::tpb), 0 = default
         double ms;
     };

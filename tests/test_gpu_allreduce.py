@@ -608,9 +608,9 @@ def test_mp_full_grid_beside_resident_service():
 def test_mp_autotune_agrees_and_stays_bit_exact(world):
     """RdcCommAutotune (bench.py runs it before the timed region at N > 1):
     every rank keeps the same winner (times agreed by a MAX allreduce), the
-    stages cover the schedules (ring vs mesh) and then the winner's shape
-    (mesh split / grid / tiles per reduce block, or ring grid / tiles per
-    block), a one-shot size changes nothing,
+    stages cover the schedules (ring, mesh, one-shot where it fits) and then
+    the winner's shape (mesh split / grid / tiles per reduce block, or ring
+    grid / tiles per block),
     and the allreduces on the chosen shape stay bit-exact."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -631,7 +631,11 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
             got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
     small = [json.load(open(os.path.join(tmp, "case0_rank%d.tune" % r))) for r in range(world)]
-    assert all(t == {"chosen": None, "candidates": []} for t in small), small
+    assert all(t == small[0] for t in small), small
+    # a one-shot size: ring, mesh and one-shot timed, then the winner's shape if it has one
+    assert [c["schedule"] for c in small[0]["candidates"][:3]] == ["ring", "mesh", "oneshot"], small[0]
+    if small[0]["chosen"]["schedule"] == "oneshot":
+        assert len(small[0]["candidates"]) == 3, small[0]
     tunes = [json.load(open(os.path.join(tmp, "case1_rank%d.tune" % r))) for r in range(world)]
     assert all(t == tunes[0] for t in tunes), tunes  # identical bits on every rank
     t = tunes[0]
