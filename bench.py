@@ -533,11 +533,13 @@ def main():
         sync_check(comm, sp, dist, torch)
     wall = t1 - t0
     kern_ms = e0.elapsed_time(e1) / args.steps
-    timed_algo = None
-    if world > 1:  # the schedule the library chose for the timed launches
+    timed_algo = timed_launch = None
+    if world > 1:  # the schedule and launch shape the library used for the timed launches
         ll = (ctypes.c_uint64 * 6)()
         if _LIB.RdcCommLastLaunch(comm.handle, ll) == 0:
             timed_algo = {1: "ring", 2: "mesh", 3: "oneshot", 4: "tree"}.get(int(ll[5]))
+            timed_launch = {"schedule": timed_algo, "grid": int(ll[0]), "scatter_blocks": int(ll[1]),
+                            "reduce_blocks": int(ll[2]), "gather_blocks": int(ll[3]), "tile_bytes": int(ll[4])}
     if world > 1:
         tt = torch.tensor([wall, kern_ms], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -660,6 +662,8 @@ def main():
                 args.buckets, (S // args.buckets) >> 10, args.dtype, S >> 20,
                 "separate calls" if args.unfused else "one coalesced call", algo_name)
         par = "dp%d (one process per GPU, xGMI P2P)" % world
+        if timed_launch is not None:
+            timed_launch["note"] = "last launch of the timed region (RdcCommLastLaunch)"
     out = {
         "metric": "allreduce GB/s (device-resident fp32) at 1/2/4/8 GPUs; % xGMI roofline",
         "value": round(value, 2),
@@ -673,7 +677,8 @@ def main():
         "vs_baseline": None,
         "dtype": DT_SHORT[args.dtype],
         "data": "synthetic (splitmix64 device generator, seed 0x5EED0000)",
-        "config": {"workload": workload, "bytes_per_gpu": S, "parallelism": par},
+        "config": dict({"workload": workload, "bytes_per_gpu": S, "parallelism": par},
+                       **({"launch": timed_launch} if timed_launch is not None else {})),
         "value_definition": "reduce kernel alone: S / t" if world == 1 else
                             "busbw = S / t x 2(n-1)/n (algbw_GBps = S / t)",
         "algbw_GBps": round(S / (wall / args.steps) / 1e9, 2),
