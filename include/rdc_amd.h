@@ -221,7 +221,9 @@ int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t t
  * fastest schedule and shape for allreduces of that size class ([2^k,
  * 2^(k+1)) bytes; other sizes keep the automatic rule and the configured
  * shape, RdcCommTune clears every autotuned one, and nothing is tuned while
- * RDC_ALGO forces a schedule).  cand (room for max_cand; 16 suffices)
+ * RDC_ALGO forces a schedule; with RDC_TUNE_FILE set, rank 0 appends the
+ * winner there and later communicators of the same rank and CU count start
+ * from it).  cand (room for max_cand; 16 suffices)
  * receives every timed candidate with its slowest-rank ms; *ncand their count,
  * *best the chosen index (-1 and nothing changed for sizes that take the
  * tree order, rdc_reduce_ring_mincount).  Results stay bit-identical whatever wins.  No

@@ -67,7 +67,7 @@ void dbg(const char* fmt, int rank, const char* what) {
     }
 }
 
-constexpr int kPlanKeys = 15;  // PlanKey below; sizes PeerInfo::plan
+constexpr int kPlanKeys = 16;  // PlanKey below; sizes PeerInfo::plan
 
 struct PeerInfo {
     uint64_t channel;   // id of the live channel this rank would share (0 = none)
@@ -99,20 +99,59 @@ struct Handles {  // round 2 of Create: IPC handles (scratch ones only for a new
 // Every parameter a plan depends on is exchanged at creation and compared.
 // The small-allreduce service's switches too: a rank that serves a small host
 // buffer through it while a peer launches a kernel would wait out RDC_TIMEOUT.
-void PlanKey(const CommConfig& c, uint64_t (&k)[kPlanKeys]) {
+void PlanKey(const CommConfig& c, uint64_t tune_hash, uint64_t (&k)[kPlanKeys]) {
     const uint64_t v[kPlanKeys] = {(uint64_t)c.algo, (uint64_t)c.max_blocks, (uint64_t)c.tile_bytes,
                                    (uint64_t)c.oneshot_push_max, (uint64_t)c.fuse_bytes, (uint64_t)c.coalesce_fused,
                                    (uint64_t)c.fuse_bytes_direct, (uint64_t)c.bcast_split_bytes,
                                    (uint64_t)c.mesh_split.s16, (uint64_t)c.mesh_split.r16, (uint64_t)c.ring_mincount,
                                    (uint64_t)c.scratch_bytes, (uint64_t)SmallService::Enabled(),
-                                   (uint64_t)SmallService::ShareMax(), (uint64_t)HostPieceBytes()};
+                                   (uint64_t)SmallService::ShareMax(), (uint64_t)HostPieceBytes(), tune_hash};
     memcpy(k, v, sizeof(v));
 }
 const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_ONESHOT_BYTES",
                                         "RDC_FUSE_BYTES", "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT",
                                         "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "RDC_MESH_SPLIT",
                                         "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES", "RDC_HOST_SERVICE",
-                                        "RDC_HOST_SERVICE_SHARE_MAX", "RDC_HOST_PIECE_BYTES"};
+                                        "RDC_HOST_SERVICE_SHARE_MAX", "RDC_HOST_PIECE_BYTES",
+                                        "RDC_TUNE_FILE (contents)"};
+
+// Autotune results kept across runs (RDC_TUNE_FILE): one line per winner,
+// "rdc-tune 1 <ranks> <cus> <size class> <algo> <s16> <r16> <grid> <tpb> <ms>",
+// later lines overriding earlier ones.  Every rank reads the file itself at
+// communicator creation; its contents' hash is a plan key, so ranks that read
+// different tables are refused instead of planning differently.  Only rank 0
+// appends (Communicator::Autotune).
+struct TuneEntry {
+    int n, cus, cls, algo, s16, r16, grid, tpb;
+};
+std::string tune_file() {
+    const char* e = getenv("RDC_TUNE_FILE");
+    return e && *e ? std::string(e) : std::string();
+}
+std::vector<TuneEntry> read_tune_file(const std::string& path, uint64_t* hash) {
+    std::vector<TuneEntry> out;
+    *hash = 0;
+    if (path.empty()) return out;
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) return out;  // no table yet: nothing tuned (hash 0 on every rank)
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over the bytes
+    char line[256];
+    while (fgets(line, sizeof(line), f)) {
+        for (const char* p = line; *p; ++p) h = (h ^ (unsigned char)*p) * 1099511628211ull;
+        TuneEntry e;
+        int ver = 0;
+        double ms = 0;
+        if (sscanf(line, "rdc-tune %d %d %d %d %d %d %d %d %d %lf", &ver, &e.n, &e.cus, &e.cls, &e.algo, &e.s16,
+                   &e.r16, &e.grid, &e.tpb, &ms) == 10 &&
+            ver == 1 && e.cls >= 0 && e.cls < 64 &&
+            (e.algo == RDC_ALGO_RING || e.algo == RDC_ALGO_MESH || e.algo == RDC_ALGO_ONESHOT) && e.s16 >= 1 &&
+            e.r16 >= 1 && e.s16 + e.r16 <= 15 && e.grid >= 0 && e.tpb >= 0)
+            out.push_back(e);
+    }
+    fclose(f);
+    *hash = h;
+    return out;
+}
 
 // The point-to-point control block (rdc_p2p.h) in POSIX shared memory: rank 0
 // creates it, every rank maps it, rank 0 unlinks the name once all mapped.
@@ -381,7 +420,9 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     mine.slot_bytes = L.slot_bytes;
     mine.max_tiles = L.max_tiles;
     mine.num_cus = c->num_cus_;
-    PlanKey(cfg, mine.plan);
+    uint64_t tune_hash = 0;
+    const std::vector<TuneEntry> tuned = read_tune_file(tune_file(), &tune_hash);
+    PlanKey(cfg, tune_hash, mine.plan);
     std::shared_ptr<Channel> cand;
     if (share_enabled()) {
         std::lock_guard<std::mutex> lk(g_reg_mu);
@@ -431,6 +472,19 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         for (int q = 0; q < c->n_; ++q) same += strncmp(all[(size_t)p].pci, all[(size_t)q].pci, sizeof(mine.pci)) == 0;
         c->share_max_ = std::max(c->share_max_, same);
     }
+    // schedules and shapes an earlier Autotune of this node measured for this
+    // rank count and CU count (RDC_TUNE_FILE); every rank read the same table
+    if (cfg.algo == RDC_ALGO_AUTO)
+        for (const TuneEntry& e : tuned) {
+            if (e.n != c->n_ || e.cus != c->cus_min_) continue;
+            Shape s;
+            s.split.s16 = e.s16;
+            s.split.r16 = e.r16;
+            s.split.tpb = e.tpb;
+            s.max_blocks = e.grid;
+            c->tuned_[e.cls * 8 + e.algo] = s;
+            c->tuned_algo_[e.cls] = e.algo;
+        }
     // direct peer access between distinct devices (xGMI); IPC mapping with
     // hipIpcMemLazyEnablePeerAccess covers the rest.
     for (int p = 0; p < c->n_; ++p) {
@@ -1255,6 +1309,21 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
             w = agree(lo);
         }
         set_shape(cand[w]);
+        const std::string tf = tune_file();
+        if (!tf.empty()) {
+            // rank 0 records the winner; the closing collective keeps every
+            // rank from reading the table (a new communicator) before it has
+            if (rank_ == 0) {
+                FILE* f = fopen(tf.c_str(), "a");
+                if (!f) throw std::runtime_error("rdc: cannot append to RDC_TUNE_FILE " + tf);
+                fprintf(f, "rdc-tune 1 %d %d %d %d %d %d %d %d %.4f\n", n_, cus_min_, cls, cand[w].algo, cand[w].s16,
+                        cand[w].r16, cand[w].grid, cand[w].tpb, cand[w].ms);
+                fclose(f);
+            }
+            hip_check(hipMemsetAsync(dms, 0, sizeof(double), stream), "memset");
+            Allreduce(dms, 1, RDC_DT_FLOAT64, RDC_OP_MAX, stream, RDC_ALGO_AUTO);
+            Check(stream);
+        }
         *best = w;
     } catch (...) {
         tuned_ = saved_shapes;

@@ -648,6 +648,37 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
     assert all(c["schedule"] == t["chosen"]["schedule"] for c in t["candidates"][2:]), t
 
 
+def test_mp_tune_file_persists_autotune():
+    """RDC_TUNE_FILE: rank 0 appends the winner of RdcCommAutotune; a later
+    job on the same node (new processes, no autotune) loads it at
+    communicator creation and launches the same schedule and shape, still
+    bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    big = 8 << 20
+    path = os.path.join(tempfile.mkdtemp(prefix="rdc_tune_"), "tune.txt")
+    env = {"RDC_TUNE_FILE": path}
+    first = run_mp(2, [{"count": big, "dtype": 6, "op": 2, "autotune": big * 4, "last_launch": True}],
+                   timeout=400, env_extra=env)
+    lines = open(path).read().splitlines()
+    assert len(lines) == 1 and lines[0].startswith("rdc-tune 1 2 "), lines
+    second = run_mp(2, [{"count": big, "dtype": 6, "op": 2, "last_launch": True},
+                        {"count": big + 3, "dtype": 10, "op": 2, "last_launch": True}], env_extra=env)
+    tuned = json.load(open(os.path.join(first, "case0_rank0.tune")))
+    for r in range(2):
+        a = json.load(open(os.path.join(first, "case0_rank%d.launch" % r)))
+        b = json.load(open(os.path.join(second, "case0_rank%d.launch" % r)))
+        assert a == b, (a, b, tuned)
+        assert {1: "ring", 2: "mesh", 3: "oneshot"}[b[5]] == tuned["chosen"]["schedule"], (b, tuned)
+    for tmp, cases in ((first, [{"count": big, "dtype": 6, "op": 2}]),
+                       (second, [{"count": big, "dtype": 6, "op": 2}, {"count": big + 3, "dtype": 10, "op": 2}])):
+        for i, c in enumerate(cases):
+            want = expected_for(c, 2)
+            for r in range(2):
+                got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+                assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (tmp, i, r)
+
+
 def test_mp_many_small_buckets_cfg5_shape():
     """test/mallreduce.cc shape: back-to-back 1 MiB fp32 allreduces on one buffer."""
     if not torch.cuda.is_available():
