@@ -664,6 +664,9 @@ def main():
         par = "dp%d (one process per GPU, xGMI P2P)" % world
         if timed_launch is not None:
             timed_launch["note"] = "last launch of the timed region (RdcCommLastLaunch)"
+            timed_launch["source"] = ("RdcCommAutotune on this node before the warm-up (see `autotune`)"
+                                      if isinstance(tuned, dict) and tuned.get("chosen") else
+                                      "library defaults (automatic rule)")
     out = {
         "metric": "allreduce GB/s (device-resident fp32) at 1/2/4/8 GPUs; % xGMI roofline",
         "value": round(value, 2),
