@@ -212,14 +212,29 @@ __device__ __forceinline__ void mesh_reduce_tile(const CollArgs& a, int t, uint6
 // works on the unit pieces of its tile directly, so no staging image exists.
 __device__ __forceinline__ int unit_first(const PackUnit* u, int nunits, uint64_t pos) {
     __shared__ int s_first;
-    if (threadIdx.x == 0) {  // first unit whose range ends after pos
-        int lo = 0, hi = nunits;
+    if (threadIdx.x < 64) {
+        // first unit whose range ends after pos: a 64-ary search by wave 0
+        // (each pass one load per lane, all in flight together) — 2 passes
+        // for cfg5's 1024 buckets instead of 10 dependent loads by one lane.
+        // ends(i) <= pos is monotone in i: the lanes that see it true are a
+        // prefix, and the answer lies after the last of them.
+        const int lane = threadIdx.x;
+        int lo = 0, hi = nunits;  // answer in [lo, hi]
         while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (u[mid].packed + u[mid].len <= pos) lo = mid + 1;
-            else hi = mid;
+            const int step = (hi - lo + 63) >> 6;
+            const int idx = lo + lane * step;
+            const bool before = idx < hi && u[idx].packed + u[idx].len <= pos;
+            const int k = __popcll(__ballot(before));  // lanes 0..k-1 are before pos
+            if (k == 0) {
+                hi = lo;  // u[lo] already ends after pos
+            } else {
+                const int nlo = lo + (k - 1) * step + 1;
+                const int nhi = lo + k * step;
+                lo = nlo;
+                if (nhi < hi) hi = nhi;
+            }
         }
-        s_first = lo;
+        if (lane == 0) s_first = lo;
     }
     __syncthreads();
     const int f = s_first;
