@@ -118,7 +118,8 @@ COALESCED = [
 @pytest.mark.parametrize("n,counts", COALESCED)
 @pytest.mark.parametrize("dt", [O.DT_INT8, O.DT_FLOAT16, O.DT_FLOAT32, O.DT_FLOAT64])
 def test_coalesced_plan_packs_chunk_major(n, counts, dt):
-    """Every (buffer, Split chunk c) segment lands once, 16-B aligned, inside
+    """Every (buffer, Split chunk c) segment lands once, congruent mod 16 with
+    its offset in the buffer, inside
     packed chunk c's range; chunk ranges are disjoint, 256-B aligned and in
     order; copy units cover each segment contiguously."""
     esz = np.dtype(O.NP_DTYPE[dt]).itemsize
@@ -143,7 +144,7 @@ def test_coalesced_plan_packs_chunk_major(n, counts, dt):
                 assert lo <= boff and boff + l <= hi           # inside buffer b's chunk c
                 assert off[c] <= packed and packed + l <= off[c] + ln[c]  # inside packed chunk c
                 if boff == lo:
-                    assert packed % 16 == 0                    # segment start aligned
+                    assert packed % 16 == boff % 16            # congruent with its bytes in a 16-B aligned buffer
                 pos += 1
         assert sum(s[2] for s in segs) == cnt * esz           # every byte exactly once
     # image ranges of distinct units never overlap
