@@ -59,6 +59,9 @@ def parse():
                     help="N>1: also time cfg4 (fp16) and cfg5 (1024 buckets) this many steps after the timed region")
     ap.add_argument("--ring-steps", type=int, default=5,
                     help="N>1: also time the reference's ring schedule this many steps after the timed region")
+    ap.add_argument("--extras-budget-s", type=float, default=200.0,
+                    help="N>1: wall-clock budget (s) of everything after the timed region, agreed across ranks; "
+                         "extras that do not fit are skipped and listed in extras_skipped")
     ap.add_argument("--autotune-reps", type=int, default=3,
                     help="N>1: before the warm-up, RdcCommAutotune times the launch shapes (role split, grid, "
                          "tile) for this buffer size on this node and keeps the fastest (0 = library defaults)")
@@ -155,7 +158,7 @@ def time_ring(lib, comm, buf, count, dt_enum, sp, dist, torch, steps):
     return timed_ms(one, comm, sp, dist, torch, steps)
 
 
-def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, autotune_reps=0):
+def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, autotune_reps=0, budget=None):
     """The other BASELINE.json configs on the same communicator, after the
     timed region (informational): cfg4 = fp16 allreduce of a buffer of S
     bytes, cfg5 = 1024 buckets of S/1024 bytes fp32 in one coalesced call,
@@ -217,6 +220,9 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
     for nb in (4 << 10, 64 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, big):
         if nb > big:
             continue
+        if budget is not None and budget.left() < 8:
+            out.setdefault("skipped", []).append("sizes_fp32[%d]" % nb)
+            continue
         # small calls: enough of them that the closing device sync + barrier
         # (~1 ms with gloo) is noise (50 calls made it 20 us of a 4 KiB call)
         ns = max(steps, 2000 if nb <= (64 << 10) else 400 if nb <= (1 << 20) else 50 if nb <= (16 << 20) else 0)
@@ -240,74 +246,207 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
     return out
 
 
-def parity_checks(lib, comm, S, world, rank, sp, dist, torch, out):
-    """Bit-exact checks at the bench's own shapes (after all timing): fresh
-    synthetic inputs, ONE collective, then windows of every rank's result -
-    each chunk's head and tail, i.e. every Split boundary, where a misplanned
-    tile or a stale hand-off shows first - compared with the oracle's ring
-    order computed on the window alone.  cfg3 (mesh and the reference ring
-    schedule), cfg4 (fp16) and cfg5 (1024 buckets, three whole buckets).
-    Every rank checks its own result; the line reports the AND over ranks."""
+class Budget(object):
+    """Wall-clock budget of the informational extras after the timed region,
+    agreed across ranks: left() is the same number on every rank (the
+    slowest rank's elapsed time, MAX over the CPU process group), so every
+    rank takes the same skip decision and no rank waits in a collective its
+    peers skipped."""
+
+    def __init__(self, seconds, dist, torch, world):
+        self.limit, self.dist, self.torch, self.world = float(seconds), dist, torch, world
+        self.t0 = time.perf_counter()
+
+    def elapsed(self):
+        el = time.perf_counter() - self.t0
+        if self.world > 1:
+            t = self.torch.tensor([el], dtype=self.torch.float64)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            el = float(t[0])
+        return el
+
+    def left(self):
+        return self.limit - self.elapsed()
+
+
+def parity_checks(lib, comm, S, world, rank, sp, dist, torch, out, budget=None):
+    """Bit-exact checks at the bench's own shapes (after all timing), each on
+    fresh synthetic inputs, every key its own boolean (AND over ranks):
+
+    * cfg3_mesh / cfg3_ring / cfg4_fp16: ONE allreduce of the whole S-byte
+      buffer.  Every rank hashes its WHOLE result (sha256) and the ranks
+      compare digests; rank r compares Split chunk r of its result, every
+      element, with the oracle's ring order.  Identical digests + every chunk
+      verified on some rank = every byte of every rank's buffer verified:
+      every tile of every chunk, i.e. every hand-off the schedule made.
+    * cfg5_buckets: 1024 buckets in one coalesced call; digests over all
+      buckets compared across ranks, rank r verifies buckets b = r mod n
+      whole (so every bucket, every chunk boundary).
+    * oneshot_512KiB: four back-to-back one-shot launches (no host sync in
+      between: the slot halves are reused while peers may still read), every
+      result whole on every rank.
+    * service_host_4KiB: eight synchronous 4 KiB fp32 HOST-buffer allreduces
+      through RdcAllreduce (the small-allreduce service's LL-word exchange
+      where it runs, the launch path otherwise), every result whole.
+    * tree_order: a 64 KiB + 12 B fp32 buffer in the reference's tree order
+      (algo 4 = what rdc_reduce_ring_mincount selects), against the oracle's
+      restated tree.
+    * broadcast_nonzero_root: 8 MiB + 12 B from root n-1 (forwarded through
+      the other ranks at n >= 3), every byte on every rank.
+    * allgather_varsize: per-rank sizes 1 MiB + c x 4100 B, every buffer on
+      every rank.
+    """
     from rdc_amd._lib import check_call
-    import numpy as np
-    import rdc_amd
+    import hashlib
     from oracle import oracle as O
+
+    t_start = time.perf_counter()
+    wall = {}
 
     def agree(ok):
         f = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
         dist.all_reduce(f, op=dist.ReduceOp.MAX)
         return float(f[0]) == 0.0
 
-    def windows(count):
-        W = min(count, 1 << 14)
-        starts = {0, max(0, count - W)}
-        for b, _ in O.split(count, world)[1:]:
-            starts.add(max(0, b - W // 2))
-        return sorted((st, min(W, count - st)) for st in starts)
+    def identical(host_bytes):
+        """Every rank holds the same bytes (sha256 compared over gloo)."""
+        d = hashlib.sha256(host_bytes).hexdigest()
+        ds = [None] * world
+        dist.all_gather_object(ds, d)
+        return all(x == d for x in ds)
 
-    def check_buf(t, count, dt, seed):
-        ok = True
-        for st, m in windows(count):
-            got = t[st:st + m].cpu().contiguous().view(torch.uint8).numpy().tobytes()
-            ok = ok and got == O.expected_window(count, st, m, world, dt, 2, seed).tobytes()
-        return ok
+    def host_u8(t):
+        return t.cpu().contiguous().view(torch.uint8).numpy()
+
+    def verify_range(u8, total, lo, hi, dt, seed, esz, block=1 << 20):
+        """Elements [lo, hi) of a `total`-element result vs the oracle's ring
+        order, block by block (the oracle computes each window alone)."""
+        for st in range(lo, hi, block):
+            m = min(block, hi - st)
+            want = O.expected_window(total, st, m, world, dt, 2, seed)
+            if u8[st * esz:(st + m) * esz].tobytes() != want.tobytes():
+                return False
+        return True
+
+    def fill(t, count, dt, seed, r):
+        check_call(lib.RdcFill(ctypes.c_void_p(t.data_ptr()), count, dt, seed, r, sp))
+
+    def should_run(name, need_s):
+        if budget is not None and budget.left() < need_s:
+            out.setdefault("skipped", []).append(name)
+            return False
+        return True
 
     for name, dt, algo, tdt in (("cfg3_mesh", 6, 2, torch.float32), ("cfg3_ring", 6, 1, torch.float32),
                                 ("cfg4_fp16", 10, 0, torch.float16)):
+        if not should_run(name, 20):
+            continue
+        t0 = time.perf_counter()
         esz = 4 if dt == 6 else 2
         count = S // esz
         t = torch.empty(count, dtype=tdt, device="cuda")
         seed = 0x5EED1000 + dt * 16 + algo
-        check_call(lib.RdcFill(ctypes.c_void_p(t.data_ptr()), count, dt, seed, rank, sp))
+        fill(t, count, dt, seed, rank)
         check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(t.data_ptr()), count, dt, 2, algo, sp))
         sync_check(comm, sp, dist, torch)
-        out[name] = agree(check_buf(t, count, dt, seed))
+        u8 = host_u8(t)
         del t
-    K = 1024
-    per = S // 4 // K
-    bks = [torch.empty(per, dtype=torch.float32, device="cuda") for _ in range(K)]
-    for b, t in enumerate(bks):
-        check_call(lib.RdcFill(ctypes.c_void_p(t.data_ptr()), per, 6, 0x5EED2000 + b, rank, sp))
-    ptrs = (ctypes.c_void_p * K)(*[t.data_ptr() for t in bks])
-    cnts = (ctypes.c_size_t * K)(*([per] * K))
-    check_call(lib.RdcCommAllreduceCoalesced(comm.handle, ptrs, cnts, K, 6, 2, 0, sp))
-    sync_check(comm, sp, dist, torch)
-    ok = True
-    for b in (0, K // 2 + 1, K - 1):
-        got = bks[b].cpu().numpy().tobytes()
-        ok = ok and got == O.expected_window(per, 0, per, world, 6, 2, 0x5EED2000 + b).tobytes()
-    out["cfg5_buckets"] = agree(ok)
-    del bks
-    out["method"] = ("one collective on fresh synthetic inputs; windows of 16 Ki elements at both ends of every "
-                     "Split chunk (cfg3/cfg4) and three whole buckets (cfg5) compared bit-exact with the oracle's "
-                     "ring order on every rank")
+        lo, hi = O.split(count, world)[rank]
+        ok = verify_range(u8, count, lo, hi, dt, seed, esz)
+        out[name] = agree(ok) and identical(u8.data)
+        del u8
+        wall[name] = round(time.perf_counter() - t0, 2)
+    if should_run("cfg5_buckets", 20):
+        t0 = time.perf_counter()
+        K = 1024
+        per = S // 4 // K
+        bks = [torch.empty(per, dtype=torch.float32, device="cuda") for _ in range(K)]
+        for b, t in enumerate(bks):
+            fill(t, per, 6, 0x5EED2000 + b, rank)
+        ptrs = (ctypes.c_void_p * K)(*[t.data_ptr() for t in bks])
+        cnts = (ctypes.c_size_t * K)(*([per] * K))
+        check_call(lib.RdcCommAllreduceCoalesced(comm.handle, ptrs, cnts, K, 6, 2, 0, sp))
+        sync_check(comm, sp, dist, torch)
+        u8 = host_u8(torch.cat(bks))
+        del bks
+        ok = all(verify_range(u8[b * per * 4:(b + 1) * per * 4], per, 0, per, 6, 0x5EED2000 + b, 4)
+                 for b in range(rank, K, world))
+        out["cfg5_buckets"] = agree(ok) and identical(u8.data)
+        del u8
+        wall["cfg5_buckets"] = round(time.perf_counter() - t0, 2)
+    if should_run("oneshot_512KiB", 5):
+        t0 = time.perf_counter()
+        count = (512 << 10) // 4
+        ts = [torch.empty(count, dtype=torch.float32, device="cuda") for _ in range(4)]
+        for k, t in enumerate(ts):
+            fill(t, count, 6, 0x5EED4000 + k, rank)
+        for t in ts:  # back to back on one stream: consecutive launches alternate slot halves
+            check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(t.data_ptr()), count, 6, 2, 3, sp))
+        sync_check(comm, sp, dist, torch)
+        ok = all(host_u8(t).tobytes() == O.expected_window(count, 0, count, world, 6, 2, 0x5EED4000 + k).tobytes()
+                 for k, t in enumerate(ts))
+        out["oneshot_512KiB"] = agree(ok)
+        wall["oneshot_512KiB"] = round(time.perf_counter() - t0, 2)
+    if should_run("service_host_4KiB", 5):
+        t0 = time.perf_counter()
+        ok = True
+        g = torch.empty(1024, dtype=torch.float32, device="cuda")
+        for k in range(8):
+            fill(g, 1024, 6, 0x5EED5000 + k, rank)  # the device generator: same values as the oracle's
+            torch.cuda.synchronize()
+            a = g.cpu().numpy().copy()             # pageable host memory, as rdc/core.py passes it
+            check_call(lib.RdcAllreduce(ctypes.c_void_p(a.ctypes.data), 1024, 6, 2, None, None))
+            ok = ok and a.tobytes() == O.expected_window(1024, 0, 1024, world, 6, 2, 0x5EED5000 + k).tobytes()
+        out["service_host_4KiB"] = agree(ok)
+        wall["service_host_4KiB"] = round(time.perf_counter() - t0, 2)
+    if should_run("tree_order", 5):
+        t0 = time.perf_counter()
+        count = (64 << 10) // 4 + 3
+        t = torch.empty(count, dtype=torch.float32, device="cuda")
+        fill(t, count, 6, 0x5EED6000, rank)
+        check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(t.data_ptr()), count, 6, 2, 4, sp))
+        sync_check(comm, sp, dist, torch)
+        want = O.expected_tree([O.fill(count, 6, 0x5EED6000, r) for r in range(world)], 6, 2)
+        out["tree_order"] = agree(host_u8(t).tobytes() == want.tobytes())
+        wall["tree_order"] = round(time.perf_counter() - t0, 2)
+    if should_run("broadcast_nonzero_root", 5):
+        t0 = time.perf_counter()
+        root = world - 1
+        count = (8 << 20) // 4 + 3
+        t = torch.empty(count, dtype=torch.float32, device="cuda")
+        fill(t, count, 6, 0x5EED7000 if rank == root else 0x5EED7001, rank)
+        check_call(lib.RdcCommBroadcast(comm.handle, ctypes.c_void_p(t.data_ptr()), count * 4, root, sp))
+        sync_check(comm, sp, dist, torch)
+        out["broadcast_nonzero_root"] = agree(host_u8(t).tobytes() == O.fill(count, 6, 0x5EED7000, root).tobytes())
+        wall["broadcast_nonzero_root"] = round(time.perf_counter() - t0, 2)
+    if should_run("allgather_varsize", 5):
+        t0 = time.perf_counter()
+        counts = [(1 << 18) + 1025 * c for c in range(world)]
+        bufs = [torch.zeros(c, dtype=torch.float32, device="cuda") for c in counts]
+        fill(bufs[rank], counts[rank], 6, 0x5EED8000, rank)
+        ptrs = (ctypes.c_void_p * world)(*[b.data_ptr() for b in bufs])
+        sizes = (ctypes.c_size_t * world)(*[4 * c for c in counts])
+        check_call(lib.RdcCommAllgather(comm.handle, ptrs, sizes, sp))
+        sync_check(comm, sp, dist, torch)
+        ok = all(host_u8(b).tobytes() == O.fill(counts[c], 6, 0x5EED8000, c).tobytes() for c, b in enumerate(bufs))
+        out["allgather_varsize"] = agree(ok)
+        wall["allgather_varsize"] = round(time.perf_counter() - t0, 2)
+    out["wall_s"] = wall
+    out["method"] = ("fresh synthetic inputs per check.  cfg3/cfg4: one allreduce of the whole buffer; rank r "
+                     "compares every element of Split chunk r with the oracle's ring order and the ranks compare "
+                     "sha256 digests of their whole results (identical digests + every chunk verified on some "
+                     "rank = every byte of every rank verified).  cfg5: the same over 1024 buckets (rank r "
+                     "verifies buckets r mod n whole).  oneshot / service / tree / broadcast / allgather: every "
+                     "result whole on every rank.  Each key is the AND over ranks.")
+    out["seconds"] = round(time.perf_counter() - t_start, 2)
     return out
 
 
-def rccl_compare(S, world, rank, local, dist, torch, steps):
+def rccl_compare(S, world, rank, local, dist, torch, steps, limit_s=150.0):
     """The same allreduce through RCCL (torch.distributed nccl backend), one
     child process per rank (tools/rccl_allreduce.py), after every rdc
-    measurement and under a time limit: informational, never costs the line.
+    measurement and under a time limit inside the extras budget:
+    informational, never costs the line.
     Skipped when ranks share a GPU (RCCL needs one rank per device)."""
     import subprocess
     if torch.cuda.device_count() < world:
@@ -319,14 +458,14 @@ def rccl_compare(S, world, rank, local, dist, torch, steps):
            str(port), str(S), str(steps)]
     res = {"error": "no result"}
     try:
-        p = subprocess.run(cmd, capture_output=True, text=True, timeout=150)
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=max(10.0, limit_s))
         lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
         if lines:
             res = json.loads(lines[-1])
         elif p.returncode != 0:
             res = {"error": "rc=%d: %s" % (p.returncode, p.stderr[-300:])}
     except subprocess.TimeoutExpired:
-        res = {"error": "timed out after 150 s"}
+        res = {"error": "timed out after %.0f s" % max(10.0, limit_s)}
     except Exception as e:  # noqa: BLE001 - informational only
         res = {"error": str(e)}
     dist.barrier()
@@ -551,11 +690,25 @@ def main():
     # process group (sync_check), so all ranks leave a failed extra together;
     # once one has failed the communicator is unusable, and the remaining
     # extras that need it are skipped.  Partial results are kept.
+    #
+    # The extras share one wall-clock budget (--extras-budget-s), agreed
+    # across ranks before each one: an extra that needs more than what is
+    # left is skipped (`extras_skipped`), so the line is printed well inside
+    # the driver's limit however slow the node is.  Each extra's wall
+    # seconds are in `extras_wall_s`.  Order = value of the evidence: the
+    # parity checks (every hand-off verified over the real links) first.
     extras_error = {}
+    extras_skipped = []
+    extras_wall = {}
+    budget = Budget(args.extras_budget_s, dist, torch, world)
 
-    def guarded(name, fn, needs_comm=True, partial=None):
+    def guarded(name, fn, needs_comm=True, partial=None, need_s=10.0):
         if needs_comm and extras_error:
             return None
+        if budget.left() < need_s:
+            extras_skipped.append(name)
+            return None
+        t_x = time.perf_counter()
         res, failed = None, 0.0
         try:
             res = fn()
@@ -567,6 +720,7 @@ def main():
             dist.all_reduce(f, op=dist.ReduceOp.MAX)
             if float(f[0]) > 0 and name not in extras_error:
                 extras_error[name] = "failed on another rank"
+        extras_wall[name] = round(time.perf_counter() - t_x, 2)
         if name in extras_error:
             return partial if partial else None
         return res
@@ -575,29 +729,40 @@ def main():
     f32 = args.dtype == "float32"
     roles = ring_cmp = extra = rccl = tcp = checks = None
     if multi:
-        roles = guarded("role_timeline", lambda: trace_roles(_LIB, comm, buf, count, dt_enum, sp, dist, torch))
-    if multi and args.ring_steps > 0:
-        # the reference's own schedule on the same buffer (same bits, one link
-        # direction per GPU).  Grids are clamped to what stays resident next
-        # to the ranks sharing a GPU, so this runs in rehearsals too.
-        ring_cmp = guarded("ring_schedule", lambda: time_ring(_LIB, comm, buf, count, dt_enum, sp, dist, torch,
-                                                              args.ring_steps))
+        roles = guarded("role_timeline", lambda: trace_roles(_LIB, comm, buf, count, dt_enum, sp, dist, torch),
+                        need_s=2)
     if multi:
         del buf  # room for the other configs' buffers
         torch.cuda.empty_cache()
+    if multi and f32 and not args.no_check:
+        part_c = {}
+        checks = guarded("parity_checks", lambda: parity_checks(_LIB, comm, S, world, rank, sp, dist, torch, part_c,
+                                                                budget),
+                         partial=part_c, need_s=30)
+    if multi and args.ring_steps > 0:
+        # the reference's own schedule on a buffer of the same size (same
+        # bits, one link direction per GPU).  Grids are clamped to what stays
+        # resident next to the ranks sharing a GPU, so this runs in rehearsals.
+        def ring_leg():
+            rbuf = torch.empty(count, dtype=tdtype, device="cuda")
+            rdc_amd.fill_(rbuf, 0x5EED0000, rank)
+            ms = time_ring(_LIB, comm, rbuf, count, dt_enum, sp, dist, torch, args.ring_steps)
+            del rbuf
+            torch.cuda.empty_cache()
+            return ms
+        ring_cmp = guarded("ring_schedule", ring_leg, need_s=5)
     if multi and f32 and args.extra_steps > 0:
         part = {}
         extra = guarded("extra_configs", lambda: time_extra_configs(_LIB, comm, S, world, rank, sp, dist, torch,
-                                                                    args.extra_steps, part, args.autotune_reps),
-                        partial=part)
-    if multi and f32 and not args.no_check:
-        part_c = {}
-        checks = guarded("parity_checks", lambda: parity_checks(_LIB, comm, S, world, rank, sp, dist, torch, part_c),
-                         partial=part_c)
+                                                                    args.extra_steps, part, args.autotune_reps,
+                                                                    budget),
+                        partial=part, need_s=20)
     if multi and f32 and args.rccl_steps > 0:
-        rccl = guarded("rccl_comparison", lambda: rccl_compare(S, world, rank, local, dist, torch, args.rccl_steps))
+        rccl = guarded("rccl_comparison", lambda: rccl_compare(S, world, rank, local, dist, torch, args.rccl_steps,
+                                                               limit_s=min(150.0, budget.left() - 15)),
+                       need_s=45)
     if world > 1 and args.cpu_seconds > 0:
-        tcp = guarded("cpu_tcp_ring", lambda: cpu_tcp_ring(S, world, rank, dist), needs_comm=False)
+        tcp = guarded("cpu_tcp_ring", lambda: cpu_tcp_ring(S, world, rank, dist), needs_comm=False, need_s=20)
 
     # spot check (outside the timed region): N=1 reduce result vs oracle on a slice
     check = None
@@ -713,6 +878,10 @@ def main():
         out["oracle_check"] = check
     if extras_error:
         out["extras_error"] = extras_error
+    if world > 1:
+        out["extras_budget_s"] = args.extras_budget_s
+        out["extras_wall_s"] = extras_wall
+        out["extras_skipped"] = extras_skipped
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

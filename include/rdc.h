@@ -250,6 +250,10 @@ inline void Check(int rc, const char* what) {
         abort();
     }
 }
+inline void Fail(const char* what, const std::string& why) {
+    fprintf(stderr, "rdc: %s failed: %s\n", what, why.c_str());
+    abort();
+}
 }  // namespace detail
 
 /*! \brief completion of an ISend / IRecv (include/core/work_request.h:240-270).
@@ -390,13 +394,6 @@ inline void ICommunicator::Allreduce(Buffer buf, ReduceFunction reducer) {
     const uint64_t S = buf.size_in_bytes();
     if (n <= 1 || S == 0) return;  // communicator_base.h:133-138
     const uint64_t isz = buf.item_size(), count = buf.Count();
-    // every rank's input on every rank (host copies), moved over the device path
-    std::vector<std::vector<char>> in((size_t)n, std::vector<char>((size_t)S));
-    detail::Check(RdcMemcpy(in[(size_t)r].data(), buf.addr(), S), "Allreduce input copy");
-    std::vector<void*> ptrs((size_t)n);
-    std::vector<size_t> sizes((size_t)n, (size_t)S);
-    for (int q = 0; q < n; ++q) ptrs[(size_t)q] = in[(size_t)q].data();
-    Allgather(ptrs.data(), sizes.data());
     auto view = [&](std::vector<char>& v, uint64_t off, uint64_t len) {
         Buffer b(v.data() + off, len, off, off + len);
         b.set_item_size(isz);
@@ -406,7 +403,14 @@ inline void ICommunicator::Allreduce(Buffer buf, ReduceFunction reducer) {
     detail::Check(RdcCommGetParam(handle_, "rdc_reduce_ring_mincount", &mincount), "Allreduce");
     if (S <= mincount) {
         // TryAllreduceTree (communicator_collective.cc:14-43,71-78): the fold
-        // to rank 0 in the tree's order, then everyone gets rank 0's bytes
+        // to rank 0 in the tree's order over whole (small: <= the threshold)
+        // buffers, then everyone gets rank 0's bytes
+        std::vector<std::vector<char>> in((size_t)n, std::vector<char>((size_t)S));
+        detail::Check(RdcMemcpy(in[(size_t)r].data(), buf.addr(), S), "Allreduce input copy");
+        std::vector<void*> ptrs((size_t)n);
+        std::vector<size_t> sizes((size_t)n, (size_t)S);
+        for (int q = 0; q < n; ++q) ptrs[(size_t)q] = in[(size_t)q].data();
+        Allgather(ptrs.data(), sizes.data());
         int dst[16], src[16];
         const int k = RdcPlanTree(n, dst, src);
         for (int i = 0; i < k; ++i) reducer(view(in[(size_t)src[i]], 0, S), view(in[(size_t)dst[i]], 0, S));
@@ -415,7 +419,11 @@ inline void ICommunicator::Allreduce(Buffer buf, ReduceFunction reducer) {
     }
     // TryReduceScatterRing (:115-182): rank r ends with chunk r of
     // utils::Split(0, count, n) = x[r] (+) (x[r+1] (+) ... (+) x[r-1]), each
-    // step reducer(src = received partial, dst = this rank's chunk)
+    // step reducer(src = received partial, dst = this rank's chunk).  Only
+    // chunk r of every rank's input is needed for that: rank q sends its
+    // chunk c straight to rank c (point-to-point over the device path, all
+    // pairs at once), (n-1)/n x S in and out per rank — the reference ring's
+    // reduce-scatter traffic — and the host holds S/n per peer, not S.
     std::vector<uint64_t> off((size_t)n), len((size_t)n);
     const uint64_t kq = count / (uint64_t)n, km = count % (uint64_t)n;
     for (int c = 0; c < n; ++c) {
@@ -425,14 +433,39 @@ inline void ICommunicator::Allreduce(Buffer buf, ReduceFunction reducer) {
         len[(size_t)c] = (e - b) * isz;
     }
     const uint64_t o = off[(size_t)r], l = len[(size_t)r];
-    std::vector<char> partial(in[(size_t)((r - 1 + n) % n)].begin() + (ptrdiff_t)o,
-                              in[(size_t)((r - 1 + n) % n)].begin() + (ptrdiff_t)(o + l));
-    for (int j = 2; j <= n; ++j) {
-        std::vector<char>& x = in[(size_t)((r - j + n) % n)];  // this copy is no longer needed whole
-        reducer(view(partial, 0, l), view(x, o, l));
-        partial.assign(x.begin() + (ptrdiff_t)o, x.begin() + (ptrdiff_t)(o + l));
+    std::vector<std::vector<char>> x((size_t)n);  // x[q] = rank q's chunk r
+    if (l > 0) {
+        for (int q = 0; q < n; ++q) x[(size_t)q].resize((size_t)l);
+        detail::Check(RdcMemcpy(x[(size_t)r].data(), static_cast<char*>(buf.addr()) + o, l), "Allreduce input copy");
     }
-    detail::Check(RdcMemcpy(static_cast<char*>(buf.addr()) + o, partial.data(), l), "Allreduce result copy");
+    std::vector<WorkCompletion*> pending;
+    for (int k = 1; k < n; ++k) {
+        const int q = (r + k) % n;  // send chunk q to rank q; receive chunk r from rank (r - k)
+        const int p = (r - k + n) % n;
+        if (len[(size_t)q] > 0) pending.push_back(ISend(static_cast<char*>(buf.addr()) + off[(size_t)q], len[(size_t)q], q));
+        if (l > 0) pending.push_back(IRecv(x[(size_t)p].data(), l, p));
+    }
+    bool ok = true;
+    std::string err;
+    for (WorkCompletion* w : pending) {
+        if (!w->Wait() && ok) {
+            ok = false;
+            err = w->Error();
+        }
+        delete w;
+    }
+    if (!ok) detail::Fail("Allreduce chunk exchange", err);
+    if (l > 0) {
+        std::vector<char> partial(x[(size_t)((r - 1 + n) % n)]);
+        for (int j = 2; j <= n; ++j) {
+            std::vector<char>& d = x[(size_t)((r - j + n) % n)];
+            Buffer dv(d.data(), l, o, o + l);  // the same Slice(o, o + l) view the full-buffer form passed
+            dv.set_item_size(isz);
+            reducer(view(partial, 0, l), dv);
+            partial.swap(d);  // d (now the new partial) is not needed as an input again
+        }
+        detail::Check(RdcMemcpy(static_cast<char*>(buf.addr()) + o, partial.data(), l), "Allreduce result copy");
+    }
     // TryAllgatherRing (:79-114): chunk c from rank c, in place
     std::vector<void*> cb((size_t)n);
     std::vector<size_t> cs((size_t)n);

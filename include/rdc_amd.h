@@ -98,7 +98,7 @@ int RdcAllreduceCoalesced(void** bufs, const size_t* counts, int nbuf, int dtype
 int RdcAllreduceCoalescedOn(void* comm, void** bufs, const size_t* counts, int nbuf, int dtype, int op);
 
 /* rdc::NewCommunicator / GetCommunicator (include/rdc.h:62-71;
- * rdc/comm.py:398-427 calls RdcNewCommunicator(byref(handle), name)).
+ * rdc/comm.py:90-93,106-109 call RdcNewCommunicator(byref(handle), name)).
  * NewCommunicator is collective over all ranks.  Named communicators over the
  * same ranks share one scratch channel (one pool of uncached HBM per rank):
  * every rank must then issue the collectives of ALL those communicators in
@@ -216,9 +216,12 @@ int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t t
  * `bytes` of `dtype` on this node — mesh: role split, then grid, then
  * tiles per reduce block; ring: grid, then tiles per block (a granularity, so
  * the chosen tiles scale with later buffers' sizes) — `reps` Sum allreduces each on a scratch
- * buffer; agree on the per-candidate times with a MAX allreduce over `comm`
- * (identical on every rank, so every rank keeps the same winner) and keep the
- * fastest schedule and shape for allreduces of that size class ([2^k,
+ * buffer, in 3 rounds per candidate taken round-robin over each stage; agree
+ * on the per-round times with a MAX allreduce over `comm` (identical on every
+ * rank, so every rank keeps the same winner); a candidate's time is the median
+ * of its rounds, and each stage keeps its first candidate (stage 0: the
+ * automatic rule's schedule; later: the previous winner) unless another is
+ * faster by more than 3 %; keep the chosen schedule and shape for allreduces of that size class ([2^k,
  * 2^(k+1)) bytes; other sizes keep the automatic rule and the configured
  * shape, RdcCommTune clears every autotuned one, and nothing is tuned while
  * RDC_ALGO forces a schedule; with RDC_TUNE_FILE set, rank 0 appends the
@@ -232,7 +235,8 @@ typedef struct {
     int algo;                           /* RDC_ALGO_RING (1), RDC_ALGO_MESH (2), RDC_ALGO_ONESHOT (3) */
     int mesh_s16, mesh_r16, max_blocks; /* max_blocks 0 = automatic grid */
     int tiles_per_block;                /* 0 = default (mesh 2 per reduce block, ring 1) */
-    double ms;                          /* per allreduce, max over ranks */
+    double ms;                          /* per allreduce: median over rounds of the slowest rank's time */
+    double ms_min, ms_max;              /* spread of that time over the rounds */
 } RdcTuneCand;
 int RdcCommAutotune(void* comm, size_t bytes, int dtype, int reps, void* stream, RdcTuneCand* cand, int max_cand,
                     int* ncand, int* best);

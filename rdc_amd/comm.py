@@ -1,5 +1,5 @@
 """Communicator handles — rdc/comm.py's ``new_comm`` / ``get_comm`` / ``Comm``
-(rdc/comm.py:351-427) over the MI355X device path, plus single-process
+(rdc/comm.py:36-112) over the MI355X device path, plus single-process
 multi-rank groups (``init_group``) for driving several GPUs from one process.
 """
 import ctypes
@@ -16,7 +16,8 @@ class TuneCand(ctypes.Structure):
     """RdcTuneCand (include/rdc_amd.h): one launch shape timed by RdcCommAutotune."""
     _fields_ = [("algo", ctypes.c_int), ("mesh_s16", ctypes.c_int), ("mesh_r16", ctypes.c_int),
                 ("max_blocks", ctypes.c_int),
-                ("tiles_per_block", ctypes.c_int), ("ms", ctypes.c_double)]
+                ("tiles_per_block", ctypes.c_int), ("ms", ctypes.c_double), ("ms_min", ctypes.c_double),
+                ("ms_max", ctypes.c_double)]
 
 
 class WorkComp(object):
@@ -80,7 +81,14 @@ class Comm(object):
         return _LIB.RdcCommAllocKind(self.handle)
 
     def allreduce(self, tensor, op, algo="auto", stream=None):
-        """In-place allreduce of a contiguous ROCm tensor; returns it."""
+        """In-place allreduce of a contiguous ROCm tensor on this
+        communicator; returns it.  A numpy array takes rdc.allreduce's host
+        path and copy rule (rdc/core.py:196-217) on this communicator
+        (rdc::Allreduce<OP>(buf, count, comm_name), include/api.h:62-64) and
+        returns the reduced flat array."""
+        if not _is_tensor(tensor):
+            from .core import host_allreduce
+            return host_allreduce(tensor, op, comm=self.handle)
         _dev._check_tensor(tensor)
         s = stream if stream is not None else _dev.current_stream_ptr(tensor.device)
         check_call(_LIB.RdcCommAllreduceEx(self.handle, ctypes.c_void_p(tensor.data_ptr()), tensor.numel(),
@@ -209,7 +217,8 @@ class Comm(object):
         def row(c):
             return {"schedule": {1: "ring", 2: "mesh", 3: "oneshot"}.get(c.algo, c.algo),
                     "split": [c.mesh_s16, c.mesh_r16], "grid": c.max_blocks or "auto",
-                    "tiles_per_block": c.tiles_per_block or "auto", "ms": round(c.ms, 4)}
+                    "tiles_per_block": c.tiles_per_block or "auto", "ms": round(c.ms, 4),
+                    "spread_ms": [round(c.ms_min, 4), round(c.ms_max, 4)]}
         rows = [row(cand[k]) for k in range(nc.value)]
         return {"chosen": rows[best.value] if best.value >= 0 else None, "candidates": rows}
 

@@ -134,6 +134,13 @@ def allreduce(data, op, prepare_fun=None):
         if prepare_fun is not None:
             prepare_fun(data)
         return _comm.get_comm("main").allreduce(data, op)
+    return host_allreduce(data, op, prepare_fun)
+
+
+def host_allreduce(data, op, prepare_fun=None, comm=None):
+    """rdc/core.py:172-217 on a host ndarray: RdcAllreduce on "main", or
+    RdcAllreduceOn on the communicator handle ``comm``."""
+    op = int(Op(op) if not isinstance(op, Op) else op)
     if not isinstance(data, np.ndarray):
         raise TypeError("allreduce only takes in numpy.ndarray or torch.Tensor")
     buf = data.ravel()
@@ -143,6 +150,12 @@ def allreduce(data, op, prepare_fun=None):
         raise TypeError("data type %s not supported" % str(buf.dtype))
     if not buf.flags.c_contiguous:
         buf = np.ascontiguousarray(buf)
+    if comm is not None:
+        if prepare_fun is not None:
+            prepare_fun(data)
+        check_call(_LIB.RdcAllreduceOn(comm, buf.ctypes.data_as(ctypes.c_void_p), buf.size,
+                                       DTYPE_ENUM__[buf.dtype], op))
+        return buf
     cb = None
     if prepare_fun is not None:
         cb = _PREPARE_T(lambda _arg: prepare_fun(data))

@@ -573,7 +573,8 @@ int RdcCommAutotune(void* comm, size_t bytes, int dtype, int reps, void* stream,
         int b = -1;
         const int k = as_comm(comm)->Autotune(bytes, dtype, reps, static_cast<hipStream_t>(stream), c.data(),
                                               max_cand, &b);
-        for (int i = 0; i < k; ++i) cand[i] = RdcTuneCand{c[i].algo, c[i].s16, c[i].r16, c[i].grid, c[i].tpb, c[i].ms};
+        for (int i = 0; i < k; ++i) cand[i] = RdcTuneCand{c[i].algo, c[i].s16, c[i].r16, c[i].grid, c[i].tpb, c[i].ms, c[i].ms_min,
+                                                     c[i].ms_max};
         *ncand = k;
         *best = b;
     });

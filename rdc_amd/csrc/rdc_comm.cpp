@@ -348,6 +348,9 @@ void Communicator::Attach(const std::shared_ptr<Channel>& ch) {
     {
         std::lock_guard<std::mutex> lk(ch->mu);
         ++ch->users;
+        // communicators attach to a channel in creation order, which is
+        // collective: the k-th user's tag is k on every rank (kSeqBits)
+        tag_ = ch->attached++ & 0xFFu;
     }
     Alias();
 }
@@ -712,6 +715,7 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     a->done_ctr = err_ + 16;
     a->launch_ctr = err_ + 32;
     a->launch_kind = err_ + 48;
+    a->tag = tag_;
     a->half_bytes = OneshotHalfBytes(layout());
     a->timeout_ticks = (uint64_t)(cfg_.timeout_s * (double)wall_khz_ * 1000.0);
     a->uc = (alloc_kind_ == 0 && !strict_fences()) ? 1 : 0;
@@ -1215,7 +1219,9 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     };
     try {
         hip_check(hipMallocAsync(&buf, count * esz, stream), "autotune buffer");
-        hip_check(hipMallocAsync(reinterpret_cast<void**>(&dms), sizeof(double) * (size_t)max_cand, stream),
+        // per-round times of one stage, agreed across ranks
+        constexpr int kStageMax = 16;
+        hip_check(hipMallocAsync(reinterpret_cast<void**>(&dms), sizeof(double) * kStageMax * kTuneRounds, stream),
                   "autotune times");
         hip_check(hipMemsetAsync(buf, 0, count * esz, stream), "autotune memset");
         hip_check(hipEventCreate(&e0), "event");
@@ -1231,82 +1237,95 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
             tuned_[cls * 8 + c.algo] = s;
             tuned_algo_[cls] = c.algo;
         };
-        auto time_one = [&](int algo, int s16, int r16, int grid, int tpb) {
-            if (nc >= max_cand) return;
-            const TuneCand c{algo, s16, r16, grid, tpb, 0.0};
+        auto add = [&](int algo, int s16, int r16, int grid, int tpb) {
+            if (nc < max_cand) cand[nc++] = TuneCand{algo, s16, r16, grid, tpb, 0.0, 0.0, 0.0};
+        };
+        // one round of one candidate: ms per allreduce on this rank
+        auto measure = [&](const TuneCand& c, bool warm) {
             set_shape(c);
-            Allreduce(buf, count, dtype, RDC_OP_SUM, stream, RDC_ALGO_AUTO);  // warm (and first-use work)
+            if (warm) Allreduce(buf, count, dtype, RDC_OP_SUM, stream, RDC_ALGO_AUTO);  // first-use work
             hip_check(hipEventRecord(e0, stream), "record");
             for (int i = 0; i < reps; ++i) Allreduce(buf, count, dtype, RDC_OP_SUM, stream, RDC_ALGO_AUTO);
             hip_check(hipEventRecord(e1, stream), "record");
             hip_check(hipEventSynchronize(e1), "sync");
             float ms = 0;
             hip_check(hipEventElapsedTime(&ms, e0, e1), "elapsed");
-            cand[nc] = c;
-            cand[nc++].ms = (double)ms / reps;
+            return (double)ms / reps;
         };
-        // the slowest rank's time per candidate, identical on every rank;
-        // returns the stage's winner (lowest index among equal times)
-        auto agree = [&](int lo) {
+        // a stage = candidates [lo, nc), cand[lo] the incumbent.  kTuneRounds
+        // rounds, each timing every candidate once (round-robin: a slow spell
+        // of the node hits the whole stage, not one candidate); the slowest
+        // rank's time per (candidate, round) by a MAX allreduce — identical on
+        // every rank — then each candidate's median over its rounds.  The
+        // incumbent stays unless another median beats it by > kTuneMargin.
+        auto stage = [&](int lo) {
             const int k = nc - lo;
             if (k <= 0) throw std::runtime_error("rdc: autotune ran out of candidate room");
-            double h[64];
-            if (k > 64) throw std::logic_error("rdc: autotune stage too large");
-            for (int i = 0; i < k; ++i) h[i] = cand[lo + i].ms;
-            hip_check(hipMemcpyAsync(dms, h, sizeof(double) * k, hipMemcpyHostToDevice, stream), "H2D");
-            Allreduce(dms, (size_t)k, RDC_DT_FLOAT64, RDC_OP_MAX, stream, RDC_ALGO_AUTO);
-            hip_check(hipMemcpyAsync(h, dms, sizeof(double) * k, hipMemcpyDeviceToHost, stream), "D2H");
+            if (k > kStageMax) throw std::logic_error("rdc: autotune stage too large");
+            double h[kStageMax * kTuneRounds];
+            for (int r = 0; r < kTuneRounds; ++r)
+                for (int i = 0; i < k; ++i) h[i * kTuneRounds + r] = measure(cand[lo + i], r == 0);
+            const size_t m = (size_t)k * kTuneRounds;
+            hip_check(hipMemcpyAsync(dms, h, sizeof(double) * m, hipMemcpyHostToDevice, stream), "H2D");
+            Allreduce(dms, m, RDC_DT_FLOAT64, RDC_OP_MAX, stream, RDC_ALGO_AUTO);
+            hip_check(hipMemcpyAsync(h, dms, sizeof(double) * m, hipMemcpyDeviceToHost, stream), "D2H");
             Check(stream);
-            int w = lo;
+            int fastest = lo;
             for (int i = 0; i < k; ++i) {
-                cand[lo + i].ms = h[i];
-                if (h[i] < cand[w].ms) w = lo + i;
+                double* t = h + (size_t)i * kTuneRounds;
+                std::sort(t, t + kTuneRounds);
+                TuneCand& c = cand[lo + i];
+                c.ms = t[kTuneRounds / 2];
+                c.ms_min = t[0];
+                c.ms_max = t[kTuneRounds - 1];
+                if (c.ms < cand[fastest].ms) fastest = lo + i;
             }
-            return w;
-        };
-        auto keep = [&](int w) {  // a stage's winner, already timed, carried into the next stage
-            if (nc < max_cand) cand[nc++] = cand[w];
+            return cand[fastest].ms < cand[lo].ms * (1.0 - kTuneMargin) ? fastest : lo;
         };
         const int cus = cus_min_;
         const int s0 = cfg_.mesh_split.s16, r0 = cfg_.mesh_split.r16;
-        // stage 0: the schedule (all bit-identical) with the configured shape;
-        // the one-shot (one hand-off, (n-1) x the egress) where it fits
+        const int g0 = cfg_.max_blocks, t0 = cfg_.mesh_split.tpb;
+        // stage 0: the schedule (all bit-identical) with the configured shape,
+        // the automatic rule's choice first (the incumbent); the one-shot
+        // (one hand-off, (n-1) x the egress) where it fits
         int lo = nc;
-        time_one(RDC_ALGO_RING, s0, r0, cfg_.max_blocks, cfg_.mesh_split.tpb);
-        time_one(RDC_ALGO_MESH, s0, r0, cfg_.max_blocks, cfg_.mesh_split.tpb);
-        if (oneshot_fits) time_one(RDC_ALGO_ONESHOT, s0, r0, cfg_.max_blocks, cfg_.mesh_split.tpb);
-        int w = agree(lo);
+        add(rule, s0, r0, g0, t0);
+        for (int a : {RDC_ALGO_RING, RDC_ALGO_MESH, RDC_ALGO_ONESHOT})
+            if (a != rule && (a != RDC_ALGO_ONESHOT || oneshot_fits)) add(a, s0, r0, g0, t0);
+        int w = stage(lo);
         if (cand[w].algo == RDC_ALGO_ONESHOT) {
             // no roles or tiles to shape: the schedule is the result
         } else if (cand[w].algo == RDC_ALGO_MESH) {
             static const int kSplits[][2] = {{4, 8}, {3, 9}, {5, 8}, {6, 6}, {3, 10}, {2, 10}, {5, 7}};
             lo = nc;
-            keep(w);
+            add(RDC_ALGO_MESH, cand[w].s16, cand[w].r16, cand[w].grid, cand[w].tpb);
             for (const auto& sp : kSplits)
-                if (sp[0] != cand[w].s16 || sp[1] != cand[w].r16) time_one(RDC_ALGO_MESH, sp[0], sp[1], 0, 0);
-            w = agree(lo);
+                if (sp[0] != cand[lo].s16 || sp[1] != cand[lo].r16) add(RDC_ALGO_MESH, sp[0], sp[1], cand[lo].grid, 0);
+            w = stage(lo);
             const int s16 = cand[w].s16, r16 = cand[w].r16;
             lo = nc;
-            keep(w);
+            add(RDC_ALGO_MESH, s16, r16, cand[w].grid, cand[w].tpb);
             for (int bpc : {1, 2, 3, 4})  // (grid 0 = automatic = 2 per CU)
-                if (bpc * cus != (cand[w].grid ? cand[w].grid : 2 * cus)) time_one(RDC_ALGO_MESH, s16, r16, bpc * cus, 0);
-            w = agree(lo);
+                if (bpc * cus != (cand[lo].grid ? cand[lo].grid : 2 * cus)) add(RDC_ALGO_MESH, s16, r16, bpc * cus, 0);
+            w = stage(lo);
             const int grid = cand[w].grid;
             lo = nc;
-            keep(w);
-            for (int tpb : {1, 4, 8}) time_one(RDC_ALGO_MESH, s16, r16, grid, tpb);
-            w = agree(lo);
+            add(RDC_ALGO_MESH, s16, r16, grid, cand[w].tpb);
+            for (int tpb : {1, 2, 4, 8})  // (tpb 0 = the default, 2 per reduce block)
+                if (tpb != (cand[lo].tpb ? cand[lo].tpb : 2)) add(RDC_ALGO_MESH, s16, r16, grid, tpb);
+            w = stage(lo);
         } else {
             lo = nc;
-            keep(w);
+            add(RDC_ALGO_RING, s0, r0, cand[w].grid, cand[w].tpb);
             for (int bpc : {1, 2})  // (grid 0 = automatic = 1 per CU)
-                if (bpc * cus != (cand[w].grid ? cand[w].grid : cus)) time_one(RDC_ALGO_RING, s0, r0, bpc * cus, 0);
-            w = agree(lo);
+                if (bpc * cus != (cand[lo].grid ? cand[lo].grid : cus)) add(RDC_ALGO_RING, s0, r0, bpc * cus, 0);
+            w = stage(lo);
             const int grid = cand[w].grid;
             lo = nc;
-            keep(w);
-            for (int tpb : {4, 8, 16, 32}) time_one(RDC_ALGO_RING, s0, r0, grid, tpb);
-            w = agree(lo);
+            add(RDC_ALGO_RING, s0, r0, grid, cand[w].tpb);
+            for (int tpb : {1, 4, 8, 16, 32})  // (tpb 0 = the default, 1 per block)
+                if (tpb != (cand[lo].tpb ? cand[lo].tpb : 1)) add(RDC_ALGO_RING, s0, r0, grid, tpb);
+            w = stage(lo);
         }
         set_shape(cand[w]);
         const std::string tf = tune_file();
@@ -1485,9 +1504,16 @@ void Communicator::RaiseIfError(uint32_t e) const {
     if (e != RDC_KERR_NONE) {
         static const char* names[] = {"none", "reduce-scatter wait timed out", "allgather wait timed out",
                                       "broadcast wait timed out", "ring step wait timed out",
-                                      "allgather (buffers) wait timed out"};
+                                      "allgather (buffers) wait timed out",
+                                      "a peer's hand-off belongs to another communicator's collective"};
+        if (e == RDC_KERR_ORDER)
+            throw std::runtime_error(std::string("rdc: device collective failed on rank ") + std::to_string(rank_) +
+                                     ": " + names[e] +
+                                     " (communicators sharing a scratch channel were used in different orders "
+                                     "on different ranks; issue them in one order everywhere or set "
+                                     "RDC_SHARE_SCRATCH=0; communicator is now unusable)");
         throw std::runtime_error(std::string("rdc: device collective failed on rank ") + std::to_string(rank_) +
-                                 ": " + (e < 6 ? names[e] : "unknown") +
+                                 ": " + (e < 7 ? names[e] : "unknown") +
                                  " (a peer did not join the collective; communicator is now unusable)");
     }
 }

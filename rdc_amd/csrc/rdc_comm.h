@@ -92,6 +92,7 @@ struct Channel {
     std::unique_ptr<SmallService> svc;  // started on first use
     std::mutex mu;
     int users = 0;                     // communicators attached
+    uint32_t attached = 0;             // communicators ever attached (the next one's tag)
     uint32_t notify_token = 0;
     hipEvent_t last_ev = nullptr;
     hipStream_t last_stream = nullptr;
@@ -174,13 +175,24 @@ public:
     // same bits, so the same winner), and keep the fastest for allreduces of
     // the same size class ([2^k, 2^(k+1)) bytes: tuned_algo_ / tuned_; Tune
     // clears them; nothing is tuned while RDC_ALGO forces a schedule).
-    // Candidates in cand[] ({algo, s16, r16, grid, tpb, ms}; up to max_cand);
-    // returns their count and *best = the chosen index (-1: nothing to tune,
-    // a tree-order size).  Results stay bit-identical whatever wins.
+    // Noise: every stage times each candidate in kTuneRounds rounds of `reps`
+    // calls, round-robin over the stage's candidates (drift hits them alike);
+    // a candidate's time is the median over rounds of the slowest rank's time
+    // (ms_min / ms_max the spread), and a stage's first candidate — the
+    // automatic rule's schedule in stage 0, the previous stage's winner after
+    // that, re-timed — stays unless another beats its median by more than
+    // kTuneMargin.
+    // Candidates in cand[] ({algo, s16, r16, grid, tpb, ms, ms_min, ms_max};
+    // up to max_cand); returns their count and *best = the chosen index (-1:
+    // nothing to tune, a tree-order size).  Results stay bit-identical
+    // whatever wins.
+    static constexpr int kTuneRounds = 3;
+    static constexpr double kTuneMargin = 0.03;
     struct TuneCand {
         int algo;                 // RDC_ALGO_MESH / RDC_ALGO_RING / RDC_ALGO_ONESHOT
         int s16, r16, grid, tpb;  // tpb: automatic tiles per block (MeshSplit::tpb), 0 = default
-        double ms;
+        double ms;                // median over rounds (slowest rank per round)
+        double ms_min, ms_max;    // spread over rounds
     };
     int Autotune(size_t bytes, int dtype, int reps, hipStream_t stream, TuneCand* cand, int max_cand, int* best);
 
@@ -281,6 +293,7 @@ private:
     size_t slot_bytes_ = 0, region_bytes_ = 0, flag_bytes_ = 0;
     uint32_t max_tiles_ = 0;
     uint32_t seq_ = 0;
+    uint32_t tag_ = 0;              // bits 24-31 of this communicator's launch sequence numbers
     int alloc_kind_ = 0;
     int num_cus_ = 256;             // this GPU
     int cus_min_ = 256;             // fewest CUs of any rank's GPU (grids are planned identically on all ranks)

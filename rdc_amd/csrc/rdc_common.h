@@ -49,7 +49,11 @@ enum {
     RDC_KERR_TIMEOUT_AG = 2,
     RDC_KERR_TIMEOUT_BCAST = 3,
     RDC_KERR_TIMEOUT_RING = 4,
-    RDC_KERR_TIMEOUT_ALLGATHER = 5
+    RDC_KERR_TIMEOUT_ALLGATHER = 5,
+    // a peer's hand-off carried this launch's sequence number but another
+    // communicator's tag: ranks issued the collectives of communicators that
+    // share a channel in different orders (rdc_device.h kSeqBits)
+    RDC_KERR_ORDER = 6
 };
 
 static inline size_t rdc_dtype_size(int dtype) {
@@ -94,6 +98,7 @@ struct CollArgs {
     uint32_t* done_ctr;                  // local per-launch block arrival counter (self-resetting)
     uint32_t* launch_ctr;                // local count of completed launches (device-side seq)
     uint32_t* launch_kind;               // local: kind of the last completed launch
+    uint32_t tag;                        // communicator's tag on its channel: bits 24-31 of every seq
     int kind;                            // this launch's RDC_KIND_*
     int bcast_split;                     // broadcast: root -> forwarder per tile -> other ranks (n >= 3)
     uint64_t half_bytes;                 // one-shot: offset of the slot half used by odd seq

@@ -170,7 +170,20 @@ __device__ __forceinline__ uint32_t flag_load(const uint32_t* p) {
 __device__ __forceinline__ void flag_store(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ bool seq_reached(uint32_t v, uint32_t seq) { return (int32_t)(v - seq) >= 0; }
+// A launch's sequence number: bits 0-23 count the channel's launches (every
+// communicator sharing a channel draws from one counter), bits 24-31 are the
+// launching communicator's tag.  Hand-off flags carry the whole word, so a
+// rank waiting for launch k of communicator X that finds launch k of
+// communicator Y — ranks that issued two communicators' collectives in
+// different orders — fails with RDC_KERR_ORDER instead of folding unrelated
+// buffers.  "Done" words (a peer finished launch k-1, whichever communicator
+// issued it) compare the counter only.  Counters compare modulo 2^24.
+constexpr uint32_t kSeqBits = 24;
+constexpr uint32_t kSeqMask = (1u << kSeqBits) - 1u;
+__device__ __forceinline__ bool seq_reached(uint32_t v, uint32_t seq) {
+    return (int32_t)((v - seq) << (32 - kSeqBits)) >= 0;
+}
+__device__ __forceinline__ bool same_tag(uint32_t v, uint32_t seq) { return ((v ^ seq) >> kSeqBits) == 0; }
 
 // Called by EVERY thread of the block after its payload stores.  Lanes
 // 0..nflags-1 of wave 0 then store flags[i] = seq.
@@ -216,22 +229,36 @@ struct Abort {
 // Block-wide wait until every flags[i] (i < nflags <= 64) reached seq.  Wave 0
 // polls (one lane per flag), sleeping between polls; the other waves park at
 // the barrier.  Returns false (uniformly) on timeout or if another block of
-// this launch already aborted.  With cached scratch the matching lane then
+// this launch already aborted.  tagged (hand-off flags of this launch): a
+// flag that reached the counter with another communicator's tag is an order
+// violation (RDC_KERR_ORDER, immediate); untagged (done words): the counter only.  With cached scratch the matching lane then
 // runs a system-scope acquire (L2 / L1 invalidate) so the block's plain loads
 // of the handed-off bytes cannot hit stale lines; uncached scratch (`uc`) is
 // never held in any GPU cache, so its loads after the matched poll read
 // memory and need no invalidate (MI355X_MICROARCH.md: an acquire is ≈1.7 us).
 __device__ __forceinline__ bool block_wait(uint32_t* const* flags, int nflags, uint32_t seq,
-                                           const Abort& ab, uint32_t code, int uc) {
+                                           const Abort& ab, uint32_t code, int uc, bool tagged = true) {
     __shared__ int s_ok;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         bool mine = lane >= nflags;
         bool ok = true;
+        bool wrong = false;  // this lane's flag reached the counter with another tag
         uint32_t spins = 0;
         while (true) {
-            if (!mine) mine = seq_reached(flag_load(flags[lane]), seq);
+            if (!mine) {
+                const uint32_t v = flag_load(flags[lane]);
+                if (seq_reached(v, seq)) {
+                    if (!tagged || same_tag(v, seq)) mine = true;
+                    else wrong = true;
+                }
+            }
             if (__all(mine)) break;
+            if (__any(wrong)) {
+                code = RDC_KERR_ORDER;
+                ok = false;
+                break;
+            }
             if ((++spins & 63) == 0) {
                 bool dead = wall_clock64() > ab.deadline ||
                             __hip_atomic_load(ab.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;

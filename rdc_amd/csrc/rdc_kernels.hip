@@ -30,7 +30,7 @@ __device__ void allgather_body(const CollArgs& a, uint32_t seq) {
         if (b < items) {
             if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = done_word(a, r, (r + 1 + threadIdx.x) % n);
             __syncthreads();
-            if (!block_wait(s_flags, n - 1, seq - 1, ab, RDC_KERR_TIMEOUT_ALLGATHER, a.uc)) return;
+            if (!block_wait(s_flags, n - 1, seq - 1, ab, RDC_KERR_TIMEOUT_ALLGATHER, a.uc, false)) return;
         }
         for (int it = b; it < items; it += a.nb_scatter) {
             const int t = it / (n - 1);

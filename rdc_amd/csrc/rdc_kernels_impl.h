@@ -40,8 +40,11 @@ __device__ __forceinline__ uint32_t* done_word(const CollArgs& a, int owner, int
 // correctly: every block reads the communicator's launch counter when it
 // starts (seq = launches completed + 1, identical on every rank because all
 // ranks issue the same collectives), and the launch's last block advances it.
+// The counter lives in bits 0-23, the launching communicator's tag in bits
+// 24-31 (rdc_device.h kSeqBits).
 __device__ __forceinline__ uint32_t launch_seq(const CollArgs& a) {
-    return __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const uint32_t done = __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ((done + 1u) & kSeqMask) | (a.tag << kSeqBits);
 }
 __device__ __forceinline__ uint32_t prev_kind(const CollArgs& a) {
     return __hip_atomic_load(a.launch_kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -55,7 +58,7 @@ __device__ __forceinline__ bool gate_on_peers(const CollArgs& a, uint32_t seq, i
     __shared__ uint32_t* s_gate[RDC_MAX_RANKS];
     if (threadIdx.x < (unsigned)count) s_gate[threadIdx.x] = done_word(a, a.rank, (first + threadIdx.x) % a.n);
     __syncthreads();
-    return block_wait(s_gate, count, seq - 1, ab, code, a.uc);
+    return block_wait(s_gate, count, seq - 1, ab, code, a.uc, false);
 }
 
 
@@ -653,7 +656,7 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
             s_cnt = k;
         }
         __syncthreads();
-        if (!block_wait(s_flags, s_cnt, seq - 1, ab, RDC_KERR_TIMEOUT_BCAST, a.uc)) return;
+        if (!block_wait(s_flags, s_cnt, seq - 1, ab, RDC_KERR_TIMEOUT_BCAST, a.uc, false)) return;
     }
     for (int t = blockIdx.x; t < a.tiles[0]; t += gridDim.x) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;

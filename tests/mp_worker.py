@@ -120,6 +120,31 @@ def main():
                 e.destroy()
             print("rank %d case %d ok" % (rank, i), flush=True)
             continue
+        if kind == "order_violation":
+            # two communicators sharing one channel issued in DIFFERENT orders
+            # on different ranks (rank 0: main then x; the others: x then
+            # main): the launches with equal sequence numbers belong to
+            # different communicators, which the tagged hand-off flags turn
+            # into an error on every rank instead of folding unrelated buffers
+            other = rdc_amd.new_comm("order_%d" % i)
+            info = {"shares": [comm.get_param("shares_scratch"), other.get_param("shares_scratch")]}
+            a = torch.zeros(count, dtype=torch.float32, device="cuda")
+            b = torch.zeros(count, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            order = [(comm, a), (other, b)] if rank == 0 else [(other, b), (comm, a)]
+            err = ""
+            try:
+                for cm, t in order:
+                    check_call(_LIB.RdcCommAllreduceEx(cm.handle, ctypes.c_void_p(t.data_ptr()), count, 6, 2,
+                                                       c.get("algo", 0), sp))
+                comm.check(sp)
+            except Exception as e:  # noqa: BLE001 - the expected outcome
+                err = str(e)
+            info["error"] = err
+            open(os.path.join(outdir, "case%d_rank%d.json" % (i, rank)), "w").write(json.dumps(info))
+            print("rank %d case %d ok" % (rank, i), flush=True)
+            # the channel is unusable now: leave without finalizing collectives
+            os._exit(0)
         if kind == "bcast_chain":
             # stream-ordered chain without host syncs: refill, broadcast from a
             # rotating root, accumulate — exposes a root overwriting a peer's

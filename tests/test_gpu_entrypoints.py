@@ -79,7 +79,34 @@ def test_bench_torchrun_two_ranks():
     ex = out["extra_configs"]
     assert ex["cfg1_host_4KiB"]["us_per_call"] > 0 and ex["cfg5_buckets"]["ms_per_step"] > 0
     chk = out["oracle_check"]
-    assert all(chk[k] is True for k in ("cfg3_mesh", "cfg3_ring", "cfg4_fp16", "cfg5_buckets")), chk
+    assert all(chk.get(k) is True for k in PARITY_KEYS), chk
+    assert out["extras_skipped"] == [] and "parity_checks" in out["extras_wall_s"], out["extras_wall_s"]
+
+
+# every hand-off kind the timed lines use, verified bit-exact in bench.py's
+# parity_checks
+PARITY_KEYS = ("cfg3_mesh", "cfg3_ring", "cfg4_fp16", "cfg5_buckets", "oneshot_512KiB", "service_host_4KiB",
+               "tree_order", "broadcast_nonzero_root", "allgather_varsize")
+
+
+def test_bench_tiny_extras_budget():
+    """--extras-budget-s bounds everything after the timed region: with a
+    1-second budget the headline line is still printed, every extra is listed
+    in extras_skipped and none ran."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--bytes", str(16 << 20), "--extras-budget-s", "1",
+           "--autotune-reps", "0"]
+    p = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ), capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["value"] > 0 and out["extras_budget_s"] == 1
+    assert set(out["extras_skipped"]) >= {"parity_checks", "ring_schedule", "extra_configs", "cpu_tcp_ring"}, out
+    assert out["extras_wall_s"].get("role_timeline") is not None or "role_timeline" in out["extras_skipped"]
+    assert "extra_configs" not in out and "oracle_check" not in out
 
 
 def test_launcher_cpp_known_answer(known_answer_exe):
@@ -93,6 +120,28 @@ def test_launcher_cpp_known_answer(known_answer_exe):
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     for r in range(3):
         assert "rank %d: known-answer OK" % r in p.stdout, p.stdout
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_python_surface_across_ranks(world):
+    """rdc_amd's Python surface at world size > 1, launched as the reference
+    launches pytest/allreduce.py (launcher -n N python script): the harness's
+    MAX/SUM known answers, allreduce's copy rule on owning / 2-D / view /
+    non-contiguous arrays, prepare_fun inside RdcAllreduce, pickled broadcast
+    from non-zero roots, and collectives on new_comm("x") / get_comm("x")
+    handles (host allreduce, isend/irecv ring, device allreduce)
+    (tests/py_surface_worker.py)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, RDC_SCRATCH_BYTES="64M")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-m", "rdc_amd.launcher", "-n", str(world), "--gpus", "1", sys.executable,
+                        os.path.join(ROOT, "tests", "py_surface_worker.py")],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(world):
+        assert "rank %d: python surface OK" % r in p.stdout, p.stdout + p.stderr[-2000:]
 
 
 @pytest.fixture(scope="module")
