@@ -87,11 +87,16 @@ int RdcAllgatherOn(void* comm, void** bufs, const size_t* sizes);
 
 /* Coalesced (bucketed) allreduce: the result of one RdcAllreduce per buffer,
  * in order, bit-identical, but the buffers move in fused launches (BASELINE
- * cfg5 / test/mallreduce.cc's back-to-back shape).  With the mesh schedule the
- * launches read and write the buffers in place through a cached unit table
- * (groups of up to RDC_FUSE_BYTES_DIRECT, default 16 GiB); one-shot / ring
- * lists are packed chunk-major into an HBM staging image in groups of
- * RDC_FUSE_BYTES (default 256 MiB).
+ * cfg5 / test/mallreduce.cc's back-to-back shape).  A list takes the schedule
+ * and launch shape one buffer of its total size would get (the automatic rule,
+ * or what RdcCommAutotune chose for that size class); the mesh and the ring
+ * read and write the buffers in place through a cached unit table (groups of
+ * up to RDC_FUSE_BYTES_DIRECT, default 16 GiB); one-shot lists are packed
+ * chunk-major into an HBM staging image in groups of RDC_FUSE_BYTES (default
+ * 256 MiB).  Buckets whose addresses are 16-B aligned take the vector paths;
+ * a bucket that is only element-aligned folds element by element (correct,
+ * slower): RdcCommGetParam(comm, "coalesced_misaligned") counts them in the
+ * last coalesced call.
  * bufs[b] holds counts[b] elements of `dtype`; all host or all device memory;
  * synchronous.  RdcAllreduceCoalesced uses the "main" communicator. */
 int RdcAllreduceCoalesced(void** bufs, const size_t* counts, int nbuf, int dtype, int op);
@@ -179,7 +184,8 @@ int RdcCommAllgather(void* comm, void** dev_bufs, const size_t* sizes, void* str
 int RdcCommCheck(void* comm, void* stream);
 /* A communicator's parameter: "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES",
  * "RDC_TILE_BYTES", "RDC_NBLOCKS", "RDC_ONESHOT_BYTES", "slot_bytes",
- * "ranks_per_gpu" (most ranks of it sharing one physical GPU), "shares_scratch"
+ * "ranks_per_gpu" (most ranks of it sharing one physical GPU), "coalesced_misaligned"
+ * (buckets of the last coalesced call not 16-B aligned), "shares_scratch"
  * (1 when another communicator uses the same scratch channel: every named
  * communicator over the same ranks shares one, RDC_SHARE_SCRATCH=0 disables). */
 int RdcCommGetParam(void* comm, const char* key, uint64_t* value);

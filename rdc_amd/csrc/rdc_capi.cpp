@@ -612,6 +612,7 @@ int RdcCommGetParam(void* comm, const char* key, uint64_t* value) {
         else if (k == "RDC_ONESHOT_BYTES") *value = g.oneshot_push_max;
         else if (k == "slot_bytes") *value = c->slot_bytes();
         else if (k == "ranks_per_gpu") *value = (uint64_t)c->ranks_per_gpu();
+        else if (k == "coalesced_misaligned") *value = (uint64_t)c->coalesced_misaligned_;
         else if (k == "shares_scratch") *value = c->shares_channel() ? 1 : 0;
         else throw std::invalid_argument("rdc: unknown parameter " + k);
     });

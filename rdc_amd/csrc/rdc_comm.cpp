@@ -74,7 +74,7 @@ struct PeerInfo {
     int32_t device;
     int32_t pid;
     int32_t alloc_kind;
-    int32_t pad;
+    int32_t svc_ok;  // a new channel may run the small-allreduce service here
     uint64_t slot_bytes;
     uint64_t max_tiles;
     uint64_t p2p_slot_bytes;
@@ -113,44 +113,59 @@ const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYT
                                         "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "RDC_MESH_SPLIT",
                                         "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES", "RDC_HOST_SERVICE",
                                         "RDC_HOST_SERVICE_SHARE_MAX", "RDC_HOST_PIECE_BYTES",
-                                        "RDC_TUNE_FILE (contents)"};
+                                        "RDC_TUNE_FILE (set or not)"};
 
 // Autotune results kept across runs (RDC_TUNE_FILE): one line per winner,
-// "rdc-tune 1 <ranks> <cus> <size class> <algo> <s16> <r16> <grid> <tpb> <ms>",
-// later lines overriding earlier ones.  Every rank reads the file itself at
-// communicator creation; its contents' hash is a plan key, so ranks that read
-// different tables are refused instead of planning differently.  Only rank 0
-// appends (Communicator::Autotune).
+// "rdc-tune 2 <ranks> <cus> <ranks per gpu> <size class> <algo> <s16> <r16>
+// <grid> <tpb> <ms>", later lines overriding earlier ones.  Rank 0 alone
+// reads the file at communicator creation and broadcasts the parsed entries,
+// so every rank plans from the same table even while another job appends to
+// the file; only rank 0 appends (Communicator::Autotune).  Entries apply to
+// communicators of the same rank count, fewest CUs and ranks per GPU (a shape
+// tuned with ranks sharing a GPU says nothing about one rank per GPU).
 struct TuneEntry {
-    int n, cus, cls, algo, s16, r16, grid, tpb;
+    int32_t n, cus, rpg, cls, algo, s16, r16, grid, tpb;
 };
+constexpr int kTuneEntriesMax = 256;  // the latest ones are kept
 std::string tune_file() {
     const char* e = getenv("RDC_TUNE_FILE");
     return e && *e ? std::string(e) : std::string();
 }
-std::vector<TuneEntry> read_tune_file(const std::string& path, uint64_t* hash) {
+std::vector<TuneEntry> read_tune_file(const std::string& path) {
     std::vector<TuneEntry> out;
-    *hash = 0;
     if (path.empty()) return out;
     FILE* f = fopen(path.c_str(), "r");
-    if (!f) return out;  // no table yet: nothing tuned (hash 0 on every rank)
-    uint64_t h = 1469598103934665603ull;  // FNV-1a over the bytes
+    if (!f) return out;  // no table yet: nothing tuned
     char line[256];
     while (fgets(line, sizeof(line), f)) {
-        for (const char* p = line; *p; ++p) h = (h ^ (unsigned char)*p) * 1099511628211ull;
         TuneEntry e;
         int ver = 0;
         double ms = 0;
-        if (sscanf(line, "rdc-tune %d %d %d %d %d %d %d %d %d %lf", &ver, &e.n, &e.cus, &e.cls, &e.algo, &e.s16,
-                   &e.r16, &e.grid, &e.tpb, &ms) == 10 &&
-            ver == 1 && e.cls >= 0 && e.cls < 64 &&
+        if (sscanf(line, "rdc-tune %d %d %d %d %d %d %d %d %d %d %lf", &ver, &e.n, &e.cus, &e.rpg, &e.cls, &e.algo,
+                   &e.s16, &e.r16, &e.grid, &e.tpb, &ms) == 11 &&
+            ver == 2 && e.rpg >= 1 && e.cls >= 0 && e.cls < 64 &&
             (e.algo == RDC_ALGO_RING || e.algo == RDC_ALGO_MESH || e.algo == RDC_ALGO_ONESHOT) && e.s16 >= 1 &&
             e.r16 >= 1 && e.s16 + e.r16 <= 15 && e.grid >= 0 && e.tpb >= 0)
             out.push_back(e);
     }
     fclose(f);
-    *hash = h;
+    if (out.size() > (size_t)kTuneEntriesMax) out.erase(out.begin(), out.end() - kTuneEntriesMax);
     return out;
+}
+// rank 0's table on every rank (collective over bs)
+std::vector<TuneEntry> shared_tune_table(Bootstrap* bs) {
+    struct {
+        int32_t count;
+        TuneEntry e[kTuneEntriesMax];
+    } msg;
+    memset(&msg, 0, sizeof(msg));
+    if (bs->rank() == 0) {
+        const std::vector<TuneEntry> t = read_tune_file(tune_file());
+        msg.count = (int32_t)t.size();
+        if (!t.empty()) memcpy(msg.e, t.data(), t.size() * sizeof(TuneEntry));
+    }
+    bs->broadcast(&msg, sizeof(msg), 0);
+    return std::vector<TuneEntry>(msg.e, msg.e + std::max(0, std::min(msg.count, kTuneEntriesMax)));
 }
 
 // The point-to-point control block (rdc_p2p.h) in POSIX shared memory: rank 0
@@ -210,6 +225,20 @@ namespace {
 std::mutex g_reg_mu;
 std::map<Bootstrap*, std::vector<std::weak_ptr<Channel>>> g_channels;
 std::map<Bootstrap*, uint64_t> g_channel_count;
+// channels of this process whose small-allreduce service may run, per device:
+// at most one (Communicator::Create), so at most one persistent service block
+// per process and GPU is resident — what LaunchGrid's one-CU-per-rank
+// reservation assumes
+// (leaked: channels may be destroyed from other translation units' static
+// destructors at exit)
+struct SvcRegistry {
+    std::mutex mu;
+    std::map<int, int> channels;
+};
+SvcRegistry& svc_registry() {
+    static SvcRegistry* r = new SvcRegistry();
+    return *r;
+}
 
 // RDC_STRICT_FENCES=1: keep the system-scope release fences on every hand-off
 // even with uncached scratch (diagnostics; rdc_device.h block_publish)
@@ -229,6 +258,10 @@ bool share_enabled() {
 
 Channel::~Channel() {
     svc.reset();  // the resident service block leaves first
+    if (svc_counted) {
+        std::lock_guard<std::mutex> lk(svc_registry().mu);
+        --svc_registry().channels[device];
+    }
     (void)hipSetDevice(device);
     (void)hipDeviceSynchronize();
     if (ipc && bs) {
@@ -423,9 +456,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     mine.slot_bytes = L.slot_bytes;
     mine.max_tiles = L.max_tiles;
     mine.num_cus = c->num_cus_;
-    uint64_t tune_hash = 0;
-    const std::vector<TuneEntry> tuned = read_tune_file(tune_file(), &tune_hash);
-    PlanKey(cfg, tune_hash, mine.plan);
+    PlanKey(cfg, tune_file().empty() ? 0 : 1, mine.plan);
     std::shared_ptr<Channel> cand;
     if (share_enabled()) {
         std::lock_guard<std::mutex> lk(g_reg_mu);
@@ -441,6 +472,13 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         }
     }
     mine.channel = cand ? cand->id : 0;
+    {
+        // a NEW channel may run the small-allreduce service only if no other
+        // channel of this process on this device may (one resident service
+        // block per process and GPU, LaunchGrid); agreed below (AND over ranks)
+        std::lock_guard<std::mutex> lk(svc_registry().mu);
+        mine.svc_ok = (SmallService::Enabled() && svc_registry().channels[device] == 0) ? 1 : 0;
+    }
     gethostname(mine.host, sizeof(mine.host) - 1);
     if (hipDeviceGetPCIBusId(mine.pci, sizeof(mine.pci) - 1, device) != hipSuccess) {
         (void)hipGetLastError();
@@ -449,8 +487,10 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     std::vector<PeerInfo> all((size_t)c->n_);
     bs->allgather(&mine, sizeof(mine), all.data());
     bool share = mine.channel != 0;
+    bool svc_all = true;
     for (int p = 0; p < c->n_; ++p) {
         const PeerInfo& q = all[(size_t)p];
+        svc_all = svc_all && q.svc_ok != 0;
         if (q.slot_bytes != mine.slot_bytes || q.max_tiles != mine.max_tiles ||
             q.p2p_slot_bytes != mine.p2p_slot_bytes)
             throw std::runtime_error("rdc: ranks disagree on scratch size (set RDC_SCRATCH_BYTES identically)");
@@ -476,10 +516,11 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         c->share_max_ = std::max(c->share_max_, same);
     }
     // schedules and shapes an earlier Autotune of this node measured for this
-    // rank count and CU count (RDC_TUNE_FILE); every rank read the same table
+    // rank count, CU count and ranks per GPU (RDC_TUNE_FILE, rank 0's table)
+    const std::vector<TuneEntry> tuned = tune_file().empty() ? std::vector<TuneEntry>() : shared_tune_table(bs);
     if (cfg.algo == RDC_ALGO_AUTO)
         for (const TuneEntry& e : tuned) {
-            if (e.n != c->n_ || e.cus != c->cus_min_) continue;
+            if (e.n != c->n_ || e.cus != c->cus_min_ || e.rpg != c->share_max_) continue;
             Shape s;
             s.split.s16 = e.s16;
             s.split.r16 = e.r16;
@@ -504,8 +545,17 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     // round 2: IPC handles of a new channel (unless shared) and of this
     // communicator's point-to-point region
     dbg("[rdc %d] %s\n", c->rank_, share ? "sharing the channel" : "alloc");
-    if (share) c->Attach(cand);
-    else c->AllocChannel();
+    if (share) {
+        c->Attach(cand);
+    } else {
+        c->AllocChannel();
+        if (svc_all) {
+            std::lock_guard<std::mutex> lk(svc_registry().mu);
+            ++svc_registry().channels[device];
+            c->ch_->svc_enabled = true;
+            c->ch_->svc_counted = true;
+        }
+    }
     c->AllocP2P();
     Handles h;
     memset(&h, 0, sizeof(h));
@@ -576,6 +626,7 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
         c->device_ = devices[i];
         c->cfg_ = cfg;
         c->AllocLocal();
+        c->ch_->svc_enabled = SmallService::Enabled();  // one process drives every rank: all or none
         cs.push_back(std::move(c));
     }
     int share = 1, cus = cs[0]->num_cus_;
@@ -861,7 +912,8 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
                                 uint64_t total, size_t esz, int algo, hipStream_t stream, const PackUnit* units,
                                 int nunits) {
     algo = PickAlgo(algo, total);
-    if (units && algo != RDC_ALGO_MESH) throw std::logic_error("rdc: unit-table launch needs the mesh schedule");
+    if (units && algo != RDC_ALGO_MESH && algo != RDC_ALGO_RING)
+        throw std::logic_error("rdc: unit-table launch needs the mesh or ring schedule");
     if (algo == RDC_ALGO_ONESHOT) {
         const Piece p = PlanOneshotRanges(n_, off, len, total, layout(), cfg_.tile_bytes,
                                           LaunchGrid(max_blocks(), ks.occupancy(RDC_KIND_ONESHOT, n_)));
@@ -918,6 +970,8 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         last_launch_[3] = (uint64_t)(algo == RDC_ALGO_RING ? 0 : p.nb_gather);
         last_launch_[4] = p.tile_bytes;
         last_launch_[5] = (uint64_t)algo;
+        a.units = units;
+        a.nunits = nunits;
         if (algo == RDC_ALGO_RING) {
             a.kind = RDC_KIND_RING;
             hip_check(ks.ring(a, grid, stream), "launch ring allreduce");
@@ -926,8 +980,6 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
             a.nb_reduce = p.nb_reduce;
             a.nb_gather = p.nb_gather;
             a.kind = RDC_KIND_MESH;
-            a.units = units;
-            a.nunits = nunits;
             hip_check(ks.mesh(a, grid, stream), "launch mesh allreduce");
         }
     }
@@ -1027,10 +1079,13 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
                                     std::to_string(op) + ")");
     if (nbuf < 0 || (nbuf > 0 && (!bufs || !counts))) throw std::invalid_argument("rdc: bad buffer list");
     const size_t esz = rdc_dtype_size(dtype);
+    int misaligned = 0;
     for (int b = 0; b < nbuf; ++b) {
         if (counts[b] && bufs[b] == nullptr) throw std::invalid_argument("rdc: null buffer in coalesced allreduce");
         if ((uintptr_t)bufs[b] % esz) throw std::invalid_argument("rdc: buffer not aligned to its element size");
+        misaligned += counts[b] != 0 && ((uintptr_t)bufs[b] & 15) != 0;
     }
+    coalesced_misaligned_ = misaligned;
     if (n_ == 1 || nbuf == 0) return;
     hip_check(hipSetDevice(device_), "hipSetDevice");
     ChannelCall call(ch_.get(), stream);
@@ -1069,13 +1124,14 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
                 bytes += (uint64_t)counts[b] * esz;
                 live += counts[b] != 0;
             }
-            // auto picks the ring at n = 2, but a list is faster through the
-            // unit-table mesh (no staging image) than staged through the ring
+            // the schedule (and, via ShapeFor, the launch shape) a single
+            // buffer of the list's size class gets — the automatic rule or
+            // what Autotune measured — run over the unit table: mesh and ring
+            // read and write the user buffers in place, no staging image
             const int pick = PickAlgo(algo, bytes);
-            const bool automatic = algo == RDC_ALGO_AUTO && cfg_.algo == RDC_ALGO_AUTO;
-            if (live >= 2 && (pick == RDC_ALGO_MESH || (automatic && pick == RDC_ALGO_RING))) {
+            if (live >= 2 && (pick == RDC_ALGO_MESH || pick == RDC_ALGO_RING)) {
                 const PackEntry& e = PackTable(bufs + b0, counts + b0, b1 - b0, esz, stream);
-                LaunchRanges(ks, nullptr, e.off, e.len, e.total, esz, RDC_ALGO_MESH, stream, e.dtable, e.nunits);
+                LaunchRanges(ks, nullptr, e.off, e.len, e.total, esz, pick, stream, e.dtable, e.nunits);
             } else {
                 CoalescedStaged(ks, bufs + b0, counts + b0, b1 - b0, dtype, op, esz, algo, stream);
             }
@@ -1335,8 +1391,8 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
             if (rank_ == 0) {
                 FILE* f = fopen(tf.c_str(), "a");
                 if (!f) throw std::runtime_error("rdc: cannot append to RDC_TUNE_FILE " + tf);
-                fprintf(f, "rdc-tune 1 %d %d %d %d %d %d %d %d %.4f\n", n_, cus_min_, cls, cand[w].algo, cand[w].s16,
-                        cand[w].r16, cand[w].grid, cand[w].tpb, cand[w].ms);
+                fprintf(f, "rdc-tune 2 %d %d %d %d %d %d %d %d %d %.4f\n", n_, cus_min_, share_max_, cls, cand[w].algo,
+                        cand[w].s16, cand[w].r16, cand[w].grid, cand[w].tpb, cand[w].ms);
                 fclose(f);
             }
             hip_check(hipMemsetAsync(dms, 0, sizeof(double), stream), "memset");
@@ -1431,7 +1487,7 @@ bool Communicator::SmallHostAllreduce(void* host, size_t count, int dtype, int o
     // outnumber what the hardware scheduler keeps mapped and it time-slices
     // them (measured: 8 ranks on one MI355X, ~10 ms per call), so past
     // RDC_HOST_SERVICE_SHARE_MAX ranks per GPU (default 4) the launch path runs
-    if (n_ == 1 || bytes == 0 || bytes > RDC_SVC_MAX_BYTES || !ch_ || !ch_->svc_region || !SmallService::Enabled() ||
+    if (n_ == 1 || bytes == 0 || bytes > RDC_SVC_MAX_BYTES || !ch_ || !ch_->svc_region || !ch_->svc_enabled ||
         share_max_ > SmallService::ShareMax())
         return false;
     KernelSet ks;

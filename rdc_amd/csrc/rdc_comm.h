@@ -90,6 +90,8 @@ struct Channel {
     char* svc_region = nullptr;
     char* peer_svc_region[RDC_MAX_RANKS] = {};
     std::unique_ptr<SmallService> svc;  // started on first use
+    bool svc_enabled = false;          // agreed at creation: the service may run on this channel
+    bool svc_counted = false;          // counted in the process's per-device service registry
     std::mutex mu;
     int users = 0;                     // communicators attached
     uint32_t attached = 0;             // communicators ever attached (the next one's tag)
@@ -226,8 +228,8 @@ public:
     // Launch shape of a mesh / ring allreduce of `total` bytes: the shape
     // Autotune recorded for its size class (floor(log2(total))) and schedule,
     // else the communicator's configuration (defaults, RDC_* env, Tune).
-    // (A coalesced list of the same size class takes the unit-table mesh: it
-    // uses a mesh shape tuned for that class, never a ring one.)
+    // (A coalesced list of the same size class takes the same schedule and
+    // shape over its unit table.)
     struct Shape {
         MeshSplit split;
         int max_blocks = 0;
@@ -294,6 +296,9 @@ private:
     uint32_t max_tiles_ = 0;
     uint32_t seq_ = 0;
     uint32_t tag_ = 0;              // bits 24-31 of this communicator's launch sequence numbers
+public:
+    int coalesced_misaligned_ = 0;  // buckets of the last coalesced call not 16-B aligned (element-wise folds)
+private:
     int alloc_kind_ = 0;
     int num_cus_ = 256;             // this GPU
     int cus_min_ = 256;             // fewest CUs of any rank's GPU (grids are planned identically on all ranks)

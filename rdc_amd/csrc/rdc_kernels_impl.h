@@ -384,6 +384,19 @@ __device__ void block_reduce_into(char* own, const char* recv, uint64_t len) {
     for (; i < nvec; i += kBlock) st16(d + i, reduce16<OP, T>(ld16(d + i), ld16_nt(s + i)));
 }
 
+// Chunk c's user bytes [off[c] + toff, + tlen) as (user pointer, offset from
+// off[c], bytes) pieces: one piece of the buffer, or — coalesced lists
+// (a.units) — the unit pieces the packed range covers (rdc_plan.h
+// PlanCoalesced: user slices and scratch images are congruent mod 16).
+template <typename F>
+__device__ __forceinline__ void chunk_pieces(const CollArgs& a, int c, uint64_t toff, uint64_t tlen, F&& f) {
+    if (a.units)
+        for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen,
+                        [&](char* usr, uint64_t p, uint64_t l) { f(usr, p - a.off[c], l); });
+    else
+        f(a.user + a.off[c] + toff, toff, tlen);
+}
+
 template <int OP, typename T>
 __device__ void ring_body(const CollArgs& a, uint32_t seq) {
     const int n = a.n, r = a.rank;
@@ -402,8 +415,10 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
             if (t < a.tiles[cs]) {
                 uint64_t tlen = a.len[cs] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_copy<kDstPeer>(a.rs[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
-                           tlen);
+                char* dst = a.rs[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs];
+                chunk_pieces(a, cs, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
+                    block_copy<kDstPeer>(dst + co, usr, l);
+                });
                 block_publish1(a.flags[prev] + (uint64_t)j * a.max_tiles + t, seq, a.uc);
             }
             const int cr = (r + 2 + j) % n;
@@ -413,8 +428,10 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
                 if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING, a.uc)) return;
                 uint64_t tlen = a.len[cr] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_reduce_into<OP, T>(a.user + a.off[cr] + toff,
-                                         a.rs[r] + (uint64_t)j * a.slot_bytes + a.mis[cr] + toff, tlen);
+                const char* src = a.rs[r] + (uint64_t)j * a.slot_bytes + a.mis[cr];
+                chunk_pieces(a, cr, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
+                    block_reduce_into<OP, T>(usr, src + co, l);
+                });
                 __syncthreads();
             }
         }
@@ -425,8 +442,10 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
             if (t < a.tiles[cs]) {
                 uint64_t tlen = a.len[cs] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_copy<kDstPeer>(a.ag[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs] + toff, a.user + a.off[cs] + toff,
-                           tlen);
+                char* dst = a.ag[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs];
+                chunk_pieces(a, cs, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
+                    block_copy<kDstPeer>(dst + co, usr, l);
+                });
                 block_publish1(a.flags[prev] + (uint64_t)(n + j) * a.max_tiles + t, seq, a.uc);
             }
             const int cr = (r + 1 + j) % n;
@@ -436,8 +455,10 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
                 if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING, a.uc)) return;
                 uint64_t tlen = a.len[cr] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                block_copy<kDstLocal>(a.user + a.off[cr] + toff, a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr] + toff,
-                           tlen);
+                const char* src = a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr];
+                chunk_pieces(a, cr, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
+                    block_copy<kDstLocal>(usr, src + co, l);
+                });
                 __syncthreads();
             }
         }

@@ -159,8 +159,18 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
             put(j, v);
         }
         const uint64_t plane_words = nwords / 2;  // nwords is a multiple of 4
-        memcpy(box_->data, stage_.data(), plane_words * 8);
-        memcpy(box_->data + RDC_SVC_LL_MAX, stage_.data() + RDC_SVC_LL_MAX / 8, plane_words * 8);
+        // each 8-byte {payload, r} word must become visible whole: a word
+        // whose r landed before its payload would be taken with stale data.
+        // memcpy gives no such guarantee (rep movsb, overlapping vector
+        // stores); aligned 8-byte atomic stores do.
+        uint64_t* p0 = reinterpret_cast<uint64_t*>(box_->data);
+        uint64_t* p1 = reinterpret_cast<uint64_t*>(box_->data + RDC_SVC_LL_MAX);
+        const uint64_t* s0 = stage_.data();
+        const uint64_t* s1 = stage_.data() + RDC_SVC_LL_MAX / 8;
+        for (uint64_t j = 0; j < plane_words; ++j) {
+            __atomic_store_n(p0 + j, s0[j], __ATOMIC_RELAXED);
+            __atomic_store_n(p1 + j, s1[j], __ATOMIC_RELAXED);
+        }
         if (args_.trace) ht_[0] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     } else {
         memcpy(box_->data, host, bytes);

@@ -639,7 +639,7 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
              {"count": 2 * big, "dtype": 10, "op": 2},
              {"count": big + 12345, "dtype": 2, "op": 0},
              {"count": big // 2 - 7, "dtype": 7, "op": 1},
-             # a coalesced list of the tuned size class keeps the unit-table mesh whichever schedule won
+             # a coalesced list of the tuned size class takes the schedule and shape that won (unit table)
              {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1 << 20] * 8}]
     tmp = run_mp(world, cases, timeout=400)
     for i, c in enumerate(cases):
@@ -690,7 +690,7 @@ def test_mp_tune_file_persists_autotune():
     first = run_mp(2, [{"count": big, "dtype": 6, "op": 2, "autotune": big * 4, "last_launch": True}],
                    timeout=400, env_extra=env)
     lines = open(path).read().splitlines()
-    assert len(lines) == 1 and lines[0].startswith("rdc-tune 1 2 "), lines
+    assert len(lines) == 1 and lines[0].startswith("rdc-tune 2 2 "), lines
     second = run_mp(2, [{"count": big, "dtype": 6, "op": 2, "last_launch": True},
                         {"count": big + 3, "dtype": 10, "op": 2, "last_launch": True}], env_extra=env)
     tuned = json.load(open(os.path.join(first, "case0_rank0.tune")))
@@ -806,12 +806,14 @@ def test_group3_coalesced(group3, dtype, op, algo):
                 assert same_bits(got[r][b], want, dtype), (counts, algo, b, r)
 
 
+@pytest.mark.parametrize("algo", [2, 1])
 @pytest.mark.parametrize("fused,tile", [("1", "16K"), ("1", "0"), ("0", "16K")])
-def test_group_coalesced_mesh_unit_table(fused, tile):
-    """The mesh on a coalesced list moves bytes straight between the user
-    buffers and the peers' scratch through the unit table (no staging image);
-    small tiles make tiles start and end inside units and span several.
-    RDC_COALESCE_FUSED=0 keeps the pack / mesh / unpack path.  Bit-exact."""
+def test_group_coalesced_mesh_unit_table(fused, tile, algo):
+    """The mesh (algo 2) and the ring (algo 1) on a coalesced list move bytes
+    straight between the user buffers and the peers' scratch through the unit
+    table (no staging image); small tiles make tiles start and end inside
+    units and span several.  RDC_COALESCE_FUSED=0 keeps the pack / schedule /
+    unpack path.  Bit-exact."""
     from rdc_amd._lib import _LIB
     assert _LIB.RdcSetParam(b"RDC_COALESCE_FUSED", fused.encode()) == 0
     assert _LIB.RdcSetParam(b"RDC_TILE_BYTES", tile.encode()) == 0
@@ -827,11 +829,11 @@ def test_group_coalesced_mesh_unit_table(fused, tile):
                                   (7, 2, [40000, 40001, 2])]:
             sets = [[rand_input(rng, k, dtype) for k in counts] for _ in range(2)]
             pads = [[(r + b) % 3 for b in range(len(counts))] for r in range(2)]
-            got = run_group_coalesced(g, sets, dtype, op, 2, pads)
+            got = run_group_coalesced(g, sets, dtype, op, algo, pads)
             for b, k in enumerate(counts):
                 want = O.expected_allreduce([sets[r][b] for r in range(2)], dtype, op)
                 for r in range(2):
-                    assert same_bits(got[r][b], want, dtype), (dtype, counts, b, r)
+                    assert same_bits(got[r][b], want, dtype), (dtype, counts, algo, b, r)
     finally:
         for c in g:
             c.destroy()
