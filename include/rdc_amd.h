@@ -221,7 +221,7 @@ int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t t
  * slot) the one-shot schedule, then the launch shapes of the fastest, for
  * `bytes` of `dtype` on this node — mesh: role split, then grid, then
  * tiles per reduce block; ring: grid, then tiles per block (a granularity, so
- * the chosen tiles scale with later buffers' sizes) — `reps` Sum allreduces each on a scratch
+ * the chosen tiles scale with later buffers' sizes) — `reps` Max allreduces of synthetic data each on a scratch
  * buffer, in 3 rounds per candidate taken round-robin over each stage; agree
  * on the per-round times with a MAX allreduce over `comm` (identical on every
  * rank, so every rank keeps the same winner); a candidate's time is the median

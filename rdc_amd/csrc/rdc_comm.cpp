@@ -1279,7 +1279,11 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
         constexpr int kStageMax = 16;
         hip_check(hipMallocAsync(reinterpret_cast<void**>(&dms), sizeof(double) * kStageMax * kTuneRounds, stream),
                   "autotune times");
-        hip_check(hipMemsetAsync(buf, 0, count * esz, stream), "autotune memset");
+        // synthetic full-entropy values, reduced with Max so they stay that way:
+        // the timing depends on the data (1 GiB ring, n = 2 on one GPU: zeros
+        // 1.42 ms, random 1.51 ms under Max or Sum; tools/data_sensitivity.py,
+        // profiles/r03/data_sensitivity_*), and Sum would drive them to inf
+        DeviceFill(buf, count, dtype, 0x5EED7E57ull, rank_, stream);
         hip_check(hipEventCreate(&e0), "event");
         hip_check(hipEventCreate(&e1), "event");
         // a candidate = schedule + shape, installed where PickAlgo / ShapeFor
@@ -1299,9 +1303,9 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
         // one round of one candidate: ms per allreduce on this rank
         auto measure = [&](const TuneCand& c, bool warm) {
             set_shape(c);
-            if (warm) Allreduce(buf, count, dtype, RDC_OP_SUM, stream, RDC_ALGO_AUTO);  // first-use work
+            if (warm) Allreduce(buf, count, dtype, RDC_OP_MAX, stream, RDC_ALGO_AUTO);  // first-use work
             hip_check(hipEventRecord(e0, stream), "record");
-            for (int i = 0; i < reps; ++i) Allreduce(buf, count, dtype, RDC_OP_SUM, stream, RDC_ALGO_AUTO);
+            for (int i = 0; i < reps; ++i) Allreduce(buf, count, dtype, RDC_OP_MAX, stream, RDC_ALGO_AUTO);
             hip_check(hipEventRecord(e1, stream), "record");
             hip_check(hipEventSynchronize(e1), "sync");
             float ms = 0;

@@ -172,7 +172,7 @@ public:
     // for `bytes` of `dtype` (mesh: role split, then grid, then tiles per
     // reduce block; ring: grid, then tiles per block — granularity that scales
     // with the buffer), `reps`
-    // Sum allreduces each on a scratch buffer, agree on the per-candidate
+    // Max allreduces of synthetic data each on a scratch buffer, agree on the per-candidate
     // times by a MAX allreduce over this communicator (every rank gets the
     // same bits, so the same winner), and keep the fastest for allreduces of
     // the same size class ([2^k, 2^(k+1)) bytes: tuned_algo_ / tuned_; Tune

@@ -8,7 +8,7 @@ namespace rdc_amd {
 
 __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
     const uint32_t seq = launch_seq(a);
-    bcast_body(a, seq);
+    if (!channel_failed(a)) bcast_body(a, seq);
     launch_done(a, seq);
 }
 
@@ -64,7 +64,7 @@ __device__ void allgather_body(const CollArgs& a, uint32_t seq) {
 
 __global__ __launch_bounds__(kBlock) void k_allgather(CollArgs a) {
     const uint32_t seq = launch_seq(a);
-    allgather_body(a, seq);
+    if (!channel_failed(a)) allgather_body(a, seq);
     launch_done(a, seq);
 }
 

@@ -46,6 +46,20 @@ __device__ __forceinline__ uint32_t launch_seq(const CollArgs& a) {
     const uint32_t done = __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return ((done + 1u) & kSeqMask) | (a.tag << kSeqBits);
 }
+// A channel that failed (a peer missed a hand-off, an order violation) is
+// unusable: later launches move nothing — in particular they push nothing
+// into peers' scratch, where a peer still inside the failed launch would take
+// a later launch's flags (>= its seq) for its own — and only advance the
+// counters.  The host raises the recorded error at its next check.
+// (Block-uniform: one load by thread 0, shared with the block.)
+__device__ __forceinline__ bool channel_failed(const CollArgs& a) {
+    __shared__ int s_failed;
+    if (threadIdx.x == 0) s_failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    __syncthreads();
+    const bool f = s_failed != 0;
+    __syncthreads();
+    return f;
+}
 __device__ __forceinline__ uint32_t prev_kind(const CollArgs& a) {
     return __hip_atomic_load(a.launch_kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -771,7 +785,7 @@ template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
     const uint64_t t0 = wall_clock64();
     const uint32_t seq = launch_seq(a);
-    mesh_body<OP, T, NMAX>(a, seq);
+    if (!channel_failed(a)) mesh_body<OP, T, NMAX>(a, seq);
     trace_block(a, t0);
     launch_done(a, seq);
 }
@@ -779,14 +793,14 @@ __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_oneshot(CollArgs a) {
     const uint32_t seq = launch_seq(a);
-    oneshot_body<OP, T, NMAX>(a, seq);
+    if (!channel_failed(a)) oneshot_body<OP, T, NMAX>(a, seq);
     launch_done(a, seq);
 }
 
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_tree(CollArgs a) {
     const uint32_t seq = launch_seq(a);
-    oneshot_body<OP, T, NMAX, true>(a, seq);
+    if (!channel_failed(a)) oneshot_body<OP, T, NMAX, true>(a, seq);
     launch_done(a, seq);
 }
 
@@ -794,7 +808,7 @@ template <int OP, typename T>
 __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
     const uint64_t t0 = wall_clock64();
     const uint32_t seq = launch_seq(a);
-    ring_body<OP, T>(a, seq);
+    if (!channel_failed(a)) ring_body<OP, T>(a, seq);
     trace_block(a, t0);
     launch_done(a, seq);
 }

@@ -133,6 +133,8 @@ def main():
             torch.cuda.synchronize()
             order = [(comm, a), (other, b)] if rank == 0 else [(other, b), (comm, a)]
             err = ""
+            import time as _time
+            t_start = _time.time()
             try:
                 for cm, t in order:
                     check_call(_LIB.RdcCommAllreduceEx(cm.handle, ctypes.c_void_p(t.data_ptr()), count, 6, 2,
@@ -141,6 +143,7 @@ def main():
             except Exception as e:  # noqa: BLE001 - the expected outcome
                 err = str(e)
             info["error"] = err
+            info["seconds"] = round(_time.time() - t_start, 3)
             open(os.path.join(outdir, "case%d_rank%d.json" % (i, rank)), "w").write(json.dumps(info))
             print("rank %d case %d ok" % (rank, i), flush=True)
             # the channel is unusable now: leave without finalizing collectives

@@ -488,10 +488,10 @@ def test_mp_shared_channel_order_violation_is_an_error(world, algo):
         pytest.skip("no GPU")
     cases = [{"count": 100003, "dtype": 6, "op": 2, "kind": "order_violation", "algo": algo}]
     tmp = run_mp(world, cases, timeout=120, env_extra={"RDC_TIMEOUT": "30"})
-    for r in range(world):
-        info = json.load(open(os.path.join(tmp, "case0_rank%d.json" % r)))
-        assert info["shares"] == [1, 1], info
-        assert "another communicator" in info["error"] and "different orders" in info["error"], info
+    infos = [json.load(open(os.path.join(tmp, "case0_rank%d.json" % r))) for r in range(world)]
+    for info in infos:
+        assert info["shares"] == [1, 1], infos
+        assert "another communicator" in info["error"] and "different orders" in info["error"], infos
 
 
 def test_mp_full_size_cfg2():
