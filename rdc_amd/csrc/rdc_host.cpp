@@ -65,10 +65,7 @@ void HostPath::SpinEvent(hipEvent_t e, const char* what) {
 }
 
 HostPath::HostPath(int device, size_t zc_max)
-    : device_(device),
-      zc_max_(zc_max),
-      pool_(std::max(0, env_int("RDC_HOST_THREADS", 4) - 1)),
-      out_pool_(std::max(0, env_int("RDC_HOST_THREADS", 4) - 1)) {
+    : device_(device), zc_max_(zc_max), pool_(std::max(0, env_int("RDC_HOST_THREADS", 4) - 1)) {
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "stream");
     hip_check(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking), "stream");
@@ -89,10 +86,7 @@ HostPath::~HostPath() {
         if (pin_in_[i]) (void)hipHostFree(pin_in_[i]);
         (void)hipEventDestroy(in_done_[i]);
     }
-    for (int i = 0; i < kOutSlots; ++i)
-        if (pin_out_[i]) (void)hipHostFree(pin_out_[i]);
     for (hipEvent_t e : ar_done_) (void)hipEventDestroy(e);
-    for (hipEvent_t e : out_done_) (void)hipEventDestroy(e);
     if (pin_small_) (void)hipHostFree(pin_small_);
     if (small_done_) (void)hipEventDestroy(small_done_);
     if (dev_small_) (void)hipFree(dev_small_);
@@ -118,24 +112,11 @@ void HostPath::Reserve(size_t piece_bytes, size_t total_bytes, int pieces, hipSt
             if (pin_in_[i]) (void)hipHostFree(pin_in_[i]);
             pin_in_[i] = nullptr;
         }
-        for (int i = 0; i < kOutSlots; ++i) {
-            if (pin_out_[i]) (void)hipHostFree(pin_out_[i]);
-            pin_out_[i] = nullptr;
-        }
         slot_bytes_ = 0;
         for (int i = 0; i < kSlots; ++i)
             hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_in_[i]), piece_bytes, hipHostMallocDefault),
                       "hipHostMalloc");
-        // output slots only for pipelined calls (a one-piece call copies straight back)
-        if (pieces > 1)
-            for (int i = 0; i < kOutSlots; ++i)
-                hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_out_[i]), piece_bytes, hipHostMallocDefault),
-                          "hipHostMalloc");
         slot_bytes_ = piece_bytes;
-    } else if (pieces > 1 && !pin_out_[0]) {
-        for (int i = 0; i < kOutSlots; ++i)
-            hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin_out_[i]), slot_bytes_, hipHostMallocDefault),
-                      "hipHostMalloc");
     }
     if (total_bytes > dev_bytes_) {
         if (dev_) {
@@ -151,29 +132,23 @@ void HostPath::Reserve(size_t piece_bytes, size_t total_bytes, int pieces, hipSt
         hipEvent_t e;
         hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
         ar_done_.push_back(e);
-        hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
-        out_done_.push_back(e);
     }
 }
 
-void HostPath::Copy(CopyPool& pool, char* dst, const char* src, size_t bytes) {
+void HostPath::Copy(char* dst, const char* src, size_t bytes) {
     if (bytes < kParallelMin) {
         memcpy(dst, src, bytes);
         return;
     }
     const int parts = (int)std::min<size_t>(16, bytes / (kParallelMin / 2));
     const size_t per = (bytes / (size_t)parts + 4095) & ~(size_t)4095;
-    pool.Run(parts, [&](int i) {
+    pool_.Run(parts, [&](int i) {
         const size_t lo = (size_t)i * per;
         if (lo >= bytes) return;
         memcpy(dst + lo, src + lo, std::min(per, bytes - lo));
     });
 }
 
-// The drain thread: piece by piece, wait (spinning: the wait is short and a
-// blocking one pays a wake-up) until the piece's D2H into its output slot is
-// done, copy the slices into the user's buffer with its own copy pool, and
-// free the slot (drained_, which the caller waits on before reusing it).
 void HostPath::DrainLoop() {
     for (;;) {
         Drain d;
@@ -189,14 +164,17 @@ void HostPath::DrainLoop() {
         try {
             hip_check(hipSetDevice(device_), "hipSetDevice");
             const double t0 = tracing() ? trace_now() : 0;
-            SpinEvent(d.ready, "wait D2H");
+            // blocking waits here: a spinning drain thread competes with the
+            // copy threads for cores and measured no faster (2-16 MiB)
+            hip_check(hipEventSynchronize(d.ready), "wait allreduce");
             const double t1 = tracing() ? trace_now() : 0;
-            const char* slot = pin_out_[d.oslot];
             for (int q = 0; q < d.nslice; ++q)
-                if (d.len[q]) Copy(out_pool_, dst + d.off[q], slot + d.pos[q], d.len[q]);
+                if (d.len[q])
+                    hip_check(hipMemcpyAsync(dst + d.off[q], dev_ + d.off[q], d.len[q], hipMemcpyDeviceToHost, d2h_),
+                              "D2H");
+            hip_check(hipStreamSynchronize(d2h_), "D2H sync");
             if (tracing())
-                fprintf(stderr, "[host %.3f] drain: waited D2H %.3f ms, copy-out %.3f ms\n", t1, t1 - t0,
-                        trace_now() - t1);
+                fprintf(stderr, "[host %.3f] drain: waited AR %.3f ms, D2H %.3f ms\n", t1, t1 - t0, trace_now() - t1);
         } catch (const std::exception& e) {
             err = e.what();
         }
@@ -314,11 +292,9 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
         for (int k = 0; k < K; ++k) {
             const int slot = k % kSlots;
             Drain d;
-            d.ready = out_done_[(size_t)k];
+            d.ready = ar_done_[(size_t)k];
             d.nslice = n;
-            d.oslot = k % kOutSlots;
-            uint64_t* pos = d.pos;
-            uint64_t bytes = 0;
+            uint64_t pos[RDC_MAX_RANKS], bytes = 0;
             for (int q = 0; q < n; ++q) {
                 const uint64_t lo = (uint64_t)cb[q] * esz + (uint64_t)k * sl;
                 const uint64_t hi = std::min<uint64_t>((uint64_t)ce[q] * esz, lo + sl);
@@ -344,19 +320,7 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
             hip_check(hipEventRecord(in_done_[slot], h2d_), "record");
             hip_check(hipStreamWaitEvent(comm_stream, in_done_[slot], 0), "wait");
             c->AllreduceRanges(dev_, d.off, d.len, dtype, op, comm_stream);
-            hip_check(hipEventRecord(ar_done_[(size_t)k], comm_stream), "record");
-            // the output slot's previous piece has been copied out
-            if (k >= kOutSlots) {
-                std::unique_lock<std::mutex> lk(dmu_);
-                ddone_cv_.wait(lk, [&] { return (int)drained_ > k - kOutSlots; });
-            }
-            hip_check(hipStreamWaitEvent(d2h_, ar_done_[(size_t)k], 0), "wait");
-            for (int q = 0; q < n; ++q)
-                if (d.len[q])
-                    hip_check(hipMemcpyAsync(pin_out_[d.oslot] + pos[q], dev_ + d.off[q], d.len[q],
-                                             hipMemcpyDeviceToHost, d2h_),
-                              "D2H");
-            hip_check(hipEventRecord(d.ready, d2h_), "record");
+            hip_check(hipEventRecord(d.ready, comm_stream), "record");
             {
                 std::lock_guard<std::mutex> lk(dmu_);
                 queue_.push_back(d);

@@ -182,3 +182,41 @@ def test_launcher_stops_all_on_failure():
     the launcher returns 3 instead of hanging."""
     p = launch(3, "fail", timeout=120)
     assert p.returncode == 3, p.stdout + p.stderr
+
+
+BUDGET = r'''
+import os, sys, time, json
+sys.path.insert(0, os.environ["ROOT"])
+import torch, torch.distributed as dist
+dist.init_process_group("gloo")
+import bench
+rank = dist.get_rank()
+b = bench.Budget(1.0, dist, torch, dist.get_world_size())
+out = []
+for step in range(4):
+    time.sleep(0.05 * (rank + 1) * (step + 1))   # rank 1 falls behind more each step
+    out.append(round(b.left(), 6))
+print("LEFT", rank, json.dumps(out), flush=True)
+'''
+
+
+def test_bench_extras_budget_agreed_across_ranks():
+    """bench.py's extras budget: every rank computes the same time left (the
+    slowest rank's elapsed time, MAX over the CPU group), so every rank takes
+    the same skip decision even when one rank runs behind."""
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = clean_env()
+        env.update(RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROOT=ROOT)
+        procs.append(subprocess.Popen([sys.executable, "-c", BUDGET], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    import json
+    lefts = []
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o
+        line = [l for l in o.splitlines() if l.startswith("LEFT")][0]
+        lefts.append(json.loads(line.split(" ", 2)[2]))
+    assert lefts[0] == lefts[1], lefts
+    assert lefts[0][-1] < 0 < lefts[0][0] and lefts[0] == sorted(lefts[0], reverse=True), lefts
