@@ -851,17 +851,23 @@ void Communicator::AllreduceRanges(void* buf, const uint64_t* off, const uint64_
                                     std::to_string(op) + ")");
     if (n_ == 1) return;
     const size_t esz = rdc_dtype_size(dtype);
-    uint64_t total = 0;
+    uint64_t total = 0, sum = 0, first = ~0ull;
     for (int c = 0; c < n_; ++c) {
         if (off[c] % esz || len[c] % esz) throw std::invalid_argument("rdc: range not element-aligned");
-        if (len[c]) total = std::max<uint64_t>(total, off[c] + len[c]);
+        if (len[c]) {
+            total = std::max<uint64_t>(total, off[c] + len[c]);
+            first = std::min<uint64_t>(first, off[c]);
+            sum += len[c];
+        }
     }
     if (total == 0) return;
     hip_check(hipSetDevice(device_), "hipSetDevice");
     ChannelCall call(ch_.get(), stream);
-    // a piece's ranges are not one contiguous span: never one-shot (it pushes [0, total))
-    int algo = PickAlgo(RDC_ALGO_AUTO);
-    if (algo == RDC_ALGO_ONESHOT) algo = RDC_ALGO_MESH;
+    // the one-shot pushes all of [0, total): only for ranges that tile it
+    // (disjoint chunk ranges starting at 0 with no gap); otherwise the mesh
+    const bool contiguous = first == 0 && sum == total;
+    int algo = contiguous ? PickAlgo(RDC_ALGO_AUTO, total) : PickAlgo(RDC_ALGO_AUTO);
+    if (algo == RDC_ALGO_ONESHOT && !contiguous) algo = RDC_ALGO_MESH;
     LaunchRanges(ks, static_cast<char*>(buf), off, len, total, esz, algo, stream);
 }
 

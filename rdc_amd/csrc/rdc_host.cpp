@@ -253,12 +253,15 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
 
     int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
     SplitRanges((int64_t)count, n, cb, ce);
-    const uint64_t maxlen = (uint64_t)(ce[0] - cb[0]) * esz;  // the first chunk is never shorter
-    // slice length per chunk and piece: a multiple of 4 KiB (hence of esz)
+    // pieces are contiguous byte ranges of the buffer, a multiple of 4 KiB
+    // (hence of esz) long: one copy in, one H2D, one D2H each (the first
+    // version cut piece k from the k-th slice of EVERY chunk — n copies each
+    // way per piece).  Every element is still folded in its own Split chunk's
+    // ring order: a piece's allreduce gets the chunk ranges it intersects.
     const uint64_t K0 = S <= kOnePieceMax ? 1 : std::max<uint64_t>(1, (S + piece_target() - 1) / piece_target());
-    const uint64_t sl = std::max<uint64_t>(4096, ((maxlen + K0 - 1) / K0 + 4095) & ~(uint64_t)4095);
-    const int K = (int)((maxlen + sl - 1) / sl);
-    Reserve((size_t)sl * (size_t)n, S, K, comm_stream);
+    const uint64_t sl = std::max<uint64_t>(4096, ((S + K0 - 1) / K0 + 4095) & ~(uint64_t)4095);
+    const int K = (int)((S + sl - 1) / sl);
+    Reserve((size_t)sl, S, K, comm_stream);
     if (K == 1) {
         // one piece (up to the piece target): nothing to overlap, so no drain
         // thread hand-off either — the slices of one piece are the chunks in
@@ -293,33 +296,30 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
             const int slot = k % kSlots;
             Drain d;
             d.ready = ar_done_[(size_t)k];
-            d.nslice = n;
-            uint64_t pos[RDC_MAX_RANKS], bytes = 0;
+            d.nslice = 1;
+            const uint64_t lo = (uint64_t)k * sl, hi = std::min<uint64_t>(S, lo + sl), bytes = hi - lo;
+            d.off[0] = lo;
+            d.len[0] = bytes;
+            // the piece's intersection with every Split chunk, relative to lo
+            uint64_t roff[RDC_MAX_RANKS], rlen[RDC_MAX_RANKS];
             for (int q = 0; q < n; ++q) {
-                const uint64_t lo = (uint64_t)cb[q] * esz + (uint64_t)k * sl;
-                const uint64_t hi = std::min<uint64_t>((uint64_t)ce[q] * esz, lo + sl);
-                pos[q] = bytes;
-                d.off[q] = hi > lo ? lo : 0;
-                d.len[q] = hi > lo ? hi - lo : 0;
-                bytes += d.len[q];
+                const uint64_t a = std::max<uint64_t>(lo, (uint64_t)cb[q] * esz);
+                const uint64_t b = std::min<uint64_t>(hi, (uint64_t)ce[q] * esz);
+                roff[q] = b > a ? a - lo : 0;
+                rlen[q] = b > a ? b - a : 0;
             }
             // the slot's previous H2D has been consumed before we overwrite it
             const double t0 = tracing() ? trace_now() : 0;
             if (k >= kSlots) hip_check(hipEventSynchronize(in_done_[slot]), "wait H2D slot");
             const double t1 = tracing() ? trace_now() : 0;
-            for (int q = 0; q < n; ++q)
-                if (d.len[q]) Copy(pin_in_[slot] + pos[q], h + d.off[q], d.len[q]);
+            Copy(pin_in_[slot], h + lo, bytes);
             if (tracing())
                 fprintf(stderr, "[host %.3f] piece %d: slot wait %.3f ms, copy-in %.3f ms (%llu B)\n", t0, k, t1 - t0,
                         trace_now() - t1, (unsigned long long)bytes);
-            for (int q = 0; q < n; ++q)
-                if (d.len[q])
-                    hip_check(hipMemcpyAsync(dev_ + d.off[q], pin_in_[slot] + pos[q], d.len[q],
-                                             hipMemcpyHostToDevice, h2d_),
-                              "H2D");
+            hip_check(hipMemcpyAsync(dev_ + lo, pin_in_[slot], bytes, hipMemcpyHostToDevice, h2d_), "H2D");
             hip_check(hipEventRecord(in_done_[slot], h2d_), "record");
             hip_check(hipStreamWaitEvent(comm_stream, in_done_[slot], 0), "wait");
-            c->AllreduceRanges(dev_, d.off, d.len, dtype, op, comm_stream);
+            c->AllreduceRanges(dev_ + lo, roff, rlen, dtype, op, comm_stream);
             hip_check(hipEventRecord(d.ready, comm_stream), "record");
             {
                 std::lock_guard<std::mutex> lk(dmu_);

@@ -1,10 +1,11 @@
 // Host-resident allreduce (rdc's own setting: buffers begin and end in host
 // memory — rdc/core.py:172-217, test/allreduce.cc), pipelined over PCIe.
 //
-// The buffer's Split chunks (include/utils/utils.h:59-70) are cut into K
-// pieces; piece k holds the k-th slice of EVERY chunk, so each piece is a
-// balanced allreduce in its own right and every element is still folded in
-// its chunk's ring order (bit-identical to one whole-buffer allreduce).
+// The buffer is cut into K contiguous pieces (RDC_HOST_PIECE_BYTES); piece k's
+// allreduce gets the Split chunk ranges (include/utils/utils.h:59-70) it
+// intersects, so every element is still folded in its own chunk's ring order
+// (bit-identical to one whole-buffer allreduce) while each piece moves as one
+// copy in, one H2D and one D2H.
 // Per piece, on three streams:
 //   host threads memcpy the slices into a pinned slot -> H2D DMA (copy stream)
 //   -> allreduce of the slices on the communicator's stream

@@ -260,10 +260,11 @@ __device__ __forceinline__ int unit_first(const PackUnit* u, int nunits, uint64_
 }
 
 // f(user pointer, packed offset, bytes) for every unit piece of packed [p0, p1)
+// (first: the first unit of the range when the caller already knows it)
 template <typename F>
-__device__ __forceinline__ void for_unit_pieces(const CollArgs& a, uint64_t p0, uint64_t p1, F&& f) {
+__device__ __forceinline__ void for_unit_pieces(const CollArgs& a, uint64_t p0, uint64_t p1, F&& f, int first = -1) {
     const PackUnit* u = static_cast<const PackUnit*>(a.units);
-    for (int i = unit_first(u, a.nunits, p0); i < a.nunits; ++i) {
+    for (int i = first >= 0 ? first : unit_first(u, a.nunits, p0); i < a.nunits; ++i) {
         const uint64_t up = u[i].packed, ul = u[i].len;
         if (up >= p1) break;
         const uint64_t lo = up > p0 ? up : p0;
@@ -402,13 +403,41 @@ __device__ void block_reduce_into(char* own, const char* recv, uint64_t len) {
 // off[c], bytes) pieces: one piece of the buffer, or — coalesced lists
 // (a.units) — the unit pieces the packed range covers (rdc_plan.h
 // PlanCoalesced: user slices and scratch images are congruent mod 16).
+// The ring touches every (chunk, tile) range twice — received at one step,
+// sent on at the next, or sent in the reduce-scatter and received in the
+// allgather — so a block remembers each chunk's first unit for its current
+// tile (UnitCache, block-shared) and searches the table once per range.
+struct UnitCache {
+    uint64_t toff[RDC_MAX_RANKS];
+    int first[RDC_MAX_RANKS];
+};
+__device__ __forceinline__ void unit_cache_reset(UnitCache& uc) {
+    if (threadIdx.x < RDC_MAX_RANKS) uc.toff[threadIdx.x] = ~0ull;
+    __syncthreads();
+}
 template <typename F>
-__device__ __forceinline__ void chunk_pieces(const CollArgs& a, int c, uint64_t toff, uint64_t tlen, F&& f) {
-    if (a.units)
+__device__ __forceinline__ void chunk_pieces(const CollArgs& a, int c, uint64_t toff, uint64_t tlen, F&& f,
+                                             UnitCache* uc = nullptr) {
+    if (a.units) {
+        int first = -1;
+        if (uc) {
+            if (uc->toff[c] == toff) {
+                first = uc->first[c];
+            } else {
+                first = unit_first(static_cast<const PackUnit*>(a.units), a.nunits, a.off[c] + toff);
+                __syncthreads();  // every thread has read the old entry
+                if (threadIdx.x == 0) {
+                    uc->toff[c] = toff;
+                    uc->first[c] = first;
+                }
+                __syncthreads();
+            }
+        }
         for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen,
-                        [&](char* usr, uint64_t p, uint64_t l) { f(usr, p - a.off[c], l); });
-    else
+                        [&](char* usr, uint64_t p, uint64_t l) { f(usr, p - a.off[c], l); }, first);
+    } else {
         f(a.user + a.off[c] + toff, toff, tlen);
+    }
 }
 
 template <int OP, typename T>
@@ -418,6 +447,9 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     if (prev_kind(a) == RDC_KIND_ONESHOT && !gate_on_peers(a, seq, prev, 1, ab, RDC_KERR_TIMEOUT_RING)) return;
     __shared__ uint32_t* s_flag[1];
+    __shared__ UnitCache s_units;
+    UnitCache* ucp = a.units ? &s_units : nullptr;
+    if (ucp) unit_cache_reset(s_units);
     int tmax = 0;
     for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
     for (int t = blockIdx.x; t < tmax; t += gridDim.x) {
@@ -432,7 +464,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
                 char* dst = a.rs[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs];
                 chunk_pieces(a, cs, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
                     block_copy<kDstPeer>(dst + co, usr, l);
-                });
+                }, ucp);
                 block_publish1(a.flags[prev] + (uint64_t)j * a.max_tiles + t, seq, a.uc);
             }
             const int cr = (r + 2 + j) % n;
@@ -445,7 +477,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
                 const char* src = a.rs[r] + (uint64_t)j * a.slot_bytes + a.mis[cr];
                 chunk_pieces(a, cr, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
                     block_reduce_into<OP, T>(usr, src + co, l);
-                });
+                }, ucp);
                 __syncthreads();
             }
         }
@@ -459,7 +491,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
                 char* dst = a.ag[prev] + (uint64_t)j * a.slot_bytes + a.mis[cs];
                 chunk_pieces(a, cs, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
                     block_copy<kDstPeer>(dst + co, usr, l);
-                });
+                }, ucp);
                 block_publish1(a.flags[prev] + (uint64_t)(n + j) * a.max_tiles + t, seq, a.uc);
             }
             const int cr = (r + 1 + j) % n;
@@ -472,7 +504,7 @@ __device__ void ring_body(const CollArgs& a, uint32_t seq) {
                 const char* src = a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr];
                 chunk_pieces(a, cr, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
                     block_copy<kDstLocal>(usr, src + co, l);
-                });
+                }, ucp);
                 __syncthreads();
             }
         }

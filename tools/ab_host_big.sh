@@ -3,6 +3,7 @@
 # processes on one GPU): ab_old/librdc_amd.so (pageable D2H from a drain
 # thread) vs ab_old/librdc_amd_new.so (D2H into pinned output slots, copy-out
 # by a pool), alternated on one box; then one traced call of the new build.
+# (Round 3, second A/B: old = slices of every chunk per piece, new = contiguous pieces.)
 out=${1:-gpurun_out/ab_host_big}
 mkdir -p $out
 port=30200
