@@ -296,6 +296,10 @@ int RdcPlanResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu)
  * dst/src hold >= 16 ints.  Returns n-1, or -1 on bad arguments. */
 int RdcPlanTree(int n, int* dst, int* src);
 int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4);
+/* The host-buffer pipeline's contiguous pieces for `bytes` (RDC_HOST_PIECE_BYTES,
+ * RDC_HOST_PIECE_RAMP): bounds[0..*out_n) = {0, ..., bytes}, piece k = [bounds[k],
+ * bounds[k+1]) (one piece up to 16 MiB).  Writes at most max_bounds entries. */
+int RdcPlanHostPieces(size_t bytes, uint64_t* bounds, int max_bounds, int* out_n);
 /* The automatic schedule for an allreduce of `bytes` over n ranks: returns
  * RDC_ALGO_ONESHOT (3), RDC_ALGO_RING (1, n = 2 beyond the one-shot) or
  * RDC_ALGO_MESH (2) (negative on bad arguments).

@@ -75,6 +75,7 @@ def _load():
         "RdcMemcpy": (i, [vp, vp, sz]),
         "RdcPlanLayout": (i, [i, sz, ctypes.POINTER(u64)]),
         "RdcPlanAutoAlgo": (i, [i, sz, sz, sz]),
+        "RdcPlanHostPieces": (i, [sz, ctypes.POINTER(ctypes.c_uint64), i, ctypes.POINTER(i)]),
         "RdcPlanAllreduce": (i, [i, sz, i, sz, i, sz, i, ctypes.POINTER(u64), i, ctypes.POINTER(ctypes.c_int)]),
         "RdcAllreduceCoalesced": (i, [pvp, ctypes.POINTER(sz), i, i, i]),
         "RdcAllreduceCoalescedOn": (i, [vp, pvp, ctypes.POINTER(sz), i, i, i]),

@@ -718,6 +718,15 @@ int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_by
     return rc != 0 ? rc : algo;
 }
 
+int RdcPlanHostPieces(size_t bytes, uint64_t* bounds, int max_bounds, int* out_n) {
+    return guard([&] {
+        if (!bounds || !out_n || max_bounds < 2) throw std::invalid_argument("rdc: bad argument");
+        const std::vector<uint64_t> b = rdc_amd::HostPieceBounds(bytes);
+        *out_n = (int)b.size();
+        for (size_t i = 0; i < b.size() && i < (size_t)max_bounds; ++i) bounds[i] = b[i];
+    });
+}
+
 int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int algo, size_t tile_bytes,
                      int max_blocks, uint64_t* out, int max_pieces, int* out_pieces) {
     return guard([&] {

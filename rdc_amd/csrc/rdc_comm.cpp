@@ -105,14 +105,15 @@ void PlanKey(const CommConfig& c, uint64_t tune_hash, uint64_t (&k)[kPlanKeys]) 
                                    (uint64_t)c.fuse_bytes_direct, (uint64_t)c.bcast_split_bytes,
                                    (uint64_t)c.mesh_split.s16, (uint64_t)c.mesh_split.r16, (uint64_t)c.ring_mincount,
                                    (uint64_t)c.scratch_bytes, (uint64_t)SmallService::Enabled(),
-                                   (uint64_t)SmallService::ShareMax(), (uint64_t)HostPieceBytes(), tune_hash};
+                                   (uint64_t)SmallService::ShareMax(),
+                                   (uint64_t)HostPieceBytes() | ((uint64_t)HostPieceRamp() << 63), tune_hash};
     memcpy(k, v, sizeof(v));
 }
 const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_ONESHOT_BYTES",
                                         "RDC_FUSE_BYTES", "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT",
                                         "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "RDC_MESH_SPLIT",
                                         "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES", "RDC_HOST_SERVICE",
-                                        "RDC_HOST_SERVICE_SHARE_MAX", "RDC_HOST_PIECE_BYTES",
+                                        "RDC_HOST_SERVICE_SHARE_MAX", "RDC_HOST_PIECE_BYTES / RDC_HOST_PIECE_RAMP",
                                         "RDC_TUNE_FILE (set or not)"};
 
 // Autotune results kept across runs (RDC_TUNE_FILE): one line per winner,

@@ -52,6 +52,51 @@ size_t HostPieceBytes() {
     return v;
 }
 
+bool HostPieceRamp() {
+    static const bool v = [] {
+        const char* e = getenv("RDC_HOST_PIECE_RAMP");
+        return !(e && *e && atoi(e) == 0);
+    }();
+    return v;
+}
+
+// Contiguous pieces of about HostPieceBytes() P (multiples of 4 KiB).  With
+// the ramp (RDC_HOST_PIECE_RAMP, default on; buffers of at least 4 P) the
+// first three pieces are P/8, P/4, P/2 and the last three P/2, P/4, P/8: the
+// first H2D starts after an eighth of a piece's copy-in and the last D2H
+// moves an eighth of a piece, so the pipeline fills and drains in small steps.
+std::vector<uint64_t> HostPieceBounds(uint64_t S) {
+    const uint64_t P = piece_target();
+    auto up4k = [](uint64_t x) { return std::max<uint64_t>(4096, (x + 4095) & ~(uint64_t)4095); };
+    std::vector<uint64_t> b{0};
+    if (S <= kOnePieceMax) {
+        b.push_back(S);
+        return b;
+    }
+    uint64_t ramp[3] = {0, 0, 0}, ramp_sum = 0;
+    if (HostPieceRamp() && S >= 4 * P) {
+        for (int i = 0; i < 3; ++i) {
+            ramp[i] = up4k(P >> (3 - i));  // P/8, P/4, P/2
+            ramp_sum += ramp[i];
+        }
+    }
+    for (int i = 0; i < 3; ++i)
+        if (ramp[i]) b.push_back(b.back() + ramp[i]);
+    // the tail ramp starts on a 4 KiB boundary; the last piece takes the rest
+    const uint64_t mid_end = ramp_sum ? (S - ramp_sum) & ~(uint64_t)4095 : S;
+    const uint64_t mid = mid_end - b.back();
+    const uint64_t K0 = std::max<uint64_t>(1, (mid + P - 1) / P);
+    const uint64_t sl = up4k((mid + K0 - 1) / K0);
+    for (uint64_t x = b.back() + sl; x < mid_end; x += sl) b.push_back(x);
+    b.push_back(mid_end);
+    if (ramp_sum) {
+        b.push_back(b.back() + ramp[2]);
+        b.push_back(b.back() + ramp[1]);
+        b.push_back(S);
+    }
+    return b;  // b.back() == S
+}
+
 // ---------------------------------------------------------------- HostPath --
 // wait for an event by polling it: a blocking synchronisation may sleep and
 // pay a wake-up on every piece
@@ -258,9 +303,10 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
     // version cut piece k from the k-th slice of EVERY chunk — n copies each
     // way per piece).  Every element is still folded in its own Split chunk's
     // ring order: a piece's allreduce gets the chunk ranges it intersects.
-    const uint64_t K0 = S <= kOnePieceMax ? 1 : std::max<uint64_t>(1, (S + piece_target() - 1) / piece_target());
-    const uint64_t sl = std::max<uint64_t>(4096, ((S + K0 - 1) / K0 + 4095) & ~(uint64_t)4095);
-    const int K = (int)((S + sl - 1) / sl);
+    const std::vector<uint64_t> bounds = HostPieceBounds(S);
+    const int K = (int)bounds.size() - 1;
+    uint64_t sl = 0;  // the largest piece: the pinned slot size
+    for (int k = 0; k < K; ++k) sl = std::max<uint64_t>(sl, bounds[(size_t)k + 1] - bounds[(size_t)k]);
     Reserve((size_t)sl, S, K, comm_stream);
     if (K == 1) {
         // one piece (up to the piece target): nothing to overlap, so no drain
@@ -297,7 +343,7 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
             Drain d;
             d.ready = ar_done_[(size_t)k];
             d.nslice = 1;
-            const uint64_t lo = (uint64_t)k * sl, hi = std::min<uint64_t>(S, lo + sl), bytes = hi - lo;
+            const uint64_t lo = bounds[(size_t)k], hi = bounds[(size_t)k + 1], bytes = hi - lo;
             d.off[0] = lo;
             d.len[0] = bytes;
             // the piece's intersection with every Split chunk, relative to lo

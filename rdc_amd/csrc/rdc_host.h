@@ -34,6 +34,10 @@ namespace rdc_amd {
 // buffer into the same pieces, so it is one of the plan keys agreed at
 // communicator creation (rdc_comm.cpp PlanKey)
 size_t HostPieceBytes();
+// RDC_HOST_PIECE_RAMP (default 1): small first and last pieces (a plan key too)
+bool HostPieceRamp();
+// the pipeline's piece boundaries for an S-byte host buffer: {0, ..., S}
+std::vector<uint64_t> HostPieceBounds(uint64_t S);
 
 // fixed pool of memcpy threads; Run(n, f) calls f(0..n-1) across the pool
 // and the caller, returning when all are done

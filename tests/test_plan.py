@@ -6,11 +6,13 @@ Split chunk (include/utils/utils.h:59-70) exactly once, in order, that every
 piece fits its scratch slot, tiles and flag indices stay in range, and the
 scratch placement is rank-independent (off % 16)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
 
 from oracle import oracle as O
+from tests.conftest import ROOT
 
 WORDS = 68
 
@@ -235,3 +237,57 @@ def test_auto_schedule_oneshot_vs_mesh():
     assert pick(2, 2 * M, M) == RING
     # never beyond half a slot, never for one rank; n = 2 beyond it: the ring
     assert pick(2, 1 << 40) == RING and pick(4, 1 << 40) == MESH and pick(1, 4096) == MESH
+
+
+PIECES = r'''
+import ctypes, json, sys
+sys.path.insert(0, sys.argv[1])
+from rdc_amd._lib import _LIB
+out = {}
+for S in [int(x) for x in sys.argv[2:]]:
+    b = (ctypes.c_uint64 * 4096)()
+    n = ctypes.c_int()
+    assert _LIB.RdcPlanHostPieces(S, b, 4096, ctypes.byref(n)) == 0
+    out[S] = list(b[:n.value])
+print(json.dumps(out))
+'''
+
+
+def host_pieces(sizes, env):
+    import json
+    import subprocess
+    import sys
+    e = dict(os.environ, **env)
+    p = subprocess.run([sys.executable, "-c", PIECES, ROOT] + [str(s) for s in sizes], env=e, capture_output=True,
+                       text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    return {int(k): v for k, v in json.loads(p.stdout).items()}
+
+
+@pytest.mark.parametrize("piece,ramp", [("8M", "1"), ("8M", "0"), ("4M", "1"), ("1M", "1")])
+def test_host_pipeline_pieces(piece, ramp):
+    """The host pipeline's contiguous pieces (rdc_host.cpp HostPieceBounds):
+    they tile [0, S) in order, interior bounds on 4 KiB (hence element)
+    boundaries, one piece up to 16 MiB, pieces of about RDC_HOST_PIECE_BYTES
+    P, and with the ramp the first and last three P/8, P/4, P/2 (mirrored)
+    for buffers of at least 4 P."""
+    P = {"8M": 8 << 20, "4M": 4 << 20, "1M": 1 << 20}[piece]
+    sizes = [16 << 20, (16 << 20) + 4, 64 << 20, (64 << 20) + 12, 100000012, 256 << 20, 3 * P + 4096 * 7 + 8]
+    got = host_pieces(sizes, {"RDC_HOST_PIECE_BYTES": str(P), "RDC_HOST_PIECE_RAMP": ramp})
+    for S in sizes:
+        b = got[S]
+        assert b[0] == 0 and b[-1] == S, (S, b[:4], b[-4:])
+        lens = [y - x for x, y in zip(b, b[1:])]
+        assert all(l > 0 for l in lens), (S, lens)
+        assert all(x % 4096 == 0 for x in b[1:-1]), S
+        if S <= 16 << 20:
+            assert lens == [S]
+            continue
+        ramped = ramp == "1" and S >= 4 * P
+        if ramped:
+            assert lens[:3] == [P // 8, P // 4, P // 2] and lens[-3:-1] == [P // 2, P // 4], (S, lens)
+            assert P // 8 <= lens[-1] < P // 8 + 4096, (S, lens)
+            mid = lens[3:-3]
+        else:
+            mid = lens
+        assert max(mid) <= P + 4096 and len(mid) == -(-(S - (sum(lens) - sum(mid))) // P), (S, P, mid)
