@@ -61,7 +61,9 @@ bool HostPieceRamp() {
 }
 
 // Contiguous pieces of about HostPieceBytes() P (multiples of 4 KiB).  With
-// the ramp (RDC_HOST_PIECE_RAMP, default on; buffers of at least 4 P) the
+// the ramp (RDC_HOST_PIECE_RAMP, default on; buffers of at least 8 P: n = 2
+// on one GPU, same box, alternating, 64 MiB 5.0 / 5.1 vs 5.7 / 6.1 ms without,
+// but 32 MiB 2.7 / 3.1 vs 2.5 / 2.5 ms — profiles/r03/host_ramp/) the
 // first three pieces are P/8, P/4, P/2 and the last three P/2, P/4, P/8: the
 // first H2D starts after an eighth of a piece's copy-in and the last D2H
 // moves an eighth of a piece, so the pipeline fills and drains in small steps.
@@ -74,7 +76,7 @@ std::vector<uint64_t> HostPieceBounds(uint64_t S) {
         return b;
     }
     uint64_t ramp[3] = {0, 0, 0}, ramp_sum = 0;
-    if (HostPieceRamp() && S >= 4 * P) {
+    if (HostPieceRamp() && S >= 8 * P) {
         for (int i = 0; i < 3; ++i) {
             ramp[i] = up4k(P >> (3 - i));  // P/8, P/4, P/2
             ramp_sum += ramp[i];

@@ -270,7 +270,7 @@ def test_host_pipeline_pieces(piece, ramp):
     they tile [0, S) in order, interior bounds on 4 KiB (hence element)
     boundaries, one piece up to 16 MiB, pieces of about RDC_HOST_PIECE_BYTES
     P, and with the ramp the first and last three P/8, P/4, P/2 (mirrored)
-    for buffers of at least 4 P."""
+    for buffers of at least 8 P."""
     P = {"8M": 8 << 20, "4M": 4 << 20, "1M": 1 << 20}[piece]
     sizes = [16 << 20, (16 << 20) + 4, 64 << 20, (64 << 20) + 12, 100000012, 256 << 20, 3 * P + 4096 * 7 + 8]
     got = host_pieces(sizes, {"RDC_HOST_PIECE_BYTES": str(P), "RDC_HOST_PIECE_RAMP": ramp})
@@ -283,7 +283,7 @@ def test_host_pipeline_pieces(piece, ramp):
         if S <= 16 << 20:
             assert lens == [S]
             continue
-        ramped = ramp == "1" and S >= 4 * P
+        ramped = ramp == "1" and S >= 8 * P
         if ramped:
             assert lens[:3] == [P // 8, P // 4, P // 2] and lens[-3:-1] == [P // 2, P // 4], (S, lens)
             assert P // 8 <= lens[-1] < P // 8 + 4096, (S, lens)
