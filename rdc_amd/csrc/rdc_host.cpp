@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <chrono>
@@ -182,9 +183,46 @@ void HostPath::Reserve(size_t piece_bytes, size_t total_bytes, int pieces, hipSt
     }
 }
 
-void HostPath::Copy(char* dst, const char* src, size_t bytes) {
+namespace {
+// Copies into a pinned staging slot are read by the DMA engine, never by
+// this CPU: streaming (non-temporal) stores skip the read-for-ownership of
+// every destination line and leave the caches to the source.  glibc's memcpy
+// only streams above a size threshold the pool's 512 KiB parts stay under.
+// RDC_HOST_NT_COPY=0 turns it off.
+bool nt_copy_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("RDC_HOST_NT_COPY");
+        return !(e && *e && atoi(e) == 0) && __builtin_cpu_supports("avx2");
+    }();
+    return v;
+}
+__attribute__((target("avx2"))) void nt_copy(char* dst, const char* src, size_t bytes) {
+    size_t head = (32 - ((uintptr_t)dst & 31)) & 31;
+    if (head > bytes) head = bytes;
+    memcpy(dst, src, head);
+    size_t i = head;
+    for (; i + 128 <= bytes; i += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
+        const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), d);
+    }
+    memcpy(dst + i, src + i, bytes - i);
+    // streaming stores are weakly ordered: drain them before this thread
+    // reports its part done (the DMA that follows must see every byte)
+    _mm_sfence();
+}
+}  // namespace
+
+void HostPath::Copy(char* dst, const char* src, size_t bytes, bool to_pinned) {
+    const bool nt = to_pinned && nt_copy_enabled();
     if (bytes < kParallelMin) {
-        memcpy(dst, src, bytes);
+        if (nt) nt_copy(dst, src, bytes);
+        else memcpy(dst, src, bytes);
         return;
     }
     const int parts = (int)std::min<size_t>(16, bytes / (kParallelMin / 2));
@@ -192,7 +230,8 @@ void HostPath::Copy(char* dst, const char* src, size_t bytes) {
     pool_.Run(parts, [&](int i) {
         const size_t lo = (size_t)i * per;
         if (lo >= bytes) return;
-        memcpy(dst + lo, src + lo, std::min(per, bytes - lo));
+        if (nt) nt_copy(dst + lo, src + lo, std::min(per, bytes - lo));
+        else memcpy(dst + lo, src + lo, std::min(per, bytes - lo));
     });
 }
 
@@ -317,7 +356,7 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
         // allreduce, pageable D2H straight into the caller's buffer, all on
         // the communicator's stream, and the caller spins on the end
         const double t0 = tracing() ? trace_now() : 0;
-        Copy(pin_in_[0], h, S);
+        Copy(pin_in_[0], h, S, true);
         const double t1 = tracing() ? trace_now() : 0;
         hip_check(hipMemcpyAsync(dev_, pin_in_[0], S, hipMemcpyHostToDevice, comm_stream), "H2D");
         c->Allreduce(dev_, count, dtype, op, comm_stream);
@@ -360,7 +399,7 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
             const double t0 = tracing() ? trace_now() : 0;
             if (k >= kSlots) hip_check(hipEventSynchronize(in_done_[slot]), "wait H2D slot");
             const double t1 = tracing() ? trace_now() : 0;
-            Copy(pin_in_[slot], h + lo, bytes);
+            Copy(pin_in_[slot], h + lo, bytes, true);
             if (tracing())
                 fprintf(stderr, "[host %.3f] piece %d: slot wait %.3f ms, copy-in %.3f ms (%llu B)\n", t0, k, t1 - t0,
                         trace_now() - t1, (unsigned long long)bytes);

@@ -59,7 +59,8 @@ private:
     };
     void Reserve(size_t piece_bytes, size_t total_bytes, int pieces, hipStream_t comm_stream);
     void QuiesceForRegrow(hipStream_t comm_stream);
-    void Copy(char* dst, const char* src, size_t bytes);  // parallel memcpy
+    // parallel memcpy; to_pinned: into a staging slot only the DMA reads (streaming stores)
+    void Copy(char* dst, const char* src, size_t bytes, bool to_pinned = false);
     void DrainLoop();
 
     // buffers up to kSmall: one pinned round trip, one synchronisation

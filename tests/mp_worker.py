@@ -227,7 +227,14 @@ def main():
         log("rank", rank, "case", i, "done")
         out = buf[pad: pad + nbytes].cpu().numpy()
         del buf
-        if c.get("digest"):
+        if c.get("windows"):  # huge buffers: the listed element windows + a digest of the whole result
+            import hashlib
+            e = esz[dtype]
+            win = np.concatenate([out[st * e:(st + m) * e] for st, m in c["windows"]])
+            np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), win)
+            open(os.path.join(outdir, "case%d_rank%d.sha" % (i, rank)), "w").write(
+                hashlib.sha256(out.data).hexdigest())
+        elif c.get("digest"):
             import hashlib
             open(os.path.join(outdir, "case%d_rank%d.sha" % (i, rank)), "w").write(
                 hashlib.sha256(out.tobytes()).hexdigest())

@@ -494,6 +494,34 @@ def test_mp_shared_channel_order_violation_is_an_error(world, algo):
         assert "another communicator" in info["error"] and "different orders" in info["error"], infos
 
 
+@pytest.mark.parametrize("world,kind", [(2, "allreduce"), (3, "allreduce"), (2, "host_allreduce")])
+def test_mp_count_beyond_int32(world, kind):
+    """A buffer of more than 2^31 elements (int8, 2 GiB + 4099): the
+    reference's int Split (include/utils/utils.h:59-70) overflows there; the
+    device path's 64-bit ranges and offsets must not.  Device buffers through
+    the schedule pieces, and a host buffer through the PCIe pipeline.  Windows
+    at every Split boundary, across the 2^31 element index and at both ends
+    are compared with the oracle (int8 Sum wraps, order-free), and every
+    rank's whole result must hash the same."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    count = (1 << 31) + 4099
+    W = 4096
+    starts = {0, count - W, (1 << 31) - W // 2, (1 << 31) + 4099 - W}
+    for b, _ in O.split(count, world)[1:]:
+        starts.add(b - W // 2)
+    wins = sorted((st, W) for st in starts)
+    seed = 0x5EED9000
+    cases = [{"count": count, "dtype": 0, "op": 2, "kind": kind, "seed": seed, "windows": wins}]
+    tmp = run_mp(world, cases, timeout=600)
+    shas = [open(os.path.join(tmp, "case0_rank%d.sha" % r)).read() for r in range(world)]
+    assert all(h == shas[0] for h in shas), shas
+    want = np.concatenate([O.expected_window(count, st, m, world, 0, 2, seed) for st, m in wins])
+    for r in range(world):
+        got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
+        assert got.tobytes() == want.tobytes(), r
+
+
 def test_mp_full_size_cfg2():
     """BASELINE cfg2 at full size: fp32 256 MiB allreduce over 2 ranks, both
     schedules, checked bit-exact (sha256) against the oracle's ring."""
