@@ -5,7 +5,6 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
-#include <immintrin.h>
 
 #include <algorithm>
 #include <chrono>
@@ -184,11 +183,7 @@ void HostPath::Reserve(size_t piece_bytes, size_t total_bytes, int pieces, hipSt
 }
 
 namespace {
-// Copies into a pinned staging slot are read by the DMA engine, never by
-// this CPU: streaming (non-temporal) stores skip the read-for-ownership of
-// every destination line and leave the caches to the source.  glibc's memcpy
-// only streams above a size threshold the pool's 512 KiB parts stay under.
-// RDC_HOST_NT_COPY=0 turns it off.
+// RDC_HOST_NT_COPY=0: plain memcpy into the pinned slots (rdc_copypool.h StreamCopy)
 bool nt_copy_enabled() {
     static const bool v = [] {
         const char* e = getenv("RDC_HOST_NT_COPY");
@@ -196,43 +191,10 @@ bool nt_copy_enabled() {
     }();
     return v;
 }
-__attribute__((target("avx2"))) void nt_copy(char* dst, const char* src, size_t bytes) {
-    size_t head = (32 - ((uintptr_t)dst & 31)) & 31;
-    if (head > bytes) head = bytes;
-    memcpy(dst, src, head);
-    size_t i = head;
-    for (; i + 128 <= bytes; i += 128) {
-        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
-        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
-        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
-        const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
-        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a);
-        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), b);
-        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), c);
-        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), d);
-    }
-    memcpy(dst + i, src + i, bytes - i);
-    // streaming stores are weakly ordered: drain them before this thread
-    // reports its part done (the DMA that follows must see every byte)
-    _mm_sfence();
-}
 }  // namespace
 
 void HostPath::Copy(char* dst, const char* src, size_t bytes, bool to_pinned) {
-    const bool nt = to_pinned && nt_copy_enabled();
-    if (bytes < kParallelMin) {
-        if (nt) nt_copy(dst, src, bytes);
-        else memcpy(dst, src, bytes);
-        return;
-    }
-    const int parts = (int)std::min<size_t>(16, bytes / (kParallelMin / 2));
-    const size_t per = (bytes / (size_t)parts + 4095) & ~(size_t)4095;
-    pool_.Run(parts, [&](int i) {
-        const size_t lo = (size_t)i * per;
-        if (lo >= bytes) return;
-        if (nt) nt_copy(dst + lo, src + lo, std::min(per, bytes - lo));
-        else memcpy(dst + lo, src + lo, std::min(per, bytes - lo));
-    });
+    ParallelCopy(pool_, dst, src, bytes, to_pinned && nt_copy_enabled(), kParallelMin);
 }
 
 void HostPath::DrainLoop() {

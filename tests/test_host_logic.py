@@ -36,3 +36,17 @@ def test_copypool_under_address_sanitizer(tmp_path):
         pytest.skip("no AddressSanitizer in this toolchain")
     out = subprocess.run([exe, "50000"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and "ERROR: AddressSanitizer" not in out.stderr, out.stderr[-3000:]
+
+
+def test_parallel_copy_covers_every_byte(tmp_path):
+    """rdc_copypool.h ParallelCopy, the host path's pageable <-> pinned copy
+    (streaming stores into pinned slots, memcpy out): every byte of sizes
+    around the part boundaries arrives and nothing outside the range is
+    written.  Cutting a copy by the floor of bytes / parts rounded up to
+    4 KiB used to drop the last bytes % parts bytes (e.g. 4 x 256 KiB + 3 B)."""
+    src = os.path.join(ROOT, "tests", "cpp", "hostcopy_check.cc")
+    exe = str(tmp_path / "hostcopy_check")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-I", INC, src, "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert '"bad": 0' in out.stdout
