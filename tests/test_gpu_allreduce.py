@@ -338,6 +338,10 @@ def test_mp_allreduce(world):
         {"count": 25000003, "dtype": 6, "op": 2, "kind": "host_allreduce", "reps": 2},   # 7 pipelined pieces
         {"count": 3000001, "dtype": 10, "op": 0, "kind": "host_allreduce"},
         {"count": 5, "dtype": 4, "op": 2, "kind": "host_allreduce"},
+        # host copies cut into parts whose floor is a 4 KiB multiple with bytes left over
+        # (2 x 256 KiB + 1 B staged small path, 4 x 256 KiB + 3 B one inline piece)
+        {"count": 524289, "dtype": 0, "op": 2, "kind": "host_allreduce"},
+        {"count": 1048579, "dtype": 1, "op": 0, "kind": "host_allreduce"},
         {"count": 100003, "dtype": 6, "op": 2, "algo": 2, "pad_per_rank": 4},   # ranks' buffers differ mod 16
         {"count": 100003, "dtype": 10, "op": 0, "algo": 1, "pad_per_rank": 2},
         {"count": 2, "dtype": 2, "kind": "bcast_chain", "steps": 40},
@@ -520,6 +524,41 @@ def test_mp_count_beyond_int32(world, kind):
     for r in range(world):
         got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
         assert got.tobytes() == want.tobytes(), r
+
+
+HOST_SWEEP_BYTES = [
+    65535, 65537,                      # the resident service's 64 KiB limit
+    524287, 524289, 786435,            # the copy pool's 512 KiB threshold, 2-3 parts with a remainder
+    1048575, 1048577, 1048579,         # zero-copy / staged small path (1 MiB) vs one inline piece
+    (3 << 20) + 7, 16777215, 16777217,  # one inline piece up to 16 MiB, the pipeline above
+    (33 << 20) + 4097,                 # pipeline without the ramp (< 8 pieces)
+    (64 << 20) + 4095,                 # pipeline with the ramp (>= 8 pieces), ragged last piece
+]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mp_host_size_sweep(world):
+    """Host buffers at every boundary of the host path (rdc_host.cpp: service,
+    copy-pool parts, zero-copy / staged small path, inline piece, pipeline
+    with and without the ramp) +-1 element, 1-byte and 4-byte elements, every
+    byte of every rank's result against the oracle.  A copy cut whose parts
+    did not cover the buffer (bytes % parts left over) once dropped the last
+    bytes of a piece: only sizes like these see it."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = []
+    for k, nb in enumerate(HOST_SWEEP_BYTES):
+        cases.append({"count": nb, "dtype": 1, "op": (0, 2)[k % 2], "kind": "host_allreduce", "seed": 0x5EEDA000 + k})
+        cases.append({"count": nb // 4 + 1, "dtype": 6, "op": 2, "kind": "host_allreduce", "seed": 0x5EEDB000 + k})
+    tmp = run_mp(world, cases, timeout=400)
+    for i, c in enumerate(cases):
+        want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            w = np.frombuffer(want[r].tobytes(), dtype=np.uint8)
+            assert got.shape == w.shape, (c, r)
+            bad = np.nonzero(got != w)[0]
+            assert bad.size == 0, "%r rank %d: %d bytes differ, first at byte %d" % (c, r, bad.size, bad[0])
 
 
 def test_mp_full_size_cfg2():
