@@ -561,6 +561,70 @@ def test_mp_host_size_sweep(world):
             assert bad.size == 0, "%r rank %d: %d bytes differ, first at byte %d" % (c, r, bad.size, bad[0])
 
 
+def fuzz_cases(seed, world, n=40):
+    """Seeded random sizes (log-uniform, 1 element .. 24 Mi elements), (dtype,
+    op) pairs with reference semantics, schedules, per-rank misalignment,
+    host buffers (service, zero-copy, inline piece, pipeline), broadcasts
+    from random roots and coalesced lists of random buckets."""
+    import random
+    rng = random.Random(seed)
+    pairs = [(6, 2), (6, 0), (7, 2), (7, 1), (2, 2), (2, 3), (3, 0), (0, 2), (1, 3), (4, 2), (5, 1), (10, 2),
+             (11, 2), (10, 0)]
+    esz = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 4, 7: 8, 10: 2, 11: 2}
+    cases = []
+    for k in range(n):
+        sd = seed * 1000 + k
+        kind = rng.choice(["allreduce"] * 5 + ["broadcast", "coalesced", "host_allreduce"])
+        if kind == "host_allreduce":
+            dt, op = rng.choice(pairs)
+            cases.append({"count": max(1, int(2 ** rng.uniform(0, 24))), "dtype": dt, "op": op,
+                          "kind": "host_allreduce", "seed": 0x5EED0000 + sd})
+        elif kind == "allreduce":
+            dt, op = rng.choice(pairs)
+            count = max(1, int(2 ** rng.uniform(0, 24.6)))
+            c = {"count": count, "dtype": dt, "op": op, "algo": rng.choice([0, 1, 2, 3]), "seed": 0x5EED0000 + sd}
+            if rng.random() < 0.5:  # the ranks' buffers differ mod 16 (element-aligned)
+                c["pad_per_rank"] = esz[dt] * rng.choice([1, 2, 3])
+            cases.append(c)
+        elif kind == "broadcast":
+            cases.append({"count": max(1, int(2 ** rng.uniform(0, 24))), "dtype": 0, "kind": "broadcast",
+                          "root": rng.randrange(world), "seed": 0x5EED0000 + sd, "pad": rng.choice([0, 1, 5])})
+        else:
+            dt, op = rng.choice([(6, 2), (2, 0), (10, 2), (7, 1)])
+            counts = [max(0, int(2 ** rng.uniform(-1, 19))) for _ in range(rng.randint(1, 12))]
+            cases.append({"count": 0, "dtype": dt, "op": op, "kind": "coalesced", "counts": counts,
+                          "algo": rng.choice([0, 1, 2, 3]), "seed": 0x5EED0000 + sd})
+    return cases
+
+
+@pytest.mark.parametrize("world,seed,env", [
+    (2, 21, {}),
+    (3, 22, {"RDC_SCRATCH_BYTES": "8M", "RDC_TILE_BYTES": "16K"}),   # many pieces and tiles per call
+    (2, 23, {"RDC_SCRATCH_BYTES": "4M", "RDC_NBLOCKS": "7"}),        # odd grid, tiny scratch
+    (4, 24, {}),
+    (3, 25, {"RDC_ALGO": "ring"}),          # host pipeline pieces and auto calls on the ring
+    (5, 26, {"RDC_SCRATCH_BYTES": "16M"}),
+])
+def test_mp_random_sizes_fuzz(world, seed, env):
+    """Seeded fuzz over sizes, types, ops, schedules, misalignment, scratch
+    and tile sizes (fuzz_cases): every byte of every rank's result against
+    the oracle (the reference's ring order; broadcast = the root's bytes).
+    Fixed size lists can miss a boundary a random size lands on."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = fuzz_cases(seed, world)
+    tmp = run_mp(world, cases, timeout=400, env_extra=env)
+    for i, c in enumerate(cases):
+        want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            w = np.frombuffer(want[r].tobytes(), dtype=np.uint8)
+            assert got.shape == w.shape, (i, c, r)
+            bad = np.nonzero(got != w)[0]
+            assert bad.size == 0, "case %d %r rank %d: %d bytes differ, first at byte %d" % (
+                i, c, r, bad.size, bad[0])
+
+
 def test_mp_full_size_cfg2():
     """BASELINE cfg2 at full size: fp32 256 MiB allreduce over 2 ranks, both
     schedules, checked bit-exact (sha256) against the oracle's ring."""
