@@ -210,6 +210,18 @@ int main(int argc, char** argv) {
             for (uint64_t i = 0; i < dst.Count(); ++i) d[i] += s[i];
         });
         save("custom_sum", f.data(), N * 4);
+        // chunks of zero length (count < ranks) and a count Split leaves ragged
+        for (size_t M : {(size_t)1, (size_t)2, (size_t)3, ((size_t)1 << 18) + 3}) {
+            std::vector<float> h = fill(M, 0x5EED3100 + (uint64_t)M, r);
+            rdc::Buffer hb(h.data(), M * 4);
+            hb.set_item_size(4);
+            rdc::GetCommunicator()->Allreduce(hb, [](rdc::Buffer src, rdc::Buffer dst) {
+                float* d = dst.As<float>();
+                const float* s = src.As<float>();
+                for (uint64_t i = 0; i < dst.Count(); ++i) d[i] += s[i];
+            });
+            save(("custom_sum_" + std::to_string(M)).c_str(), h.data(), M * 4);
+        }
         std::vector<float> g = fill(N, 0x5EED3200, r);
         rdc::Reducer<float, fsum> red;
         red.Allreduce(g.data(), N);

@@ -188,6 +188,12 @@ def test_cpp_buffer_surface(buffer_api_exe, tmp_path, world, mincount):
         for r in range(world):
             got = np.fromfile(str(tmp_path / ("%s_rank%d.bin" % (name, r))), dtype=np.float32)
             assert got.tobytes() == want.tobytes(), (name, r)
+    for M in (1, 2, 3, (1 << 18) + 3):  # custom reducer: empty chunks (M < world), ragged Split
+        xs = [O.fill(M, O.DT_FLOAT32, 0x5EED3100 + M, r) for r in range(world)]
+        want = (O.expected_tree if tree and 4 * M <= 4096 else O.expected_allreduce)(xs, O.DT_FLOAT32, O.OP_SUM)
+        for r in range(world):
+            got = np.fromfile(str(tmp_path / ("custom_sum_%d_rank%d.bin" % (M, r))), dtype=np.float32)
+            assert got.tobytes() == want.tobytes(), ("custom_sum", M, r)
     members = [q for q in range(world - 1, -1, -1) if q % 2 == 0]
     xs = [O.fill(N, O.DT_FLOAT32, 0x5EED3300, i) for i in range(len(members))]
     want = (O.expected_tree if tree else O.expected_allreduce)(xs, O.DT_FLOAT32, O.OP_SUM)
