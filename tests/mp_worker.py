@@ -215,10 +215,15 @@ def main():
             elif kind == "broadcast":
                 check_call(_LIB.RdcCommBroadcast(comm.handle, ctypes.c_void_p(p), nbytes, c["root"], sp))
             elif kind == "host_allreduce":
-                host = buf[pad: pad + nbytes].cpu().numpy().copy()
+                # host_offset: the host buffer starts that many bytes past an
+                # aligned allocation (element-aligned, not 16-B aligned)
+                ho = c.get("host_offset", 0)
+                backing = np.empty(nbytes + ho + 64, dtype=np.uint8)
+                host = backing[ho: ho + nbytes]
+                host[:] = buf[pad: pad + nbytes].cpu().numpy()
                 check_call(_LIB.RdcAllreduce(host.ctypes.data_as(ctypes.c_void_p), count, dtype, c["op"], None,
                                              None))
-                buf[pad: pad + nbytes] = torch.from_numpy(host).cuda()
+                buf[pad: pad + nbytes] = torch.from_numpy(host.copy()).cuda()
         log("rank", rank, "case", i, "launched")
         comm.check(sp)
         if c.get("last_launch"):

@@ -578,7 +578,8 @@ def fuzz_cases(seed, world, n=40):
         if kind == "host_allreduce":
             dt, op = rng.choice(pairs)
             cases.append({"count": max(1, int(2 ** rng.uniform(0, 24))), "dtype": dt, "op": op,
-                          "kind": "host_allreduce", "seed": 0x5EED0000 + sd})
+                          "kind": "host_allreduce", "seed": 0x5EED0000 + sd,
+                          "host_offset": esz[dt] * rng.choice([0, 0, 1, 3])})
         elif kind == "allreduce":
             dt, op = rng.choice(pairs)
             count = max(1, int(2 ** rng.uniform(0, 24.6)))
