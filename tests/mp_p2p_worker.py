@@ -5,6 +5,8 @@ argv: rank world port mode.  All ranks share GPU 0 (RDC_DEVICE=0).
             100 messages, the receiver sleeping before the first) and
             pytest/comm.py (Buffer(b'hello') -> Buffer(b'00000'))
   ring    — send a multi-piece device buffer to rank+1, receive from rank-1
+  fuzz    — a seeded list of messages between random pairs, random sizes,
+            device or host memory on either side, up to 8 in flight
   timeout — rank 1 receives a message rank 0 never sends: an error, not a hang
 """
 import os
@@ -65,6 +67,36 @@ def main():
         wr = comm.irecv(g, prv)
         ws.wait(), wr.wait()
         assert np.array_equal(g, np.arange(12345, dtype=np.float64) + prv)
+    elif mode == "fuzz":
+        # a seeded global list of messages (source, destination, size 0 B ..
+        # ~24 MiB, device or host memory); every rank walks it in order,
+        # posting its own sends and receives non-blocking with up to 8 in
+        # flight, so each pair's messages are matched in list order
+        rng = np.random.default_rng(777 + world)
+        msgs = []
+        for i in range(60):
+            s = int(rng.integers(world))
+            d = int((s + 1 + rng.integers(world - 1)) % world)
+            n = 0 if rng.random() < 0.05 else int(2 ** rng.uniform(0, 24.5))
+            msgs.append((i, s, d, n, bool(rng.random() < 0.3), bool(rng.random() < 0.3)))
+        pend, checks = [], []
+        for i, s, d, n, host_s, host_r in msgs:
+            if rank == s:
+                x = np.random.default_rng(1000 + i).integers(0, 256, n, dtype=np.uint8)
+                t = x if host_s else torch.from_numpy(x).cuda()
+                pend.append((comm.isend(t, d), t))
+            if rank == d:
+                y = np.zeros(n, np.uint8) if host_r else torch.zeros(n, dtype=torch.uint8, device="cuda")
+                pend.append((comm.irecv(y, s), y))
+                checks.append((i, n, y))
+            while len(pend) > 8:
+                pend.pop(0)[0].wait()
+        for w, _ in pend:
+            w.wait()
+        for i, n, y in checks:
+            got = y if isinstance(y, np.ndarray) else y.cpu().numpy()
+            want = np.random.default_rng(1000 + i).integers(0, 256, n, dtype=np.uint8)
+            assert np.array_equal(got, want), "message %d (%d B) differs" % (i, n)
     elif mode == "timeout":
         if rank == 1:
             y = torch.zeros(100, dtype=torch.uint8, device="cuda")

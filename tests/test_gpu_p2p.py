@@ -191,6 +191,14 @@ def test_mp_ring_device_buffers():
     run_workers(3, "ring")
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_mp_sendrecv_fuzz(world):
+    """60 seeded messages between random pairs (0 B .. ~24 MiB, device or host
+    buffers on either side, multi-piece, up to 8 in flight per rank), every
+    byte checked on the receiver."""
+    run_workers(world, "fuzz", timeout=300)
+
+
 def test_mp_peer_never_sends_times_out():
     """A receive whose sender never posts ends in error after RDC_TIMEOUT."""
     run_workers(2, "timeout", env_extra={"RDC_TIMEOUT": "3"})
