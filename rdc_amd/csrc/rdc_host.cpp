@@ -23,12 +23,11 @@ int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
 }
-// Buffers up to kOnePieceMax go as ONE piece on the caller's thread; larger
-// ones through the pipeline in pieces of piece_target() bytes of all chunks'
-// slices (RDC_HOST_PIECE_BYTES, default 8 MiB: n = 2 on one GPU, 64 MiB
-// 4.7-4.9 ms vs 6.3-7.6 ms with 16 MiB pieces, 256 MiB 15-20 vs 19-23 ms;
+// Buffers up to HostInlineBytes() go as ONE piece on the caller's thread;
+// larger ones through the pipeline in pieces of piece_target() bytes
+// (RDC_HOST_PIECE_BYTES, default 8 MiB: n = 2 on one GPU, 64 MiB 4.7-4.9 ms
+// vs 6.3-7.6 ms with 16 MiB pieces, 256 MiB 15-20 vs 19-23 ms;
 // profiles/r02/host_pieces/)
-constexpr size_t kOnePieceMax = (size_t)16 << 20;
 size_t piece_target() { return HostPieceBytes(); }
 constexpr size_t kParallelMin = (size_t)512 << 10;  // below this a copy runs on the caller alone (waking the pool costs more)
 // RDC_HOST_TRACE=1: per-piece timeline on stderr (diagnostics)
@@ -43,11 +42,41 @@ bool tracing() {
 }
 }  // namespace
 
+// {integer}{B,K,M,G} as the reference's ParseUnit (communicator_manager.cc:14-42);
+// 0 when unset or malformed
+static size_t env_bytes(const char* name) {
+    const char* e = getenv(name);
+    if (!e || !*e) return 0;
+    unsigned long long amt = 0;
+    char unit = 0;
+    const int k = sscanf(e, "%llu%c", &amt, &unit);
+    if (k == 1) return (size_t)amt;
+    if (k != 2) return 0;
+    switch (unit) {
+        case 'B': return (size_t)amt;
+        case 'K': return (size_t)amt << 10;
+        case 'M': return (size_t)amt << 20;
+        case 'G': return (size_t)amt << 30;
+        default: return 0;
+    }
+}
+
 size_t HostPieceBytes() {
     static const size_t v = [] {
-        const char* e = getenv("RDC_HOST_PIECE_BYTES");
-        const long long x = e ? atoll(e) : 0;
-        return x >= (1 << 20) ? (size_t)x : (size_t)8 << 20;
+        const size_t x = env_bytes("RDC_HOST_PIECE_BYTES");
+        return x >= ((size_t)1 << 20) ? x : (size_t)8 << 20;
+    }();
+    return v;
+}
+
+// inline (one piece on the caller) up to 16 MiB by default: pipelining 4-16
+// MiB in 1-2 MiB pieces measured no better (n = 2 on one GPU, alternating:
+// 16 MiB 1.55-1.61 ms inline vs 1.53-1.65 with 2 MiB pieces, 2.8-3.1 with
+// 1 MiB; 4 MiB 0.46-0.49 vs 0.50-0.51; profiles/r03/host_inline_ab/)
+size_t HostInlineBytes() {
+    static const size_t v = [] {
+        const char* e = getenv("RDC_HOST_INLINE_BYTES");
+        return e && *e ? env_bytes("RDC_HOST_INLINE_BYTES") : (size_t)16 << 20;
     }();
     return v;
 }
@@ -71,7 +100,7 @@ std::vector<uint64_t> HostPieceBounds(uint64_t S) {
     const uint64_t P = piece_target();
     auto up4k = [](uint64_t x) { return std::max<uint64_t>(4096, (x + 4095) & ~(uint64_t)4095); };
     std::vector<uint64_t> b{0};
-    if (S <= kOnePieceMax) {
+    if (S <= HostInlineBytes()) {
         b.push_back(S);
         return b;
     }

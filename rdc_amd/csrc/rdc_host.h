@@ -36,6 +36,9 @@ namespace rdc_amd {
 size_t HostPieceBytes();
 // RDC_HOST_PIECE_RAMP (default 1): small first and last pieces (a plan key too)
 bool HostPieceRamp();
+// RDC_HOST_INLINE_BYTES (default 16 MiB): host buffers up to this size go as
+// ONE piece on the caller's thread, larger ones through the pipeline (a plan key)
+size_t HostInlineBytes();
 // the pipeline's piece boundaries for an S-byte host buffer: {0, ..., S}
 std::vector<uint64_t> HostPieceBounds(uint64_t S);
 

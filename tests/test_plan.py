@@ -291,3 +291,20 @@ def test_host_pipeline_pieces(piece, ramp):
         else:
             mid = lens
         assert max(mid) <= P + 4096 and len(mid) == -(-(S - (sum(lens) - sum(mid))) // P), (S, P, mid)
+
+
+def test_host_pipeline_knobs_parse_units():
+    """RDC_HOST_PIECE_BYTES takes the reference's size units (ParseUnit,
+    communicator_manager.cc:14-42: 4M == 4194304), and RDC_HOST_INLINE_BYTES
+    moves the one-piece threshold (0: every buffer above one piece is
+    pipelined)."""
+    sizes = [4 << 20, 16 << 20, (16 << 20) + 4096]
+    a = host_pieces(sizes, {"RDC_HOST_PIECE_BYTES": "2M"})
+    b = host_pieces(sizes, {"RDC_HOST_PIECE_BYTES": str(2 << 20)})
+    assert a == b
+    assert a[16 << 20] == [0, 16 << 20]                      # inline up to 16 MiB by default
+    assert len(a[(16 << 20) + 4096]) - 1 == 3 + 7 + 3         # ramps + pieces of <= 2 MiB above
+    c = host_pieces(sizes, {"RDC_HOST_PIECE_BYTES": "2M", "RDC_HOST_INLINE_BYTES": "1M"})
+    lens = [y - x for x, y in zip(c[16 << 20], c[16 << 20][1:])]
+    assert lens[:3] == [256 << 10, 512 << 10, 1 << 20] and max(lens) <= 2 << 20 and sum(lens) == 16 << 20
+    assert [y - x for x, y in zip(c[4 << 20], c[4 << 20][1:])] == [2 << 20, 2 << 20]
