@@ -28,9 +28,13 @@ def main():
     import torch
     import rdc_amd
     from rdc_amd._lib import _LIB, check_call
+    # RDC_DEVICE=rank: rank r on GPU r % #GPUs (a node with several GPUs);
+    # otherwise every rank on that one device (the 1-GPU box: GPU 0)
+    dev_env = os.environ.get("RDC_DEVICE", "0")
+    device = rank % max(1, torch.cuda.device_count()) if dev_env == "rank" else int(dev_env)
     rdc_amd.init(["RDC_RANK=%d" % rank, "RDC_WORLD_SIZE=%d" % world, "RDC_TRACKER_PORT=%d" % port,
-                  "RDC_TRACKER_URI=127.0.0.1", "RDC_DEVICE=%s" % os.environ.get("RDC_DEVICE", "0")])
-    torch.cuda.set_device(int(os.environ.get("RDC_DEVICE", "0")))
+                  "RDC_TRACKER_URI=127.0.0.1", "RDC_DEVICE=%d" % device])
+    torch.cuda.set_device(device)
     log("rank", rank, "init done")
     comms = {}
     esz = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 4, 7: 8, 8: 8, 9: 8, 10: 2, 11: 2}

@@ -626,6 +626,30 @@ def test_mp_random_sizes_fuzz(world, seed, env):
                 i, c, r, bad.size, bad[0])
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_mp_across_devices(world):
+    """One rank per GPU when the box has several (rank r on GPU r % #GPUs):
+    the hand-offs then cross xGMI instead of landing in one HBM.  Fixed
+    cases at every schedule plus a seeded fuzz, every byte against the
+    oracle.  Skipped on a 1-GPU box (the driver's 8-GPU bench checks the same
+    hand-offs after its timed region)."""
+    if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 or more GPUs")
+    cases = [{"count": 1001, "dtype": 6, "op": 2, "algo": a} for a in (0, 1, 2, 3)]
+    cases += [{"count": (16 << 20) + 5, "dtype": 6, "op": 2, "algo": a} for a in (1, 2)]
+    cases += [{"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"},
+              {"count": (40 << 20) + 3, "dtype": 1, "op": 0, "kind": "host_allreduce"},
+              {"count": (3 << 20) + 5, "dtype": 0, "kind": "broadcast", "root": world - 1}]
+    cases += fuzz_cases(30 + world, world, n=24)
+    tmp = run_mp(world, cases, timeout=400, env_extra={"RDC_DEVICE": "rank"})
+    for i, c in enumerate(cases):
+        want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            w = np.frombuffer(want[r].tobytes(), dtype=np.uint8)
+            assert got.tobytes() == w.tobytes(), (i, c, r)
+
+
 def test_mp_full_size_cfg2():
     """BASELINE cfg2 at full size: fp32 256 MiB allreduce over 2 ranks, both
     schedules, checked bit-exact (sha256) against the oracle's ring."""
