@@ -200,3 +200,19 @@ def test_cpp_buffer_surface(buffer_api_exe, tmp_path, world, mincount):
     for q in members:
         got = np.fromfile(str(tmp_path / ("group_sum_rank%d.bin" % q)), dtype=np.float32)
         assert got.tobytes() == want.tobytes(), ("group", q)
+
+
+def test_rccl_comparison_child_one_rank():
+    """tools/rccl_allreduce.py, the RCCL comparison child bench.py starts per
+    rank on a node with one GPU per rank (never run in the one-GPU
+    rehearsals, where ranks share the GPU): one rank, 64 MiB, a JSON line."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    port = free_port()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_allreduce.py"), "0", "1", "0", "127.0.0.1",
+                        str(port), str(64 << 20), "5"], capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["rccl"] is True and d["ms_per_step"] > 0 and d["bytes_per_gpu"] == 64 << 20, d
