@@ -209,6 +209,22 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
               "clock stops when the last call returns, max over ranks)", max(steps, 2000))
     e["us_per_call"] = round(ms * 1e3, 2)
     out["cfg1_host_4KiB"] = e
+    # the PCIe-inclusive rate (north star: rdc buffers begin and end in host
+    # memory): 64 MiB of fp32 in pageable host memory through RdcAllreduce,
+    # i.e. the host pipeline (copy in, H2D, allreduce, D2H) with each rank on
+    # its own link when ranks have a GPU each
+    if budget is None or budget.left() >= 15:
+        hb = np.ones(16 << 20, dtype=np.float32)
+        ph = ctypes.c_void_p(hb.ctypes.data)
+        ms = timed_ms(lambda: check_call(lib.RdcAllreduce(ph, hb.size, 6, 2, None, None)), comm, sp, dist, torch, 5,
+                      warm=2, synchronous=True)
+        e = entry(ms, hb.nbytes, "64 MiB float32 allreduce of HOST (pageable) memory via RdcAllreduce: copy in, "
+                  "H2D, allreduce, D2H, pipelined (PCIe-inclusive; synchronous, max over ranks)", 5)
+        e["algbw_GBps_pcie_inclusive"] = round(hb.nbytes / (ms * 1e-3) / 1e9, 2)
+        out["host_64MiB"] = e
+        del hb
+    else:
+        out.setdefault("skipped", []).append("host_64MiB")
     # cfg2's 256 MiB fp32 buffer and the sizes below it (prefixes of one
     # buffer): where the mesh's per-launch fill / drain and the one-shot
     # hand-off decide the rate, for the size thresholds at this rank count
