@@ -17,6 +17,13 @@ rendezvous completes; rejoining a running job is the tracker's recovery
 protocol, out of scope like checkpointing).  Unlike
 it, the first worker that fails for good stops the others and its exit code
 is returned (the reference raises inside a daemon thread and hangs).
+
+--numa-bind confines each worker to the CPUs of its GPU's NUMA node (read
+from sysfs before the worker starts; the launcher never touches the GPU).
+Host buffers are copied into pinned memory and DMA'd from there: at n = 2
+on one GPU, 16 MiB host allreduces ran 1.52-1.54 ms on the GPU's node vs
+1.67-1.76 ms on the other one, little difference above (DESIGN.md §5.3,
+profiles/r03/host_numa_ab2/).
 """
 import argparse
 import os
@@ -37,6 +44,8 @@ def parse_args(argv=None):
     p.add_argument("--port", type=int, default=0, help="bootstrap port (0 = pick a free one)")
     p.add_argument("--gpus", type=int, default=0, help="GPUs to spread ranks over (0 = all visible)")
     p.add_argument("--max-attempts", type=int, default=10, help="restarts per worker on exit code 254")
+    p.add_argument("--numa-bind", action="store_true",
+                   help="confine each worker to the CPUs of its GPU's NUMA node")
     p.add_argument("command", nargs=argparse.REMAINDER, help="command for launching the program")
     args, unknown = p.parse_known_args(argv)
     # the reference appends unknown options to the command (launcher_local.py:34)
@@ -68,6 +77,70 @@ def count_gpus():
         return 1
 
 
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def parse_cpulist(text):
+    """'0-63,128-191' -> {0..63, 128..191}"""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def _visible_count():
+    """Devices *_VISIBLE_DEVICES leaves to HIP (None when none is set)."""
+    n = None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            k = len([x for x in v.split(",") if x.strip()])
+            n = k if n is None else min(n, k)
+    return n
+
+
+def gpu_local_cpus(ordinal, sysfs="/sys"):
+    """CPUs local to HIP device `ordinal`: the KFD topology's GPU nodes this
+    process can read, in node order (HIP's device order); a node's
+    drm_render_minor names its render device, whose PCI function lists its
+    local CPUs.  When *_VISIBLE_DEVICES is set, only if it leaves exactly the
+    readable GPUs (a container that exposes just its own); otherwise, or when
+    sysfs cannot be read, None."""
+    base = os.path.join(sysfs, "class", "kfd", "kfd", "topology", "nodes")
+    try:
+        nodes = sorted(int(x) for x in os.listdir(base) if x.isdigit())
+    except OSError:
+        return None
+    minors = []
+    for nd in nodes:
+        props = _read(os.path.join(base, str(nd), "properties")) or ""
+        kv = dict(line.split(None, 1) for line in props.splitlines() if len(line.split(None, 1)) == 2)
+        try:
+            if int(kv.get("simd_count", "0")) > 0 and "drm_render_minor" in kv:
+                minors.append(int(kv["drm_render_minor"]))
+        except ValueError:
+            return None
+    vis = _visible_count()
+    if (vis is not None and vis != len(minors)) or ordinal >= len(minors):
+        return None
+    text = _read(os.path.join(sysfs, "class", "drm", "renderD%d" % minors[ordinal], "device", "local_cpulist"))
+    if not text:
+        return None
+    try:
+        cpus = parse_cpulist(text)
+    except ValueError:
+        return None
+    return cpus or None
+
+
 def worker_env(args, rank, port, ngpu):
     env = dict(os.environ)
     env.update({
@@ -96,6 +169,17 @@ def run(args):
 
     def keepalive(rank):
         env = worker_env(args, rank, port, ngpu)
+        if args.numa_bind:
+            local = gpu_local_cpus(rank % max(1, ngpu))
+            allowed = os.sched_getaffinity(0)
+            cpus = (local & allowed) if local else None
+            if cpus:
+                # this keepalive thread only (Linux: pid 0 = the calling
+                # thread); the worker forked from it inherits the mask
+                os.sched_setaffinity(0, cpus)
+            else:
+                print("rdc_amd.launcher: --numa-bind: no CPU list for GPU %d, worker %d unbound"
+                      % (rank % max(1, ngpu), rank), file=sys.stderr)
         attempt = 0
         while not stop.is_set():
             env["RDC_NUM_ATTEMPT"] = str(attempt)

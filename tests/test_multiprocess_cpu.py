@@ -220,3 +220,52 @@ def test_bench_extras_budget_agreed_across_ranks():
         lefts.append(json.loads(line.split(" ", 2)[2]))
     assert lefts[0] == lefts[1], lefts
     assert lefts[0][-1] < 0 < lefts[0][0] and lefts[0] == sorted(lefts[0], reverse=True), lefts
+
+
+def _fake_sysfs(root, gpus):
+    """KFD topology with a CPU node and one GPU node per (render minor,
+    local_cpulist) in `gpus`, plus the render devices' local_cpulist."""
+    nodes = root / "class" / "kfd" / "kfd" / "topology" / "nodes"
+    (nodes / "0").mkdir(parents=True)
+    (nodes / "0" / "properties").write_text("cpu_cores_count 64\nsimd_count 0\n")
+    for i, (minor, cpus) in enumerate(gpus, start=1):
+        (nodes / str(i)).mkdir()
+        (nodes / str(i) / "properties").write_text("simd_count 1024\ndrm_render_minor %d\n" % minor)
+        dev = root / "class" / "drm" / ("renderD%d" % minor) / "device"
+        dev.mkdir(parents=True)
+        (dev / "local_cpulist").write_text(cpus + "\n")
+
+
+def test_launcher_numa_cpus_from_sysfs(tmp_path, monkeypatch):
+    """--numa-bind's lookup (rdc_amd/launcher.py gpu_local_cpus): HIP device
+    k = the k-th readable KFD GPU node, its render device's local_cpulist;
+    none when *_VISIBLE_DEVICES remaps the readable GPUs or the topology is
+    missing."""
+    from rdc_amd.launcher import gpu_local_cpus, parse_cpulist
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    assert parse_cpulist("0-3,8,10-11") == {0, 1, 2, 3, 8, 10, 11}
+    _fake_sysfs(tmp_path, [(128, "0-63,128-191"), (136, "64-127,192-255")])
+    assert gpu_local_cpus(0, str(tmp_path)) == set(range(0, 64)) | set(range(128, 192))
+    assert gpu_local_cpus(1, str(tmp_path)) == set(range(64, 128)) | set(range(192, 256))
+    assert gpu_local_cpus(2, str(tmp_path)) is None
+    assert gpu_local_cpus(0, str(tmp_path / "missing")) is None
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")          # remaps 2 readable GPUs: unknown
+    assert gpu_local_cpus(0, str(tmp_path)) is None
+    one = tmp_path / "one"                                    # a container exposing only its GPU
+    _fake_sysfs(one, [(168, "0-63,128-191")])
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert gpu_local_cpus(0, str(one)) == set(range(0, 64)) | set(range(128, 192))
+
+
+def test_launcher_numa_bind_confines_workers(tmp_path):
+    """With --numa-bind every worker starts inside this process's allowed
+    CPUs (here no GPU topology: workers run unbound with a warning, and the
+    run still succeeds)."""
+    prog = tmp_path / "aff.py"
+    prog.write_text("import os\nprint('cpus', len(os.sched_getaffinity(0)))\n")
+    p = subprocess.run([sys.executable, "-m", "rdc_amd.launcher", "-n", "2", "--numa-bind", sys.executable,
+                        str(prog)], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.count("cpus") == 2

@@ -4,11 +4,23 @@
 # (tools/host_path.py), alternating.  The node comes from sysfs.
 out=${1:-gpurun_out/host_numa_ab}
 mkdir -p $out
-node=$(cat /sys/class/drm/card0/device/numa_node 2>/dev/null || echo 0)
-near=$(cat /sys/devices/system/node/node$node/cpulist)
-far=$(cat /sys/devices/system/node/node$((1 - node))/cpulist 2>/dev/null || echo $near)
-echo "gpu numa node $node near $near far $far"
-port=30900
+# the visible GPU's own CPUs (its render device's local_cpulist, as the
+# launcher's --numa-bind reads them) and the rest; /sys/class/drm/card0 is not
+# necessarily this box's GPU (the first version of this script read it and
+# labelled the two nodes the wrong way round on a box whose GPU is on node 1)
+read near far < <(python3 -c "
+import os, sys
+sys.path.insert(0, '.')
+from rdc_amd.launcher import gpu_local_cpus
+c = gpu_local_cpus(0)
+if not c:
+    sys.exit('no GPU-local CPU list')
+rest = sorted(os.sched_getaffinity(0) - c)
+fmt = lambda s: ','.join(map(str, sorted(s)))
+print(fmt(c), fmt(rest))
+") || exit 1
+echo "gpu-local cpus $near | others $far"
+port=31300
 for k in 1 2; do
   for cfg in "free" "near" "far"; do
     case $cfg in free) pre="";; near) pre="taskset -c $near";; far) pre="taskset -c $far";; esac
