@@ -654,6 +654,8 @@ def main():
         # keeps the same winner (times agreed by a MAX allreduce in the
         # library); a failure is recorded and the defaults kept.
         try:
+            if os.environ.get("RDC_BENCH_FAIL_AUTOTUNE") == str(rank):  # test hook: this rank fails
+                raise RuntimeError("injected autotune failure (RDC_BENCH_FAIL_AUTOTUNE)")
             tuned = comm.autotune(S, dt_enum, reps=args.autotune_reps, stream=sp)
             failed = 0.0
         except Exception as e:  # noqa: BLE001 - recorded in the line
@@ -661,9 +663,18 @@ def main():
         f = torch.tensor([failed], dtype=torch.float64)
         dist.all_reduce(f, op=dist.ReduceOp.MAX)
         if float(f[0]) > 0:
-            comm.tune(4, 8, 0, 0)
             if "error" not in tuned:
                 tuned = {"error": "failed on another rank"}
+            # A candidate that failed on the device (a wait timed out) leaves
+            # its channel unusable: every later launch on it skips its body
+            # and reports the error.  Every rank (the failure is agreed above)
+            # moves to a fresh communicator with a channel of its own and the
+            # library's default shape; `step` and the extras use it.
+            os.environ["RDC_SHARE_SCRATCH"] = "0"
+            comm = rdc_amd.new_comm("bench_after_autotune_failure")
+            tuned["timed_on"] = "a fresh communicator (own channel, default shape) after the failure"
+            step()
+            torch.cuda.synchronize()
         sync_check(comm, sp, dist, torch)
     for _ in range(max(0, args.warmup - 1)):
         step()

@@ -110,6 +110,33 @@ def test_bench_tiny_extras_budget():
     assert "extra_configs" not in out and "oracle_check" not in out
 
 
+def test_bench_recovers_from_autotune_failure():
+    """An autotune that fails on one rank (injected on rank 1, whose absence
+    then times out rank 0's candidates on the device) is agreed by every
+    rank, which then time the region on a fresh communicator with a channel
+    of its own (a device-side failure leaves the old channel unusable): the
+    line is printed, records the failure, and every parity check after the
+    timed region passes on the new communicator."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "2", "--bytes", str(16 << 20), "--autotune-reps", "1",
+           "--extra-steps", "0", "--ring-steps", "0", "--rccl-steps", "0", "--cpu-seconds", "0"]
+    # rank 1 skips autotune: rank 0's candidates wait for it until RDC_TIMEOUT,
+    # so rank 0's channel really fails on the device
+    env = dict(os.environ, RDC_BENCH_FAIL_AUTOTUNE="1", RDC_TIMEOUT="8")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["value"] > 0
+    assert "error" in out["autotune"] and "fresh communicator" in out["autotune"]["timed_on"], out["autotune"]
+    assert out["config"]["launch"]["source"] == "library defaults (automatic rule)", out["config"]
+    chk = out["oracle_check"]
+    assert all(chk.get(k) is True for k in PARITY_KEYS), chk
+
+
 def test_launcher_cpp_known_answer(known_answer_exe):
     """The reference's workflow (launcher -n N prog args) with rdc_amd's
     launcher: the C++ known-answer program at 3 ranks, rendezvous from env."""
