@@ -683,7 +683,6 @@ def main():
     if world > 1:
         sync_check(comm, sp, dist, torch)
         dist.barrier()
-        probe = xgmi_probe(_LIB, comm, sp, dist, torch)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -755,6 +754,10 @@ def main():
     multi = world > 1 and args.buckets == 1 and args.algo == "auto"
     f32 = args.dtype == "float32"
     roles = ring_cmp = extra = rccl = tcp = checks = None
+    if world > 1:
+        # the measured link rates (every rank idle), after the timed region so
+        # that a failure here cannot cost the headline
+        probe = guarded("xgmi_probe", lambda: xgmi_probe(_LIB, comm, sp, dist, torch), need_s=5)
     if multi:
         roles = guarded("role_timeline", lambda: trace_roles(_LIB, comm, buf, count, dt_enum, sp, dist, torch),
                         need_s=2)
