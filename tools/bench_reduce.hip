@@ -198,6 +198,22 @@ __global__ __launch_bounds__(B) void k_gsp(v4u* __restrict__ d, const v4u* __res
 
 typedef void (*KFn)(v4u*, const v4u*, uint64_t);
 
+// splitmix64 bits mapped to floats in [-1, 1) (a bounded Sum stays finite)
+__global__ void k_fill_random(v4u* p, uint64_t nvec, uint64_t seed) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * blockDim.x) {
+        v4u v;
+        for (int k = 0; k < 4; ++k) {
+            uint64_t z = (seed << 40) ^ (4 * i + k);
+            z += 0x9E3779B97F4A7C15ull;
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            z ^= z >> 31;
+            v[k] = __float_as_uint((float)((z >> 40) * (1.0 / 16777216.0)) * 2.0f - 1.0f);
+        }
+        p[i] = v;
+    }
+}
+
 struct Variant {
     const char* name;
     KFn fn;
@@ -212,6 +228,11 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&s, S));
     CK(hipMemset(d, 0, S));
     CK(hipMemset(s, 0, S));
+    if (getenv("SWEEP_RANDOM")) {  // full-entropy floats instead of zeros (the bench's data)
+        hipLaunchKernelGGL(k_fill_random, dim3(1024), dim3(256), 0, 0, d, nvec, 1ull);
+        hipLaunchKernelGGL(k_fill_random, dim3(1024), dim3(256), 0, 0, const_cast<v4u*>(s), nvec, 2ull);
+        CK(hipDeviceSynchronize());
+    }
     const bool quick = getenv("SWEEP_QUICK") != nullptr;
     std::vector<Variant> qv = {
         {"gs U2 nt/nt B256", (KFn)k_gs<2, true, true, 256>, 256},
