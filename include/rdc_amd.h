@@ -127,7 +127,10 @@ int RdcCreateGroup(void** out, void* parent, const int* ranks, int nranks, const
  * 56-80; rdc/comm.py:46-80 binds RdcISend / RdcIRecv / RdcWorkCompletion*).
  * Buffers are rdc Buffer handles (rdc/buffer.py:34-38: RdcNewBuffer(byref(h),
  * addr, size, pinned)) over host OR device memory; `pinned` page-locks a host
- * range (hipHostRegister) for the buffer's lifetime.  Data moves GPU to GPU
+ * range (hipHostRegister) for the buffer's lifetime (whole pages only: a
+ * page-aligned address and size).  A host allreduce (RdcAllreduce /
+ * RdcCommAllreduce on a host pointer) whose buffer lies inside such a range
+ * DMAs straight from and into it, with no copy through staging memory.  Data moves GPU to GPU
  * over xGMI through the receiver's IPC-mapped slots; messages on one (src,
  * dst) pair are matched in order and must have equal sizes on both sides.
  * A request that makes no progress for RDC_TIMEOUT seconds ends in error.
@@ -187,7 +190,9 @@ int RdcCommCheck(void* comm, void* stream);
  * "ranks_per_gpu" (most ranks of it sharing one physical GPU), "coalesced_misaligned"
  * (buckets of the last coalesced call not 16-B aligned), "shares_scratch"
  * (1 when another communicator uses the same scratch channel: every named
- * communicator over the same ranks shares one, RDC_SHARE_SCRATCH=0 disables). */
+ * communicator over the same ranks shares one, RDC_SHARE_SCRATCH=0 disables),
+ * "host_registered_calls" (host allreduces of this process that DMA'd in place
+ * from a pinned RdcNewBuffer range). */
 int RdcCommGetParam(void* comm, const char* key, uint64_t* value);
 int RdcCommRank(void* comm);
 int RdcCommSize(void* comm);

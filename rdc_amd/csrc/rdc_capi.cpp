@@ -614,6 +614,7 @@ int RdcCommGetParam(void* comm, const char* key, uint64_t* value) {
         else if (k == "ranks_per_gpu") *value = (uint64_t)c->ranks_per_gpu();
         else if (k == "coalesced_misaligned") *value = (uint64_t)c->coalesced_misaligned_;
         else if (k == "shares_scratch") *value = c->shares_channel() ? 1 : 0;
+        else if (k == "host_registered_calls") *value = HostRegisteredCalls();
         else throw std::invalid_argument("rdc: unknown parameter " + k);
     });
 }
@@ -824,6 +825,9 @@ int RdcNewBuffer(void** out, void* addr, size_t size, int pinned) {
             // runtime's own copies behind this registration's back
             b->registered = hipHostRegister(addr, size, hipHostRegisterDefault) == hipSuccess;
             (void)hipGetLastError();
+            // host allreduces inside the range DMA straight from / into it
+            // (HostPath::AllreduceRegistered)
+            if (b->registered) HostRegistryAdd(addr, size);
         }
         *out = b.release();
     });
@@ -833,7 +837,10 @@ int RdcDelBuffer(void* buf) {
     return guard([&] {
         if (!buf) return;
         BufferH* b = static_cast<BufferH*>(buf);
-        if (b->registered) (void)hipHostUnregister(b->addr);
+        if (b->registered) {
+            HostRegistryRemove(b->addr);
+            (void)hipHostUnregister(b->addr);
+        }
         delete b;
     });
 }

@@ -7,7 +7,9 @@
 #include <time.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <map>
 #include <stdexcept>
 #include <string>
 
@@ -128,6 +130,34 @@ std::vector<uint64_t> HostPieceBounds(uint64_t S) {
     return b;  // b.back() == S
 }
 
+// ------------------------------------------------------ registered ranges --
+namespace {
+std::mutex g_reg_mu;
+std::map<uintptr_t, size_t> g_reg;  // start -> bytes, non-overlapping (hipHostRegister refuses overlaps)
+std::atomic<uint64_t> g_reg_calls{0};
+}  // namespace
+
+void HostRegistryAdd(const void* p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[(uintptr_t)p] = bytes;
+}
+
+void HostRegistryRemove(const void* p) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg.erase((uintptr_t)p);
+}
+
+bool HostRegistryCovers(const void* p, size_t bytes) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound(a);  // the first range starting after a
+    if (it == g_reg.begin()) return false;
+    --it;
+    return a - it->first <= it->second && bytes <= it->second - (a - it->first);
+}
+
+uint64_t HostRegisteredCalls() { return g_reg_calls.load(std::memory_order_relaxed); }
+
 // ---------------------------------------------------------------- HostPath --
 // wait for an event by polling it: a blocking synchronisation may sleep and
 // pay a wake-up on every piece
@@ -163,6 +193,7 @@ HostPath::~HostPath() {
         (void)hipEventDestroy(in_done_[i]);
     }
     for (hipEvent_t e : ar_done_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : h2d_done_) (void)hipEventDestroy(e);
     if (pin_small_) (void)hipHostFree(pin_small_);
     if (small_done_) (void)hipEventDestroy(small_done_);
     if (dev_small_) (void)hipFree(dev_small_);
@@ -303,6 +334,74 @@ void HostPath::AllreduceSmall(Communicator* c, char* h, size_t count, size_t S, 
     Copy(h, pin_small_, S);
 }
 
+namespace {
+// the intersection of piece [lo, hi) with every Split chunk, relative to lo
+void piece_ranges(uint64_t lo, uint64_t hi, int n, const int64_t* cb, const int64_t* ce, size_t esz, uint64_t* roff,
+                  uint64_t* rlen) {
+    for (int q = 0; q < n; ++q) {
+        const uint64_t a = std::max<uint64_t>(lo, (uint64_t)cb[q] * esz);
+        const uint64_t b = std::min<uint64_t>(hi, (uint64_t)ce[q] * esz);
+        roff[q] = b > a ? a - lo : 0;
+        rlen[q] = b > a ? b - a : 0;
+    }
+}
+}  // namespace
+
+// A registered buffer is DMA-able in place (57 GB/s either way on the box,
+// the rate of hipHostMalloc memory): no pinned slots, no copy pool, no drain
+// thread.  Every piece's H2D, allreduce and D2H is queued up front on the
+// three streams, chained by per-piece events, and the caller spins once on the
+// last D2H.  Pieces and collectives are the pipeline's (HostPieceBounds, the
+// same AllreduceRanges calls), so ranks with and without a registered buffer
+// issue matching collectives and every element is folded in its chunk's ring
+// order either way.
+void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int dtype, int op,
+                                   hipStream_t comm_stream, const std::vector<uint64_t>& bounds, const int64_t* cb,
+                                   const int64_t* ce) {
+    const int n = c->size();
+    const size_t esz = rdc_dtype_size(dtype);
+    const size_t S = count * esz;
+    const int K = (int)bounds.size() - 1;
+    Reserve(0, S, K, comm_stream);
+    while ((int)h2d_done_.size() < K) {
+        hipEvent_t e;
+        hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+        h2d_done_.push_back(e);
+    }
+    g_reg_calls.fetch_add(1, std::memory_order_relaxed);
+    if (K == 1) {  // the inline piece's collective: the whole buffer
+        hip_check(hipMemcpyAsync(dev_, h, S, hipMemcpyHostToDevice, comm_stream), "H2D");
+        c->Allreduce(dev_, count, dtype, op, comm_stream);
+        hip_check(hipMemcpyAsync(h, dev_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
+        hip_check(hipEventRecord(in_done_[0], comm_stream), "record");
+        SpinEvent(in_done_[0], "host allreduce");
+        c->RaiseIfError(c->HostErrorWord());
+        return;
+    }
+    try {
+        for (int k = 0; k < K; ++k) {
+            const uint64_t lo = bounds[(size_t)k], hi = bounds[(size_t)k + 1];
+            uint64_t roff[RDC_MAX_RANKS], rlen[RDC_MAX_RANKS];
+            piece_ranges(lo, hi, n, cb, ce, esz, roff, rlen);
+            hip_check(hipMemcpyAsync(dev_ + lo, h + lo, hi - lo, hipMemcpyHostToDevice, h2d_), "H2D");
+            hip_check(hipEventRecord(h2d_done_[(size_t)k], h2d_), "record");
+            hip_check(hipStreamWaitEvent(comm_stream, h2d_done_[(size_t)k], 0), "wait");
+            c->AllreduceRanges(dev_ + lo, roff, rlen, dtype, op, comm_stream);
+            hip_check(hipEventRecord(ar_done_[(size_t)k], comm_stream), "record");
+            hip_check(hipStreamWaitEvent(d2h_, ar_done_[(size_t)k], 0), "wait");
+            hip_check(hipMemcpyAsync(h + lo, dev_ + lo, hi - lo, hipMemcpyDeviceToHost, d2h_), "D2H");
+        }
+        hip_check(hipEventRecord(in_done_[0], d2h_), "record");
+    } catch (...) {
+        // no DMA into or out of the caller's buffer may outlive the call
+        (void)hipStreamSynchronize(h2d_);
+        (void)hipStreamSynchronize(d2h_);
+        throw;
+    }
+    SpinEvent(in_done_[0], "host allreduce");
+    c->Check(comm_stream);  // a device-side failure surfaces here
+}
+
 void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, int op, hipStream_t comm_stream) {
     const int n = c->size();
     if (n == 1 || count == 0) return;
@@ -337,6 +436,10 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
     // ring order: a piece's allreduce gets the chunk ranges it intersects.
     const std::vector<uint64_t> bounds = HostPieceBounds(S);
     const int K = (int)bounds.size() - 1;
+    if (HostRegistryCovers(h, S)) {
+        AllreduceRegistered(c, h, count, dtype, op, comm_stream, bounds, cb, ce);
+        return;
+    }
     uint64_t sl = 0;  // the largest piece: the pinned slot size
     for (int k = 0; k < K; ++k) sl = std::max<uint64_t>(sl, bounds[(size_t)k + 1] - bounds[(size_t)k]);
     Reserve((size_t)sl, S, K, comm_stream);
@@ -378,14 +481,8 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
             const uint64_t lo = bounds[(size_t)k], hi = bounds[(size_t)k + 1], bytes = hi - lo;
             d.off[0] = lo;
             d.len[0] = bytes;
-            // the piece's intersection with every Split chunk, relative to lo
             uint64_t roff[RDC_MAX_RANKS], rlen[RDC_MAX_RANKS];
-            for (int q = 0; q < n; ++q) {
-                const uint64_t a = std::max<uint64_t>(lo, (uint64_t)cb[q] * esz);
-                const uint64_t b = std::min<uint64_t>(hi, (uint64_t)ce[q] * esz);
-                roff[q] = b > a ? a - lo : 0;
-                rlen[q] = b > a ? b - a : 0;
-            }
+            piece_ranges(lo, hi, n, cb, ce, esz, roff, rlen);
             // the slot's previous H2D has been consumed before we overwrite it
             const double t0 = tracing() ? trace_now() : 0;
             if (k >= kSlots) hip_check(hipEventSynchronize(in_done_[slot]), "wait H2D slot");

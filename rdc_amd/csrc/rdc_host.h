@@ -42,8 +42,17 @@ size_t HostInlineBytes();
 // the pipeline's piece boundaries for an S-byte host buffer: {0, ..., S}
 std::vector<uint64_t> HostPieceBounds(uint64_t S);
 
-// fixed pool of memcpy threads; Run(n, f) calls f(0..n-1) across the pool
-// and the caller, returning when all are done
+// Host ranges page-locked through RdcNewBuffer(..., pinned = 1) (rdc/buffer.py:
+// 34-38, the reference's registered Buffer).  A host allreduce whose whole
+// buffer lies in one of them skips the pinned slots, the copy pool and the
+// drain thread: the DMA engines read and write the user's pages directly
+// (HostPath::AllreduceRegistered).  The caller keeps a registered range alive
+// until RdcDelBuffer, as with any registration.
+void HostRegistryAdd(const void* p, size_t bytes);
+void HostRegistryRemove(const void* p);
+bool HostRegistryCovers(const void* p, size_t bytes);
+// host allreduces of this process that took the registered path
+uint64_t HostRegisteredCalls();
 
 class HostPath {
 public:
@@ -70,6 +79,11 @@ private:
     static constexpr size_t kSmall = (size_t)1 << 20;
     void AllreduceSmall(Communicator* c, char* host, size_t count, size_t bytes, int dtype, int op,
                         hipStream_t comm_stream);
+    // the same pieces and collectives as the pipeline, with the H2D / D2H DMA
+    // straight from / into a registered user buffer, all stream-ordered
+    void AllreduceRegistered(Communicator* c, char* host, size_t count, int dtype, int op, hipStream_t comm_stream,
+                             const std::vector<uint64_t>& bounds, const int64_t* cb, const int64_t* ce);
+    std::vector<hipEvent_t> h2d_done_;  // registered path: one per piece
 
     int device_;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;

@@ -222,12 +222,32 @@ def main():
                 # host_offset: the host buffer starts that many bytes past an
                 # aligned allocation (element-aligned, not 16-B aligned)
                 ho = c.get("host_offset", 0)
-                backing = np.empty(nbytes + ho + 64, dtype=np.uint8)
+                # pinned: True = every rank's buffer lies in a registered
+                # RdcNewBuffer(pinned=1) range (DMA in place), "even" = even
+                # ranks only (registered and staged ranks in one collective)
+                pin = c.get("pinned")
+                bh = None
+                if pin is True or (pin == "even" and rank % 2 == 0):
+                    import mmap
+                    span = (nbytes + ho + mmap.PAGESIZE - 1) // mmap.PAGESIZE * mmap.PAGESIZE
+                    backing = np.frombuffer(mmap.mmap(-1, span), dtype=np.uint8)
+                    bh = ctypes.c_void_p()
+                    check_call(_LIB.RdcNewBuffer(ctypes.byref(bh), backing.ctypes.data_as(ctypes.c_void_p), span, 1))
+                    reg0 = ctypes.c_uint64()
+                    check_call(_LIB.RdcCommGetParam(comm.handle, b"host_registered_calls", ctypes.byref(reg0)))
+                else:
+                    backing = np.empty(nbytes + ho + 64, dtype=np.uint8)
                 host = backing[ho: ho + nbytes]
                 host[:] = buf[pad: pad + nbytes].cpu().numpy()
                 check_call(_LIB.RdcAllreduce(host.ctypes.data_as(ctypes.c_void_p), count, dtype, c["op"], None,
                                              None))
                 buf[pad: pad + nbytes] = torch.from_numpy(host.copy()).cuda()
+                if bh is not None:
+                    reg1 = ctypes.c_uint64()
+                    check_call(_LIB.RdcCommGetParam(comm.handle, b"host_registered_calls", ctypes.byref(reg1)))
+                    open(os.path.join(outdir, "case%d_rank%d.reg" % (i, rank)), "w").write(
+                        str(reg1.value - reg0.value))
+                    check_call(_LIB.RdcDelBuffer(bh))
         log("rank", rank, "case", i, "launched")
         comm.check(sp)
         if c.get("last_launch"):

@@ -561,6 +561,41 @@ def test_mp_host_size_sweep(world):
             assert bad.size == 0, "%r rank %d: %d bytes differ, first at byte %d" % (c, r, bad.size, bad[0])
 
 
+REGISTERED_BYTES = [(1 << 20) + 4, (3 << 20) + 7, 16777217, (33 << 20) + 4097, (64 << 20) + 4095]
+
+
+@pytest.mark.parametrize("world,pinned", [(2, True), (3, True), (3, "even")])
+def test_mp_host_registered(world, pinned):
+    """Host buffers inside a registered RdcNewBuffer(pinned=1) range
+    (rdc/buffer.py:34-38) DMA in place (HostPath::AllreduceRegistered): the
+    inline piece, the pipeline with and without the ramp, ragged last pieces,
+    a buffer starting 4 B into its registered range, and registered ranks
+    beside staged ones in one collective ("even").  Every byte against the
+    oracle; the registered ranks report that they took the in-place path."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = []
+    for k, nb in enumerate(REGISTERED_BYTES):
+        cases.append({"count": nb, "dtype": 1, "op": (0, 2)[k % 2], "kind": "host_allreduce", "pinned": pinned,
+                      "seed": 0x5EEDC000 + k})
+        cases.append({"count": nb // 4 + 1, "dtype": 6, "op": 2, "kind": "host_allreduce", "pinned": pinned,
+                      "host_offset": 4 * (k % 2), "seed": 0x5EEDD000 + k})
+    tmp = run_mp(world, cases, timeout=400)
+    for i, c in enumerate(cases):
+        want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            w = np.frombuffer(want[r].tobytes(), dtype=np.uint8)
+            assert got.shape == w.shape, (c, r)
+            bad = np.nonzero(got != w)[0]
+            assert bad.size == 0, "%r rank %d: %d bytes differ, first at byte %d" % (c, r, bad.size, bad[0])
+            reg = os.path.join(tmp, "case%d_rank%d.reg" % (i, r))
+            if pinned is True or r % 2 == 0:
+                assert open(reg).read() == "1", (c, r)
+            else:
+                assert not os.path.exists(reg)
+
+
 def fuzz_cases(seed, world, n=40):
     """Seeded random sizes (log-uniform, 1 element .. 24 Mi elements), (dtype,
     op) pairs with reference semantics, schedules, per-rank misalignment,

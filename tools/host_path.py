@@ -4,6 +4,8 @@ allreduce, D2H copy, synchronise (RdcAllreduce on a numpy buffer).
 
     python -m torch.distributed.run --nproc-per-node N tools/host_path.py [bytes] [iters]
     python tools/host_path.py [bytes] [iters]          # N = 1: H2D + reduce + D2H
+    RDC_BENCH_PINNED=1 ...: the buffer is a registered RdcNewBuffer(pinned=1)
+    range (page-aligned mmap), so the library DMAs it in place
 
 Prints one JSON line (rank 0) with GB/s = S / t per call (max over ranks).
 """
@@ -28,12 +30,23 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
     count = S // 4
+    pinned = os.environ.get("RDC_BENCH_PINNED", "0") == "1" and world > 1
     host = np.random.default_rng(rank).standard_normal(count).astype(np.float32)
+    reg = None
+    if pinned:
+        import mmap
+        span = (S + mmap.PAGESIZE - 1) // mmap.PAGESIZE * mmap.PAGESIZE
+        backing = np.frombuffer(mmap.mmap(-1, span), dtype=np.uint8)
+        backing[:S].view(np.float32)[:] = host
+        host = backing[:S].view(np.float32)
     p = host.ctypes.data_as(ctypes.c_void_p)
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
         rdc_amd.init([])
+        if pinned:
+            reg = ctypes.c_void_p()
+            check_call(_LIB.RdcNewBuffer(ctypes.byref(reg), ctypes.c_void_p(backing.ctypes.data), span, 1))
 
         def call():
             check_call(_LIB.RdcAllreduce(p, count, 6, 2, None, None))
@@ -68,9 +81,12 @@ def main():
         print(json.dumps({"host_path": True, "n": world, "bytes": S, "ms_per_call": round(dt * 1e3, 4),
                           "us_per_call_mean": round(dt * 1e6, 2), "us_per_call_median_rank0": round(med_us, 2),
                           "us_per_call_max_rank0": round(max_us, 1),
-                          "GBps": round(S / dt / 1e9, 3), "memory": "pageable numpy"}), flush=True)
+                          "GBps": round(S / dt / 1e9, 3),
+                          "memory": "registered (RdcNewBuffer pinned)" if pinned else "pageable numpy"}), flush=True)
     if world > 1:
         dist.barrier()
+        if reg is not None:
+            check_call(_LIB.RdcDelBuffer(reg))
         rdc_amd.finalize()
 
 
