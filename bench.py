@@ -225,6 +225,29 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
         del hb
     else:
         out.setdefault("skipped", []).append("host_64MiB")
+    # the same 64 MiB in a registered RdcNewBuffer(pinned=1) range: the DMA
+    # engines read and write the caller's pages in place (no copy in)
+    if budget is None or budget.left() >= 15:
+        import mmap
+        mm = mmap.mmap(-1, 64 << 20)
+        hb = np.frombuffer(mm, dtype=np.float32)
+        hb[:] = 1.0
+        reg = ctypes.c_void_p()
+        check_call(lib.RdcNewBuffer(ctypes.byref(reg), ctypes.c_void_p(hb.ctypes.data), hb.nbytes, 1))
+        try:
+            ph = ctypes.c_void_p(hb.ctypes.data)
+            ms = timed_ms(lambda: check_call(lib.RdcAllreduce(ph, hb.size, 6, 2, None, None)), comm, sp, dist, torch,
+                          5, warm=2, synchronous=True)
+        finally:
+            check_call(lib.RdcDelBuffer(reg))
+        e = entry(ms, hb.nbytes, "64 MiB float32 allreduce of HOST memory registered with RdcNewBuffer(pinned=1) "
+                  "via RdcAllreduce: H2D, allreduce, D2H in place, pipelined (PCIe-inclusive; synchronous, max "
+                  "over ranks)", 5)
+        e["algbw_GBps_pcie_inclusive"] = round(hb.nbytes / (ms * 1e-3) / 1e9, 2)
+        out["host_64MiB_registered"] = e
+        del hb
+    else:
+        out.setdefault("skipped", []).append("host_64MiB_registered")
     # cfg2's 256 MiB fp32 buffer and the sizes below it (prefixes of one
     # buffer): where the mesh's per-launch fill / drain and the one-shot
     # hand-off decide the rate, for the size thresholds at this rank count

@@ -378,11 +378,16 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
         c->RaiseIfError(c->HostErrorWord());
         return;
     }
+    // RDC_HOST_REG_AHEAD=a > 0: piece k's H2D waits for piece k-a's allreduce
+    // (stream-ordered), so the input DMA runs at most a pieces ahead
+    static const int ahead = env_int("RDC_HOST_REG_AHEAD", 0);
     try {
         for (int k = 0; k < K; ++k) {
             const uint64_t lo = bounds[(size_t)k], hi = bounds[(size_t)k + 1];
             uint64_t roff[RDC_MAX_RANKS], rlen[RDC_MAX_RANKS];
             piece_ranges(lo, hi, n, cb, ce, esz, roff, rlen);
+            if (ahead > 0 && k >= ahead)
+                hip_check(hipStreamWaitEvent(h2d_, ar_done_[(size_t)(k - ahead)], 0), "wait");
             hip_check(hipMemcpyAsync(dev_ + lo, h + lo, hi - lo, hipMemcpyHostToDevice, h2d_), "H2D");
             hip_check(hipEventRecord(h2d_done_[(size_t)k], h2d_), "record");
             hip_check(hipStreamWaitEvent(comm_stream, h2d_done_[(size_t)k], 0), "wait");

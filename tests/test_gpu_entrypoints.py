@@ -79,6 +79,7 @@ def test_bench_torchrun_two_ranks():
     ex = out["extra_configs"]
     assert ex["cfg1_host_4KiB"]["us_per_call"] > 0 and ex["cfg5_buckets"]["ms_per_step"] > 0
     assert ex["host_64MiB"]["algbw_GBps_pcie_inclusive"] > 0, ex.get("host_64MiB")
+    assert ex["host_64MiB_registered"]["algbw_GBps_pcie_inclusive"] > 0, ex.get("host_64MiB_registered")
     chk = out["oracle_check"]
     assert all(chk.get(k) is True for k in PARITY_KEYS), chk
     assert out["extras_skipped"] == [] and "parity_checks" in out["extras_wall_s"], out["extras_wall_s"]
