@@ -71,6 +71,7 @@ def main():
         per.append(time.perf_counter() - t1)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
+    per_call_ms = [round(x * 1e3, 3) for x in per]
     per.sort()
     med_us, max_us = per[len(per) // 2] * 1e6, per[-1] * 1e6
     if world > 1:
@@ -81,6 +82,7 @@ def main():
         print(json.dumps({"host_path": True, "n": world, "bytes": S, "ms_per_call": round(dt * 1e3, 4),
                           "us_per_call_mean": round(dt * 1e6, 2), "us_per_call_median_rank0": round(med_us, 2),
                           "us_per_call_max_rank0": round(max_us, 1),
+                          "per_call_ms_rank0": per_call_ms if os.environ.get("RDC_BENCH_PER_CALL") else None,
                           "GBps": round(S / dt / 1e9, 3),
                           "memory": "registered (RdcNewBuffer pinned)" if pinned else "pageable numpy"}), flush=True)
     if world > 1:
