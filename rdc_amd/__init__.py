@@ -12,12 +12,12 @@ from .core import (DTYPE_ENUM__, Op, allgather, allreduce, allreduce_coalesced, 
                    get_rank, get_world_size, init, is_distributed, recv, send, tracker_print)
 from .comm import (ALGO_AUTO, ALGO_MESH, ALGO_ONESHOT, ALGO_RING, ALGO_TREE, WS_ERROR, WS_FINISHED,  # noqa: F401
                    WS_PENDING, Comm, WorkComp, create_group, get_comm, init_group, new_comm)
-from .buffer import Buffer  # noqa: F401
+from .buffer import Buffer, PinnedArray, pinned_empty  # noqa: F401
 from .device import dtype_enum, fill_, reduce_  # noqa: F401
 
 __all__ = [
     "Op", "init", "finalize", "get_rank", "get_world_size", "is_distributed", "tracker_print",
     "get_processor_name", "barrier", "broadcast", "allreduce", "allreduce_coalesced", "allgather", "Comm", "new_comm", "get_comm",
-    "Buffer", "WorkComp", "send", "recv",
+    "Buffer", "PinnedArray", "pinned_empty", "WorkComp", "send", "recv",
     "init_group", "create_group", "reduce_", "fill_", "dtype_enum", "RdcError",
 ]

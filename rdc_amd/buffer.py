@@ -80,3 +80,33 @@ class Buffer(object):
 
     def bytes(self):
         return self.to_numpy().tobytes()
+
+
+class PinnedArray(np.ndarray):
+    """An ndarray over page-aligned host memory registered with the HIP
+    runtime for as long as the array or any view of it lives (see
+    ``pinned_empty``)."""
+
+    def __array_finalize__(self, obj):
+        self._rdc_buf = getattr(obj, "_rdc_buf", None)
+
+
+def pinned_empty(shape, dtype=np.float32):
+    """A host array whose memory is an anonymous mmap registered through
+    ``RdcNewBuffer(..., pinned=1)`` (the reference's pinned Buffer,
+    include/transport/buffer.h:61,91).  ``allreduce`` reduces such an array in
+    place (``ravel`` gives a view of its memory, rdc/core.py:196-199), and the
+    library DMAs it straight from and into these pages instead of copying it
+    through pinned staging memory.  The registration ends with the last
+    reference to the array or its views."""
+    import mmap
+    dtype = np.dtype(dtype)
+    count = int(np.prod(shape, dtype=np.int64)) if np.ndim(shape) else int(shape)
+    nbytes = count * dtype.itemsize
+    span = max(1, (nbytes + mmap.PAGESIZE - 1) // mmap.PAGESIZE) * mmap.PAGESIZE
+    mem = np.frombuffer(mmap.mmap(-1, span), dtype=np.uint8)
+    mem[:] = 0  # fault every page in before it is pinned
+    buf = Buffer(mem, pinned=True)
+    arr = mem[:nbytes].view(dtype).reshape(shape).view(PinnedArray)
+    arr._rdc_buf = buf
+    return arr

@@ -144,6 +144,23 @@ def main():
     torch.cuda.synchronize()
     check(bool(torch.all(t2 == float(world - 1))), "device allreduce via rdc.allreduce")
 
+    # a registered host array (rdc_amd.pinned_empty): reduced in place, and the
+    # library DMAs its pages directly (host_registered_calls counts the calls)
+    import ctypes
+    from rdc_amd._lib import _LIB, check_call
+    hm = rdc.get_comm("main").handle
+    reg0, reg1 = ctypes.c_uint64(), ctypes.c_uint64()
+    check_call(_LIB.RdcCommGetParam(hm, b"host_registered_calls", ctypes.byref(reg0)))
+    for count in (1 << 20, (6 << 20) + 3):  # one 4 MiB piece; a 24 MiB + 12 B pipeline
+        pa = rdc.pinned_empty(count, np.float32)
+        pa[:] = rank + np.arange(count) % 7
+        res = rdc.allreduce(pa, rdc.Op.SUM)
+        want = (world * (np.arange(count) % 7) + world * (world - 1) // 2).astype(np.float32)
+        check(np.shares_memory(res, pa) and np.array_equal(pa, want), "pinned_empty SUM count=%d" % count)
+        del res, pa
+    check_call(_LIB.RdcCommGetParam(hm, b"host_registered_calls", ctypes.byref(reg1)))
+    check(reg1.value - reg0.value == 2, "registered host calls: %d" % (reg1.value - reg0.value))
+
     rdc.finalize()
     print("rank %d: python surface OK" % rank, flush=True)
 

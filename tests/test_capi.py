@@ -157,3 +157,18 @@ def test_cpp_header_compiles():
     os.unlink(exe)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "known-answer OK" in p.stdout
+
+
+def test_pinned_empty_is_reduced_in_place():
+    """rdc_amd.pinned_empty: page-aligned host memory behind a pinned Buffer
+    (registration itself needs a GPU); allreduce's copy rule (rdc/core.py:
+    196-199) keeps it in place, so the registered pages are what the library
+    DMAs; views keep the registration alive."""
+    import numpy as np
+    import rdc_amd
+    a = rdc_amd.pinned_empty((3, 5), np.float64)
+    assert isinstance(a, rdc_amd.PinnedArray) and a.shape == (3, 5) and a.dtype == np.float64
+    assert a.ctypes.data % 4096 == 0 and np.all(a == 0)
+    flat = a.ravel()
+    assert flat.base is not a.base and np.shares_memory(flat, a)  # not copied by host_allreduce
+    assert flat._rdc_buf is a._rdc_buf is not None and a._rdc_buf.pinned
