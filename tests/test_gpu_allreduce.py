@@ -599,7 +599,8 @@ def test_mp_host_registered(world, pinned):
 def fuzz_cases(seed, world, n=40):
     """Seeded random sizes (log-uniform, 1 element .. 24 Mi elements), (dtype,
     op) pairs with reference semantics, schedules, per-rank misalignment,
-    host buffers (service, zero-copy, inline piece, pipeline), broadcasts
+    host buffers (service, zero-copy, inline piece, pipeline; pageable or
+    in registered ranges on all or some ranks), broadcasts
     from random roots and coalesced lists of random buckets."""
     import random
     rng = random.Random(seed)
@@ -614,7 +615,10 @@ def fuzz_cases(seed, world, n=40):
             dt, op = rng.choice(pairs)
             cases.append({"count": max(1, int(2 ** rng.uniform(0, 24))), "dtype": dt, "op": op,
                           "kind": "host_allreduce", "seed": 0x5EED0000 + sd,
-                          "host_offset": esz[dt] * rng.choice([0, 0, 1, 3])})
+                          "host_offset": esz[dt] * rng.choice([0, 0, 1, 3]),
+                          # registered ranges (all / even ranks), drawn from a
+                          # separate stream so the other cases stay as they were
+                          "pinned": random.Random(sd).choice([None, None, True, "even"])})
         elif kind == "allreduce":
             dt, op = rng.choice(pairs)
             count = max(1, int(2 ** rng.uniform(0, 24.6)))
