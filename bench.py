@@ -602,6 +602,19 @@ def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
 
 def main():
     args = parse()
+    # a rehearsal of N > 4 ranks on a 1-GPU box: fewer hardware queues per
+    # process, as rdc_amd.launcher gives workers that share a GPU (the GPU's
+    # scheduler otherwise time-slices 4 x N queues, ~10 ms per slice;
+    # profiles/r03/host_n8_queues/).  Before HIP starts (launcher.py is loaded by
+    # path: importing the package would load the HIP library); never with a GPU per rank.
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_rdc_launcher", os.path.join(os.path.dirname(os.path.abspath(__file__)), "rdc_amd", "launcher.py"))
+    launcher = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(launcher)
+    q = launcher.hw_queues_per_process(int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    if q is not None and launcher.kfd_gpu_count() == 1 and "GPU_MAX_HW_QUEUES" not in os.environ:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(q)
     import torch
     import rdc_amd
     from rdc_amd._lib import _LIB, check_call
@@ -909,6 +922,7 @@ def main():
     if world > 1:
         out["busbw_GBps"] = round(value, 2)
         out["ranks_share_gpu"] = shared
+        out["gpu_max_hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")  # None: HIP's default (4)
     if ring_cmp is not None:
         rb = S / (ring_cmp * 1e-3) / 1e9 * 2 * (world - 1) / world
         out["ring_schedule"] = {"ms_per_step": round(ring_cmp, 4), "busbw_GBps": round(rb, 2),

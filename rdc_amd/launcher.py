@@ -107,6 +107,41 @@ def _visible_count():
     return n
 
 
+def kfd_gpu_count(sysfs="/sys"):
+    """GPUs in the KFD topology this process can read (None when unreadable)."""
+    base = os.path.join(sysfs, "class", "kfd", "kfd", "topology", "nodes")
+    try:
+        nodes = [x for x in os.listdir(base) if x.isdigit()]
+    except OSError:
+        return None
+    n = 0
+    for nd in nodes:
+        props = _read(os.path.join(base, nd, "properties")) or ""
+        for line in props.splitlines():
+            kv = line.split(None, 1)
+            if len(kv) == 2 and kv[0] == "simd_count" and kv[1].strip().isdigit() and int(kv[1]) > 0:
+                n += 1
+    return n or None
+
+
+# Hardware queues the GPU's scheduler maps at once, summed over the processes
+# on it.  HIP gives every process GPU_MAX_HW_QUEUES (default 4) queues; with 8
+# processes on one GPU (32 queues) the scheduler time-slices them, and a
+# collective spinning on a peer whose queue is not mapped waits ~10 ms for the
+# next slice: host allreduces of 4 KiB took 10.7 ms per call and of 64 MiB
+# 253 ms, against 62 us and 18.4 ms with 2 queues per process
+# (profiles/r03/host_n8_queues/).
+QUEUE_BUDGET = 16
+
+
+def hw_queues_per_process(ranks_per_gpu):
+    """GPU_MAX_HW_QUEUES for a process that shares its GPU with
+    ranks_per_gpu - 1 others (None: leave HIP's default of 4)."""
+    if ranks_per_gpu * 4 <= QUEUE_BUDGET:
+        return None
+    return max(1, QUEUE_BUDGET // ranks_per_gpu)
+
+
 def gpu_local_cpus(ordinal, sysfs="/sys"):
     """CPUs local to HIP device `ordinal`: the KFD topology's GPU nodes this
     process can read, in node order (HIP's device order); a node's
@@ -151,6 +186,11 @@ def worker_env(args, rank, port, ngpu):
         "RDC_WORLD_SIZE": str(args.num_workers),
         "LOCAL_RANK": str(rank % max(1, ngpu)),
     })
+    # several workers on one GPU: fewer hardware queues each, so the GPU's
+    # scheduler maps every worker's queues at once (unless the user chose)
+    q = hw_queues_per_process(-(-args.num_workers // max(1, ngpu)))
+    if q is not None and "GPU_MAX_HW_QUEUES" not in os.environ:
+        env["GPU_MAX_HW_QUEUES"] = str(q)
     # torchrun-style names would override the rdc ones inside RdcInit's
     # fallbacks only where rdc names are absent; drop stale ones anyway
     for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):

@@ -269,3 +269,21 @@ def test_launcher_numa_bind_confines_workers(tmp_path):
                         str(prog)], cwd=ROOT, capture_output=True, text=True, timeout=60)
     assert p.returncode == 0, p.stderr
     assert p.stdout.count("cpus") == 2
+
+
+def test_launcher_queue_budget(tmp_path, monkeypatch):
+    """Workers sharing a GPU get fewer hardware queues each (rdc_amd/launcher.py
+    hw_queues_per_process): up to 4 per GPU keep HIP's default, 8 get 2, 16 get
+    1; a user's GPU_MAX_HW_QUEUES is kept; the KFD GPU count from sysfs."""
+    import argparse
+    from rdc_amd.launcher import hw_queues_per_process, kfd_gpu_count, worker_env
+    assert [hw_queues_per_process(k) for k in (1, 2, 4, 5, 8, 16, 32)] == [None, None, None, 3, 2, 1, 1]
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
+    a = argparse.Namespace(host_ip="127.0.0.1", num_workers=8)
+    assert worker_env(a, 3, 1234, 1)["GPU_MAX_HW_QUEUES"] == "2"
+    assert "GPU_MAX_HW_QUEUES" not in worker_env(a, 3, 1234, 8)
+    assert "GPU_MAX_HW_QUEUES" not in worker_env(argparse.Namespace(host_ip="127.0.0.1", num_workers=4), 0, 1, 1)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    assert worker_env(a, 3, 1234, 1)["GPU_MAX_HW_QUEUES"] == "4"
+    _fake_sysfs(tmp_path, [(128, "0-3"), (136, "4-7")])
+    assert kfd_gpu_count(str(tmp_path)) == 2 and kfd_gpu_count(str(tmp_path / "missing")) is None
