@@ -259,6 +259,12 @@ def run_mp(world, cases, timeout=240, env_extra=None):
     # `world` ranks on GPU 0) unless a test forces RDC_NBLOCKS
     env.update({"RDC_DEVICE": "0", "RDC_SCRATCH_BYTES": "64M"})
     env.update(env_extra or {})
+    # every rank on GPU 0: the hardware-queue budget rdc_amd.launcher applies
+    # to workers that share a GPU (8 ranks -> 2 queues each)
+    from rdc_amd.launcher import hw_queues_per_process
+    q = hw_queues_per_process(world)
+    if q is not None and env.get("RDC_DEVICE") != "rank" and "GPU_MAX_HW_QUEUES" not in env:
+        env["GPU_MAX_HW_QUEUES"] = str(q)
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), str(r), str(world),
                                str(port), tmp, cf], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
              for r in range(world)]
