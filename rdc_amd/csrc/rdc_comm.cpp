@@ -517,6 +517,21 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         for (int q = 0; q < c->n_; ++q) same += strncmp(all[(size_t)p].pci, all[(size_t)q].pci, sizeof(mine.pci)) == 0;
         c->share_max_ = std::max(c->share_max_, same);
     }
+    {   // more than 16 hardware queues on one GPU are time-sliced by its
+        // scheduler (~10 ms slices): a collective spinning on a peer whose
+        // queue is not mapped waits a slice (DESIGN.md §4, round 3 session 3)
+        const char* q = getenv("GPU_MAX_HW_QUEUES");
+        const int per = q && *q ? atoi(q) : 4;
+        static bool warned = false;
+        if (c->rank_ == 0 && !warned && c->share_max_ * per > 16) {
+            warned = true;
+            fprintf(stderr,
+                    "rdc: %d ranks share one GPU with GPU_MAX_HW_QUEUES=%d each; the GPU time-slices that many "
+                    "queues and collectives wait ~10 ms per slice. Set GPU_MAX_HW_QUEUES=%d (rdc_amd.launcher "
+                    "does)\n",
+                    c->share_max_, per, std::max(1, 16 / c->share_max_));
+        }
+    }
     // schedules and shapes an earlier Autotune of this node measured for this
     // rank count, CU count and ranks per GPU (RDC_TUNE_FILE, rank 0's table)
     const std::vector<TuneEntry> tuned = tune_file().empty() ? std::vector<TuneEntry>() : shared_tune_table(bs);
