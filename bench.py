@@ -613,7 +613,7 @@ def main():
     launcher = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(launcher)
     q = launcher.hw_queues_per_process(int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
-    if q is not None and launcher.kfd_gpu_count() == 1 and "GPU_MAX_HW_QUEUES" not in os.environ:
+    if q is not None and launcher.visible_gpu_count() == 1 and "GPU_MAX_HW_QUEUES" not in os.environ:
         os.environ["GPU_MAX_HW_QUEUES"] = str(q)
     import torch
     import rdc_amd

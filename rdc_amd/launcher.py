@@ -107,6 +107,19 @@ def _visible_count():
     return n
 
 
+def visible_gpu_count(dev="/dev/dri"):
+    """GPUs this process may use, without initialising HIP: the
+    *_VISIBLE_DEVICES list when one is set, else the render nodes under
+    /dev/dri; None when neither tells."""
+    n = _visible_count()
+    if n is not None:
+        return n
+    try:
+        return len([d for d in os.listdir(dev) if d.startswith("renderD")]) or None
+    except OSError:
+        return None
+
+
 def kfd_gpu_count(sysfs="/sys"):
     """GPUs in the KFD topology this process can read (None when unreadable)."""
     base = os.path.join(sysfs, "class", "kfd", "kfd", "topology", "nodes")

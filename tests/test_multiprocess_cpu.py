@@ -276,7 +276,7 @@ def test_launcher_queue_budget(tmp_path, monkeypatch):
     hw_queues_per_process): up to 4 per GPU keep HIP's default, 8 get 2, 16 get
     1; a user's GPU_MAX_HW_QUEUES is kept; the KFD GPU count from sysfs."""
     import argparse
-    from rdc_amd.launcher import hw_queues_per_process, kfd_gpu_count, worker_env
+    from rdc_amd.launcher import hw_queues_per_process, kfd_gpu_count, visible_gpu_count, worker_env
     assert [hw_queues_per_process(k) for k in (1, 2, 4, 5, 8, 16, 32)] == [None, None, None, 3, 2, 1, 1]
     monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
     a = argparse.Namespace(host_ip="127.0.0.1", num_workers=8)
@@ -287,3 +287,12 @@ def test_launcher_queue_budget(tmp_path, monkeypatch):
     assert worker_env(a, 3, 1234, 1)["GPU_MAX_HW_QUEUES"] == "4"
     _fake_sysfs(tmp_path, [(128, "0-3"), (136, "4-7")])
     assert kfd_gpu_count(str(tmp_path)) == 2 and kfd_gpu_count(str(tmp_path / "missing")) is None
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    for name in ("card1", "renderD128", "renderD136"):
+        (dri / name).write_text("")
+    assert visible_gpu_count(str(dri)) == 2 and visible_gpu_count(str(tmp_path / "none")) is None
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3")
+    assert visible_gpu_count(str(dri)) == 1
