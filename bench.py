@@ -613,7 +613,8 @@ def main():
     launcher = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(launcher)
     q = launcher.hw_queues_per_process(int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
-    if q is not None and launcher.visible_gpu_count() == 1 and "GPU_MAX_HW_QUEUES" not in os.environ:
+    if q is not None and launcher.visible_gpu_count() == 1 and \
+            launcher.queues_over_budget(os.environ.get("GPU_MAX_HW_QUEUES"), q):
         os.environ["GPU_MAX_HW_QUEUES"] = str(q)
     import torch
     import rdc_amd

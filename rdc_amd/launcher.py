@@ -155,6 +155,16 @@ def hw_queues_per_process(ranks_per_gpu):
     return max(1, QUEUE_BUDGET // ranks_per_gpu)
 
 
+def queues_over_budget(current, q):
+    """True when GPU_MAX_HW_QUEUES (unset = HIP's 4) exceeds the budget q: a
+    value above it only buys the scheduler's time slices, so it is lowered
+    (GPU boxes may export the default 4 explicitly)."""
+    try:
+        return int(current) > q if current not in (None, "") else 4 > q
+    except ValueError:
+        return True
+
+
 def gpu_local_cpus(ordinal, sysfs="/sys"):
     """CPUs local to HIP device `ordinal`: the KFD topology's GPU nodes this
     process can read, in node order (HIP's device order); a node's
@@ -200,9 +210,9 @@ def worker_env(args, rank, port, ngpu):
         "LOCAL_RANK": str(rank % max(1, ngpu)),
     })
     # several workers on one GPU: fewer hardware queues each, so the GPU's
-    # scheduler maps every worker's queues at once (unless the user chose)
+    # scheduler maps every worker's queues at once (a lower setting is kept)
     q = hw_queues_per_process(-(-args.num_workers // max(1, ngpu)))
-    if q is not None and "GPU_MAX_HW_QUEUES" not in os.environ:
+    if q is not None and queues_over_budget(os.environ.get("GPU_MAX_HW_QUEUES"), q):
         env["GPU_MAX_HW_QUEUES"] = str(q)
     # torchrun-style names would override the rdc ones inside RdcInit's
     # fallbacks only where rdc names are absent; drop stale ones anyway

@@ -261,9 +261,9 @@ def run_mp(world, cases, timeout=240, env_extra=None):
     env.update(env_extra or {})
     # every rank on GPU 0: the hardware-queue budget rdc_amd.launcher applies
     # to workers that share a GPU (8 ranks -> 2 queues each)
-    from rdc_amd.launcher import hw_queues_per_process
+    from rdc_amd.launcher import hw_queues_per_process, queues_over_budget
     q = hw_queues_per_process(world)
-    if q is not None and env.get("RDC_DEVICE") != "rank" and "GPU_MAX_HW_QUEUES" not in env:
+    if q is not None and env.get("RDC_DEVICE") != "rank" and queues_over_budget(env.get("GPU_MAX_HW_QUEUES"), q):
         env["GPU_MAX_HW_QUEUES"] = str(q)
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), str(r), str(world),
                                str(port), tmp, cf], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)

@@ -274,7 +274,7 @@ def test_launcher_numa_bind_confines_workers(tmp_path):
 def test_launcher_queue_budget(tmp_path, monkeypatch):
     """Workers sharing a GPU get fewer hardware queues each (rdc_amd/launcher.py
     hw_queues_per_process): up to 4 per GPU keep HIP's default, 8 get 2, 16 get
-    1; a user's GPU_MAX_HW_QUEUES is kept; the KFD GPU count from sysfs."""
+    1; a GPU_MAX_HW_QUEUES above the budget is lowered, one below it kept; the KFD GPU count from sysfs."""
     import argparse
     from rdc_amd.launcher import hw_queues_per_process, kfd_gpu_count, visible_gpu_count, worker_env
     assert [hw_queues_per_process(k) for k in (1, 2, 4, 5, 8, 16, 32)] == [None, None, None, 3, 2, 1, 1]
@@ -283,8 +283,10 @@ def test_launcher_queue_budget(tmp_path, monkeypatch):
     assert worker_env(a, 3, 1234, 1)["GPU_MAX_HW_QUEUES"] == "2"
     assert "GPU_MAX_HW_QUEUES" not in worker_env(a, 3, 1234, 8)
     assert "GPU_MAX_HW_QUEUES" not in worker_env(argparse.Namespace(host_ip="127.0.0.1", num_workers=4), 0, 1, 1)
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
-    assert worker_env(a, 3, 1234, 1)["GPU_MAX_HW_QUEUES"] == "4"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")             # a box exporting HIP's default: lowered
+    assert worker_env(a, 3, 1234, 1)["GPU_MAX_HW_QUEUES"] == "2"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "1")             # a lower choice is kept
+    assert worker_env(a, 3, 1234, 1)["GPU_MAX_HW_QUEUES"] == "1"
     _fake_sysfs(tmp_path, [(128, "0-3"), (136, "4-7")])
     assert kfd_gpu_count(str(tmp_path)) == 2 and kfd_gpu_count(str(tmp_path / "missing")) is None
     for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
