@@ -371,7 +371,13 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
     g_reg_calls.fetch_add(1, std::memory_order_relaxed);
     if (K == 1) {  // the inline piece's collective: the whole buffer
         hip_check(hipMemcpyAsync(dev_, h, S, hipMemcpyHostToDevice, comm_stream), "H2D");
-        c->Allreduce(dev_, count, dtype, op, comm_stream);
+        hip_check(hipEventRecord(h2d_done_[0], comm_stream), "record");
+        try {
+            c->Allreduce(dev_, count, dtype, op, comm_stream);
+        } catch (...) {
+            (void)hipEventSynchronize(h2d_done_[0]);  // the H2D still reads the caller's buffer
+            throw;
+        }
         hip_check(hipMemcpyAsync(h, dev_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
         hip_check(hipEventRecord(in_done_[0], comm_stream), "record");
         SpinEvent(in_done_[0], "host allreduce");
