@@ -3,7 +3,8 @@
 "allreduce GB/s (device-resident fp32) at 1/2/4/8 GPUs; % xGMI roofline").
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+    (N>1 under a launcher: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...;
+     N>1 without one, WORLD_SIZE unset: bench.py starts that launcher itself as a child process)
 
 Workload: a 1 GiB fp32 buffer per GPU (the cfg3 buffer), synthetic data
 from the device generator, resident in HBM before timing starts.
@@ -600,8 +601,45 @@ def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
     return out
 
 
+def free_port():
+    import socket
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch_cmd(gpus, argv, port):
+    """The child command that runs `bench.py argv` as `gpus` ranks, one process
+    per GPU, exactly as the driver's N>1 form does (torch.distributed.run,
+    one node, rendezvous on 127.0.0.1) — the reference's harness likewise
+    spawns its own workers (tracker/launcher_local.py:63-100)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_self_launch(args, argv):
+    """`python bench.py --gpus N` (N > 1) started without a launcher: start the
+    N ranks as ONE child process tree (torch.distributed.run), forward its
+    output (inherited stdout/stderr: the ranks' JSON line is the only line
+    rank 0 prints) and return its exit code.  None when this process is
+    already a rank (WORLD_SIZE set) or N = 1.  Runs before torch or the HIP
+    library is loaded and never execs (a child, so nothing that touched the
+    GPU is replaced)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(self_launch_cmd(args.gpus, argv, free_port()), env=env)
+
+
 def main():
     args = parse()
+    rc = maybe_self_launch(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     # a rehearsal of N > 4 ranks on a 1-GPU box: fewer hardware queues per
     # process, as rdc_amd.launcher gives workers that share a GPU (the GPU's
     # scheduler otherwise time-slices 4 x N queues, ~10 ms per slice;

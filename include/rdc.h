@@ -72,12 +72,48 @@ template <> inline DataType GetType<long long>(void) { return kLongLong; }      
 template <> inline DataType GetType<unsigned long long>(void) { return kULongLong; }    // NOLINT
 }  // namespace mpi
 
-/*! \brief reduction operators (include/core/mpi.h:84-112) */
+/*! \brief reduction operators (include/core/mpi.h:84-120).  kType names the
+ *  device kernel the typed collectives launch; Reduce(dst, src) is the
+ *  element rule that kernel applies (rdc_amd/csrc/rdc_device.h OpF), kept
+ *  here on the host so code written against the reference — its reducer
+ *  lambda `op::Reducer<OP,DType>(src.addr(), dst.addr(), src.Count())`
+ *  (include/core/rdc-inl.h:130-132) — compiles and folds the same bits. */
 namespace op {
-struct Max { static const mpi::OpType kType = mpi::kMax; };
-struct Min { static const mpi::OpType kType = mpi::kMin; };
-struct Sum { static const mpi::OpType kType = mpi::kSum; };
-struct BitOR { static const mpi::OpType kType = mpi::kBitwiseOR; };
+struct Max {
+    static const mpi::OpType kType = mpi::kMax;
+    /*! \brief dst = src when dst < src (a NaN dst stays, a NaN src is ignored) */
+    template <typename DType> inline static void Reduce(DType& dst, const DType& src) {  // NOLINT(*)
+        if (dst < src) dst = src;
+    }
+};
+struct Min {
+    static const mpi::OpType kType = mpi::kMin;
+    /*! \brief dst = src when dst > src */
+    template <typename DType> inline static void Reduce(DType& dst, const DType& src) {  // NOLINT(*)
+        if (dst > src) dst = src;
+    }
+};
+struct Sum {
+    static const mpi::OpType kType = mpi::kSum;
+    template <typename DType> inline static void Reduce(DType& dst, const DType& src) {  // NOLINT(*)
+        dst += src;
+    }
+};
+struct BitOR {
+    static const mpi::OpType kType = mpi::kBitwiseOR;
+    template <typename DType> inline static void Reduce(DType& dst, const DType& src) {  // NOLINT(*)
+        dst |= src;
+    }
+};
+/*! \brief dst[i] = OP::Reduce(dst[i], src[i]) for i < len, on HOST memory, in
+ *  index order (include/core/mpi.h:113-120).  Device buffers: RdcReduce, the
+ *  same rule as a HIP kernel. */
+template <typename OP, typename DType>
+inline void Reducer(const void* src_, void* dst_, uint64_t len) {
+    const DType* src = static_cast<const DType*>(src_);
+    DType* dst = static_cast<DType*>(dst_);
+    for (uint64_t i = 0; i < len; ++i) OP::Reduce(dst[i], src[i]);
+}
 }  // namespace op
 
 
@@ -509,6 +545,20 @@ inline comm::ICommunicator* GetCommunicator(const std::string& name = kMainCommN
     comm::Registry().push_back(c);
     return c;
 }
+namespace comm {
+/*! \brief the reference's allreduce glue (src/comm/communicator.cc:24-28): the
+ *  named communicator's Allreduce(Buffer, ReduceFunction) with `red` as the
+ *  reducer.  dtype / op describe the buffer for the caller's benefit only, as
+ *  in the reference (which ignores them); the typed device path is
+ *  rdc::Allreduce<OP,DType>. */
+inline void Allreduce_(Buffer sendrecvbuf, ReduceFunction red, mpi::DataType dtype, mpi::OpType op,
+                       const std::string& name) {
+    (void)dtype;
+    (void)op;
+    GetCommunicator(name)->Allreduce(sendrecvbuf, red);
+}
+}  // namespace comm
+
 inline void Finalize() {
     for (comm::ICommunicator* c : comm::Registry()) delete c;
     comm::Registry().clear();

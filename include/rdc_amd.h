@@ -261,6 +261,15 @@ int RdcCommAutotune(void* comm, size_t bytes, int dtype, int reps, void* stream,
 int RdcCommTraceNext(void* comm, void* dev_words, size_t nwords);
 int RdcCommLastLaunch(void* comm, uint64_t* out6);
 
+/* Diagnostics: the device launch counter of comm's scratch channel — the
+ * counter half of every 64-bit hand-off sequence word (seq = counter << 8 |
+ * communicator tag; 56-bit counters, compared modulo 2^56, so flag slots never
+ * written or idle for any number of launches never read as "reached").
+ * RdcCommSetLaunchCounter is collective: every rank of the channel sets the
+ * same value with no collective in flight (tests start it past 2^32). */
+int RdcCommLaunchCounter(void* comm, uint64_t* value);
+int RdcCommSetLaunchCounter(void* comm, uint64_t value);
+
 /* Single process driving n ranks (devices[i] = HIP device of rank i; devices
  * may repeat).  comms[i] receives rank i's handle.  scratch_bytes 0 = default. */
 int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes);

@@ -64,6 +64,8 @@ def _load():
         "RdcCommTune": (i, [vp, i, i, i, sz]),
         "RdcCommAutotune": (i, [vp, sz, i, i, vp, vp, i, ctypes.POINTER(i), ctypes.POINTER(i)]),
         "RdcCommLastLaunch": (i, [vp, ctypes.POINTER(u64)]),
+        "RdcCommLaunchCounter": (i, [vp, ctypes.POINTER(u64)]),
+        "RdcCommSetLaunchCounter": (i, [vp, u64]),
         "RdcCommRank": (i, [vp]),
         "RdcCommSize": (i, [vp]),
         "RdcCommDevice": (i, [vp]),

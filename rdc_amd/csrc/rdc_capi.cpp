@@ -599,6 +599,17 @@ int RdcCommLastLaunch(void* comm, uint64_t* out6) {
     });
 }
 
+int RdcCommLaunchCounter(void* comm, uint64_t* value) {
+    return guard([&] {
+        if (!value) throw std::invalid_argument("rdc: null argument");
+        *value = as_comm(comm)->LaunchCounter();
+    });
+}
+
+int RdcCommSetLaunchCounter(void* comm, uint64_t value) {
+    return guard([&] { as_comm(comm)->SetLaunchCounter(value); });
+}
+
 int RdcCommGetParam(void* comm, const char* key, uint64_t* value) {
     return guard([&] {
         if (!key || !value) throw std::invalid_argument("rdc: null argument");

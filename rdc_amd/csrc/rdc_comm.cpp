@@ -343,7 +343,7 @@ void Communicator::AllocChannel() {
     int k1 = 0, k2 = 0, k3 = 0;
     ch->scratch = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k1));
     ch->scratch_ag = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k3));
-    ch->flags = static_cast<uint32_t*>(alloc_shared(ch->L.flag_bytes, &k2));
+    ch->flags = static_cast<uint64_t*>(alloc_shared(ch->L.flag_bytes, &k2));
     int k5 = 0;  // service LL slots [2][n] x RDC_SVC_SLOT_BYTES; zero: no sequence number matches
     const size_t svc_bytes = (size_t)2 * n_ * RDC_SVC_SLOT_BYTES;
     ch->svc_region = static_cast<char*>(alloc_shared(svc_bytes, &k5));
@@ -384,7 +384,7 @@ void Communicator::Attach(const std::shared_ptr<Channel>& ch) {
         std::lock_guard<std::mutex> lk(ch->mu);
         ++ch->users;
         // communicators attach to a channel in creation order, which is
-        // collective: the k-th user's tag is k on every rank (kSeqBits)
+        // collective: the k-th user's tag is k on every rank (rdc_device.h kTagBits)
         tag_ = ch->attached++ & 0xFFu;
     }
     Alias();
@@ -601,7 +601,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
             ch->peer_ag[p] = static_cast<char*>(pa);
             hip_check(hipIpcOpenMemHandle(&pf, hs[(size_t)p].flags, hipIpcMemLazyEnablePeerAccess),
                       "hipIpcOpenMemHandle(flags)");
-            ch->peer_flags[p] = static_cast<uint32_t*>(pf);
+            ch->peer_flags[p] = static_cast<uint64_t*>(pf);
             void* sv = nullptr;
             hip_check(hipIpcOpenMemHandle(&sv, hs[(size_t)p].svc, hipIpcMemLazyEnablePeerAccess),
                       "hipIpcOpenMemHandle(service)");
@@ -781,7 +781,7 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     a->err = err_;
     a->err_mirror = err_host_dev_;
     a->done_ctr = err_ + 16;
-    a->launch_ctr = err_ + 32;
+    a->launch_ctr = reinterpret_cast<uint64_t*>(err_ + 32);  // bytes 128-135
     a->launch_kind = err_ + 48;
     a->tag = tag_;
     a->half_bytes = OneshotHalfBytes(layout());
@@ -1435,6 +1435,23 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     }
     release();
     return nc;
+}
+
+uint64_t Communicator::LaunchCounter() {
+    if (err_ == nullptr) return 0;  // world size 1: nothing is ever launched
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    uint64_t v = 0;
+    hip_check(hipMemcpy(&v, err_ + 32, sizeof(v), hipMemcpyDeviceToHost), "read launch counter");
+    return v;
+}
+
+void Communicator::SetLaunchCounter(uint64_t value) {
+    if (err_ == nullptr) return;
+    if (value >> 55) throw std::invalid_argument("rdc: launch counter is 56 bits");
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    hip_check(hipMemcpy(err_ + 32, &value, sizeof(value), hipMemcpyHostToDevice), "write launch counter");
 }
 
 double Communicator::Probe(int mode, size_t* bytes_io, int reps, hipStream_t stream) {

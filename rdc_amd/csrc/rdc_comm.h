@@ -77,13 +77,13 @@ struct Channel {
     int alloc_kind = 0;
     char* scratch = nullptr;
     char* scratch_ag = nullptr;
-    uint32_t* flags = nullptr;
+    uint64_t* flags = nullptr;
     uint32_t* err = nullptr;           // [0] error word, [16] arrivals, [32] launches, [48] last kind
     uint32_t* err_host = nullptr;      // pinned: [0] error mirror, [4] notify token
     uint32_t* err_host_dev = nullptr;
     char* peer_scratch[RDC_MAX_RANKS] = {};
     char* peer_ag[RDC_MAX_RANKS] = {};
-    uint32_t* peer_flags[RDC_MAX_RANKS] = {};
+    uint64_t* peer_flags[RDC_MAX_RANKS] = {};
     // small-allreduce service (rdc_service.h): its own uncached slots
     // small-allreduce service slots (rdc_service.h): [2 halves][n] x
     // RDC_SVC_SLOT_BYTES of LL words per rank, IPC-mapped
@@ -208,6 +208,12 @@ public:
     void LastLaunch(uint64_t* out6) const {
         for (int i = 0; i < 6; ++i) out6[i] = last_launch_[i];
     }
+    // diagnostics: the channel's device launch counter (the counter half of
+    // every hand-off sequence word, rdc_device.h).  SetLaunchCounter is
+    // collective (every rank the same value, no collective in flight on any
+    // communicator of the channel); tests use it to start past 2^32.
+    uint64_t LaunchCounter();
+    void SetLaunchCounter(uint64_t value);
 
     int rank() const { return rank_; }
     int size() const { return n_; }
@@ -282,7 +288,7 @@ private:
     bool owns_peers_ipc_ = false;   // peers' p2p regions opened through IPC
     char* scratch_ = nullptr;       // RS region
     char* scratch_ag_ = nullptr;    // AG region
-    uint32_t* flags_ = nullptr;
+    uint64_t* flags_ = nullptr;
     uint32_t* err_ = nullptr;
     uint32_t* err_host_ = nullptr;  // pinned mirror of *err_ (kernel-written)
     uint32_t* err_host_dev_ = nullptr;
@@ -306,7 +312,7 @@ private:
     int wall_khz_ = 100000;         // wall_clock64() rate
     char* peer_scratch_[RDC_MAX_RANKS] = {};
     char* peer_ag_[RDC_MAX_RANKS] = {};
-    uint32_t* peer_flags_[RDC_MAX_RANKS] = {};
+    uint64_t* peer_flags_[RDC_MAX_RANKS] = {};
     std::map<std::vector<uint64_t>, PackEntry> pack_cache_;
     std::vector<std::pair<hipEvent_t, std::shared_ptr<std::vector<PackUnit>>>> retired_;  // evicted host copies
     uint64_t pack_tick_ = 0;

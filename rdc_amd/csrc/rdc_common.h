@@ -52,7 +52,7 @@ enum {
     RDC_KERR_TIMEOUT_ALLGATHER = 5,
     // a peer's hand-off carried this launch's sequence number but another
     // communicator's tag: ranks issued the collectives of communicators that
-    // share a channel in different orders (rdc_device.h kSeqBits)
+    // share a channel in different orders (rdc_device.h kTagBits)
     RDC_KERR_ORDER = 6
 };
 
@@ -88,7 +88,7 @@ struct CollArgs {
     uint32_t max_tiles;                  // flag array row stride
     char* rs[RDC_MAX_RANKS];             // rank p's reduce-scatter scratch region
     char* ag[RDC_MAX_RANKS];             // rank p's allgather scratch region
-    uint32_t* flags[RDC_MAX_RANKS];      // rank p's flag region: [2n][max_tiles] + done[n]
+    uint64_t* flags[RDC_MAX_RANKS];      // rank p's flag region: [2n][max_tiles] + done[n] (rdc_device.h seq)
     char* cbuf[RDC_MAX_RANKS];           // allgather: local buffer of rank c's data (off/len index into it)
     int nb_scatter, nb_reduce, nb_gather;  // mesh block roles (allgather: push / -, gather)
     uint32_t* err;                       // local device error word
@@ -96,9 +96,9 @@ struct CollArgs {
     uint32_t* notify;                    // optional pinned word: the last block stores notify_val there when
     uint32_t notify_val;                 //   the launch is complete (host spins on it instead of a stream sync)
     uint32_t* done_ctr;                  // local per-launch block arrival counter (self-resetting)
-    uint32_t* launch_ctr;                // local count of completed launches (device-side seq)
+    uint64_t* launch_ctr;                // local count of completed launches (device-side seq counter)
     uint32_t* launch_kind;               // local: kind of the last completed launch
-    uint32_t tag;                        // communicator's tag on its channel: bits 24-31 of every seq
+    uint32_t tag;                        // communicator's tag on its channel: bits 0-7 of every seq
     int kind;                            // this launch's RDC_KIND_*
     int bcast_split;                     // broadcast: root -> forwarder per tile -> other ranks (n >= 3)
     uint64_t half_bytes;                 // one-shot: offset of the slot half used by odd seq

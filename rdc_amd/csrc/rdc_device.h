@@ -164,26 +164,33 @@ __device__ __forceinline__ void st_elem_wt(void* p, T v) {
 enum { kDstLocal = 0, kDstPeer = 1 };
 
 // ------------------------------------------------------------- hand-off ----
-__device__ __forceinline__ uint32_t flag_load(const uint32_t* p) {
+// Hand-off flags are 64-bit words holding a launch's sequence number:
+//   seq = (counter << kTagBits) | tag
+// counter: the channel's launch count (every communicator sharing a channel
+// draws from one counter, 56 bits: it never wraps in practice, so a slot no
+// launch has written yet (0) or one idle for any number of launches never
+// looks "reached"); tag: the launching communicator's tag on that channel.
+// Hand-off flags carry the whole word, so a rank waiting for launch k of
+// communicator X that finds launch k of communicator Y — ranks that issued two
+// communicators' collectives in different orders — fails with RDC_KERR_ORDER
+// instead of folding unrelated buffers.  "Done" words (a peer finished launch
+// k-1, whichever communicator issued it) compare the counter only.
+constexpr uint32_t kTagBits = 8;
+constexpr uint64_t kTagMask = (1ull << kTagBits) - 1ull;
+__device__ __forceinline__ uint64_t flag_load(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ void flag_store(uint32_t* p, uint32_t v) {
+__device__ __forceinline__ void flag_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// A launch's sequence number: bits 0-23 count the channel's launches (every
-// communicator sharing a channel draws from one counter), bits 24-31 are the
-// launching communicator's tag.  Hand-off flags carry the whole word, so a
-// rank waiting for launch k of communicator X that finds launch k of
-// communicator Y — ranks that issued two communicators' collectives in
-// different orders — fails with RDC_KERR_ORDER instead of folding unrelated
-// buffers.  "Done" words (a peer finished launch k-1, whichever communicator
-// issued it) compare the counter only.  Counters compare modulo 2^24.
-constexpr uint32_t kSeqBits = 24;
-constexpr uint32_t kSeqMask = (1u << kSeqBits) - 1u;
-__device__ __forceinline__ bool seq_reached(uint32_t v, uint32_t seq) {
-    return (int32_t)((v - seq) << (32 - kSeqBits)) >= 0;
+__device__ __forceinline__ uint64_t seq_counter(uint64_t seq) { return seq >> kTagBits; }
+// counter of v >= counter of seq (modulo 2^56)
+__device__ __forceinline__ bool seq_reached(uint64_t v, uint64_t seq) {
+    return (int64_t)((seq_counter(v) - seq_counter(seq)) << kTagBits) >= 0;
 }
-__device__ __forceinline__ bool same_tag(uint32_t v, uint32_t seq) { return ((v ^ seq) >> kSeqBits) == 0; }
+__device__ __forceinline__ bool same_tag(uint64_t v, uint64_t seq) { return ((v ^ seq) & kTagMask) == 0; }
+// the previous launch's number (counter - 1, same tag; compared untagged)
+__device__ __forceinline__ uint64_t seq_prev(uint64_t seq) { return seq - (1ull << kTagBits); }
 
 // Called by EVERY thread of the block after its payload stores.  Lanes
 // 0..nflags-1 of wave 0 then store flags[i] = seq.
@@ -197,7 +204,7 @@ __device__ __forceinline__ bool same_tag(uint32_t v, uint32_t seq) { return ((v 
 // only add an L2 write-back (buffer_wbl2 sc0 sc1, 1.7-6.5 us per call) of
 // cached lines no peer reads, so it is issued only for fine- / coarse-grained
 // scratch (alloc fallbacks).
-__device__ __forceinline__ void block_publish(uint32_t* const* flags, int nflags, uint32_t seq, int uc) {
+__device__ __forceinline__ void block_publish(uint64_t* const* flags, int nflags, uint64_t seq, int uc) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < (unsigned)nflags) {
@@ -209,7 +216,7 @@ __device__ __forceinline__ void block_publish(uint32_t* const* flags, int nflags
     }
 }
 
-__device__ __forceinline__ void block_publish1(uint32_t* flag, uint32_t seq, int uc) {
+__device__ __forceinline__ void block_publish1(uint64_t* flag, uint64_t seq, int uc) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -236,7 +243,7 @@ struct Abort {
 // of the handed-off bytes cannot hit stale lines; uncached scratch (`uc`) is
 // never held in any GPU cache, so its loads after the matched poll read
 // memory and need no invalidate (MI355X_MICROARCH.md: an acquire is ≈1.7 us).
-__device__ __forceinline__ bool block_wait(uint32_t* const* flags, int nflags, uint32_t seq,
+__device__ __forceinline__ bool block_wait(uint64_t* const* flags, int nflags, uint64_t seq,
                                            const Abort& ab, uint32_t code, int uc, bool tagged = true) {
     __shared__ int s_ok;
     if (threadIdx.x < 64) {
@@ -247,7 +254,7 @@ __device__ __forceinline__ bool block_wait(uint32_t* const* flags, int nflags, u
         uint32_t spins = 0;
         while (true) {
             if (!mine) {
-                const uint32_t v = flag_load(flags[lane]);
+                const uint64_t v = flag_load(flags[lane]);
                 if (seq_reached(v, seq)) {
                     if (!tagged || same_tag(v, seq)) mine = true;
                     else wrong = true;

@@ -7,7 +7,7 @@
 namespace rdc_amd {
 
 __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
-    const uint32_t seq = launch_seq(a);
+    const uint64_t seq = launch_seq(a);
     if (!channel_failed(a)) bcast_body(a, seq);
     launch_done(a, seq);
 }
@@ -20,17 +20,17 @@ __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
 // each peer's AG slot `rank` over all links at once (push blocks) and lands
 // the peers' buffers from its own AG slots (gather blocks).  Like broadcast,
 // receivers never answer, so pushes wait for the targets' done words.
-__device__ void allgather_body(const CollArgs& a, uint32_t seq) {
+__device__ void allgather_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
-    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
+    __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
     int b = blockIdx.x;
     if (b < a.nb_scatter) {
         const int items = (n - 1) * a.tiles[r];
         if (b < items) {
             if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = done_word(a, r, (r + 1 + threadIdx.x) % n);
             __syncthreads();
-            if (!block_wait(s_flags, n - 1, seq - 1, ab, RDC_KERR_TIMEOUT_ALLGATHER, a.uc, false)) return;
+            if (!block_wait(s_flags, n - 1, seq_prev(seq), ab, RDC_KERR_TIMEOUT_ALLGATHER, a.uc, false)) return;
         }
         for (int it = b; it < items; it += a.nb_scatter) {
             const int t = it / (n - 1);
@@ -63,7 +63,7 @@ __device__ void allgather_body(const CollArgs& a, uint32_t seq) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_allgather(CollArgs a) {
-    const uint32_t seq = launch_seq(a);
+    const uint64_t seq = launch_seq(a);
     if (!channel_failed(a)) allgather_body(a, seq);
     launch_done(a, seq);
 }

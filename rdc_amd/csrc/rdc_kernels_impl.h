@@ -31,7 +31,7 @@ namespace rdc_amd {
 constexpr int kBlock = 256;
 
 // rank `owner`'s flag word that rank `writer` sets when it finished a launch
-__device__ __forceinline__ uint32_t* done_word(const CollArgs& a, int owner, int writer) {
+__device__ __forceinline__ uint64_t* done_word(const CollArgs& a, int owner, int writer) {
     return a.flags[owner] + (uint64_t)(2 * a.n) * a.max_tiles + writer;
 }
 
@@ -40,11 +40,11 @@ __device__ __forceinline__ uint32_t* done_word(const CollArgs& a, int owner, int
 // correctly: every block reads the communicator's launch counter when it
 // starts (seq = launches completed + 1, identical on every rank because all
 // ranks issue the same collectives), and the launch's last block advances it.
-// The counter lives in bits 0-23, the launching communicator's tag in bits
-// 24-31 (rdc_device.h kSeqBits).
-__device__ __forceinline__ uint32_t launch_seq(const CollArgs& a) {
-    const uint32_t done = __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return ((done + 1u) & kSeqMask) | (a.tag << kSeqBits);
+// seq = (counter << kTagBits) | the launching communicator's tag
+// (rdc_device.h).
+__device__ __forceinline__ uint64_t launch_seq(const CollArgs& a) {
+    const uint64_t done = __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ((done + 1ull) << kTagBits) | ((uint64_t)a.tag & kTagMask);
 }
 // A channel that failed (a peer missed a hand-off, an order violation) is
 // unusable: later launches move nothing — in particular they push nothing
@@ -67,12 +67,12 @@ __device__ __forceinline__ uint32_t prev_kind(const CollArgs& a) {
 // Block-wide: wait until each listed peer finished launch seq-1 (its done word
 // in MY flag array).  Used before writing into peers' scratch when no data
 // dependency already orders the write.
-__device__ __forceinline__ bool gate_on_peers(const CollArgs& a, uint32_t seq, int first, int count,
+__device__ __forceinline__ bool gate_on_peers(const CollArgs& a, uint64_t seq, int first, int count,
                                               const Abort& ab, uint32_t code) {
-    __shared__ uint32_t* s_gate[RDC_MAX_RANKS];
+    __shared__ uint64_t* s_gate[RDC_MAX_RANKS];
     if (threadIdx.x < (unsigned)count) s_gate[threadIdx.x] = done_word(a, a.rank, (first + threadIdx.x) % a.n);
     __syncthreads();
-    return block_wait(s_gate, count, seq - 1, ab, code, a.uc, false);
+    return block_wait(s_gate, count, seq_prev(seq), ab, code, a.uc, false);
 }
 
 
@@ -274,13 +274,13 @@ __device__ __forceinline__ void for_unit_pieces(const CollArgs& a, uint64_t p0, 
 }
 
 template <int OP, typename T, int NMAX>
-__device__ void mesh_body(const CollArgs& a, uint32_t seq) {
+__device__ void mesh_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     int b = blockIdx.x;
     int tmax = 0;
     for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
-    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
+    __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
 
     if (b < a.nb_scatter) {
         // ---- scatter: my copy of chunk c's tile t -> owner c's rs slot r
@@ -441,12 +441,12 @@ __device__ __forceinline__ void chunk_pieces(const CollArgs& a, int c, uint64_t 
 }
 
 template <int OP, typename T>
-__device__ void ring_body(const CollArgs& a, uint32_t seq) {
+__device__ void ring_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
     const int prev = (r - 1 + n) % n;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     if (prev_kind(a) == RDC_KIND_ONESHOT && !gate_on_peers(a, seq, prev, 1, ab, RDC_KERR_TIMEOUT_RING)) return;
-    __shared__ uint32_t* s_flag[1];
+    __shared__ uint64_t* s_flag[1];
     __shared__ UnitCache s_units;
     UnitCache* ucp = a.units ? &s_units : nullptr;
     if (ucp) unit_cache_reset(s_units);
@@ -648,11 +648,11 @@ __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
 }
 
 template <int OP, typename T, int NMAX, bool TREE = false>
-__device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
+__device__ void oneshot_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
-    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
-    const uint64_t half = (seq & 1u) ? a.half_bytes : 0;
+    __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
+    const uint64_t half = (seq_counter(seq) & 1u) ? a.half_bytes : 0;
     const uint64_t total = a.total_bytes;
     const int ntiles = a.tiles[0];
     // 1) push every tile of my buffer into every peer's slot r (never waits)
@@ -703,11 +703,11 @@ __device__ void oneshot_body(const CollArgs& a, uint32_t seq) {
 // (direct, or the forwarder's own flag) or the tile's forwarder.
 __device__ __forceinline__ int bcast_forwarder(int n, int root, int t) { return (root + 1 + t % (n - 1)) % n; }
 
-__device__ void bcast_body(const CollArgs& a, uint32_t seq) {
+__device__ void bcast_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank, root = a.root;
     const bool split = a.bcast_split != 0 && n >= 3;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
-    __shared__ uint32_t* s_flags[RDC_MAX_RANKS];
+    __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
     __shared__ int s_cnt;
     if (blockIdx.x < a.tiles[0] && (r == root || split)) {
         // A broadcast's receivers never report back, so before overwriting a
@@ -723,7 +723,7 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
             s_cnt = k;
         }
         __syncthreads();
-        if (!block_wait(s_flags, s_cnt, seq - 1, ab, RDC_KERR_TIMEOUT_BCAST, a.uc, false)) return;
+        if (!block_wait(s_flags, s_cnt, seq_prev(seq), ab, RDC_KERR_TIMEOUT_BCAST, a.uc, false)) return;
     }
     for (int t = blockIdx.x; t < a.tiles[0]; t += gridDim.x) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
@@ -778,7 +778,7 @@ __device__ void bcast_body(const CollArgs& a, uint32_t seq) {
 // buffer writes through the kernel boundary).  A launch that writes host
 // memory (zero-copy host path: `notify`) or uses cached scratch keeps the
 // system-scope fences, so the host reads the results after the notify word.
-__device__ __forceinline__ void launch_done(const CollArgs& a, uint32_t seq) {
+__device__ __forceinline__ void launch_done(const CollArgs& a, uint64_t seq) {
     const bool fence = a.notify != nullptr || !a.uc;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -792,7 +792,7 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint32_t seq) {
             for (int p = 0; p < a.n; ++p)
                 if (p != a.rank) flag_store(done_word(a, p, a.rank), seq);
             __hip_atomic_store(a.launch_kind, (uint32_t)a.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.launch_ctr, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.launch_ctr, seq_counter(seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the host reads the (sticky) error word here after a stream sync: no
             // copy needed.  The mirror starts at 0 and only ever changes to an
             // error, so the PCIe write (whose completion the kernel's end waits
@@ -816,7 +816,7 @@ __device__ __forceinline__ void trace_block(const CollArgs& a, uint64_t t0) {
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
     const uint64_t t0 = wall_clock64();
-    const uint32_t seq = launch_seq(a);
+    const uint64_t seq = launch_seq(a);
     if (!channel_failed(a)) mesh_body<OP, T, NMAX>(a, seq);
     trace_block(a, t0);
     launch_done(a, seq);
@@ -824,14 +824,14 @@ __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
 
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_oneshot(CollArgs a) {
-    const uint32_t seq = launch_seq(a);
+    const uint64_t seq = launch_seq(a);
     if (!channel_failed(a)) oneshot_body<OP, T, NMAX>(a, seq);
     launch_done(a, seq);
 }
 
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_tree(CollArgs a) {
-    const uint32_t seq = launch_seq(a);
+    const uint64_t seq = launch_seq(a);
     if (!channel_failed(a)) oneshot_body<OP, T, NMAX, true>(a, seq);
     launch_done(a, seq);
 }
@@ -839,7 +839,7 @@ __global__ __launch_bounds__(kBlock) void k_tree(CollArgs a) {
 template <int OP, typename T>
 __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
     const uint64_t t0 = wall_clock64();
-    const uint32_t seq = launch_seq(a);
+    const uint64_t seq = launch_seq(a);
     if (!channel_failed(a)) ring_body<OP, T>(a, seq);
     trace_block(a, t0);
     launch_done(a, seq);

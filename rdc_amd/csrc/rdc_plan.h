@@ -16,7 +16,7 @@ struct Layout {
     size_t slot_bytes = 0;    // one slot = one chunk piece (+ alignment slack)
     size_t region_bytes = 0;  // n slots; RS and AG regions are separate allocations
     uint32_t max_tiles = 0;   // flag-row length
-    size_t flag_bytes = 0;    // [2n][max_tiles] + done[n] uint32, rounded to 4 KiB
+    size_t flag_bytes = 0;    // [2n][max_tiles] + done[n] uint64 sequence words, rounded to 4 KiB
 };
 // RS / AG regions are capped below 2 GiB: on ROCm 7.2 (dmabuf IPC)
 // hipIpcOpenMemHandle of an allocation >= 2 GiB never returns

@@ -228,6 +228,56 @@ int main(int argc, char** argv) {
         save("reducer_sum", g.data(), N * 4);
     }
 
+    // ---- the reference's own reducer idiom (include/core/rdc-inl.h:125-135):
+    // a typed Buffer, the lambda over op::Reducer<OP,DType> (mpi.h:113-120),
+    // through the virtual ICommunicator::Allreduce(Buffer, ReduceFunction) and
+    // through comm::Allreduce_ (src/comm/communicator.cc:24-28)
+    {
+        const size_t N = 1001;
+        std::vector<float> f = fill(N, 0x5EED3400, r);
+        rdc::Buffer sendrecvbuf(f.data(), N * sizeof(float));
+        sendrecvbuf.set_item_size(sizeof(float));
+        auto reducer = [](rdc::Buffer src, rdc::Buffer dst) {
+            rdc::op::Reducer<rdc::op::Sum, float>(src.addr(), dst.addr(), src.Count());
+        };
+        rdc::GetCommunicator()->Allreduce(sendrecvbuf, reducer);
+        save("op_reducer_sum", f.data(), N * 4);
+
+        std::vector<float> m = fill(N, 0x5EED3500, r);
+        rdc::Buffer mb(m.data(), N * sizeof(float));
+        mb.set_item_size(sizeof(float));
+        rdc::comm::Allreduce_(mb, [](rdc::Buffer src, rdc::Buffer dst) {
+            rdc::op::Reducer<rdc::op::Max, float>(src.addr(), dst.addr(), src.Count());
+        }, rdc::mpi::GetType<float>(), rdc::op::Max::kType, rdc::kMainCommName);
+        save("op_reducer_max", m.data(), N * 4);
+
+        // test/allreduce.cc's integer known answers through the same idiom
+        std::vector<int32_t> a(N);
+        for (size_t i = 0; i < N; ++i) a[i] = r + (int32_t)N + (int32_t)i;
+        rdc::Buffer ab(a.data(), N * sizeof(int32_t));
+        ab.set_item_size(sizeof(int32_t));
+        rdc::comm::Allreduce_(ab, [](rdc::Buffer src, rdc::Buffer dst) {
+            rdc::op::Reducer<rdc::op::Sum, int32_t>(src.addr(), dst.addr(), src.Count());
+        }, rdc::mpi::kInt, rdc::mpi::kSum, rdc::kMainCommName);
+        for (size_t i = 0; i < N; ++i) {
+            int32_t want = 0;
+            for (int q = 0; q < n; ++q) want += q + (int32_t)N + (int32_t)i;
+            EXPECT(a[i] == want, "op::Reducer<Sum,int> at %zu: %d != %d", i, a[i], want);
+        }
+        std::vector<uint8_t> bits(N);
+        for (size_t i = 0; i < N; ++i) bits[i] = (uint8_t)(1u << ((i + (size_t)r) % 8));
+        rdc::Buffer bb(bits.data(), N);
+        bb.set_item_size(1);
+        rdc::GetCommunicator()->Allreduce(bb, [](rdc::Buffer src, rdc::Buffer dst) {
+            rdc::op::Reducer<rdc::op::BitOR, uint8_t>(src.addr(), dst.addr(), src.Count());
+        });
+        for (size_t i = 0; i < N; ++i) {
+            uint8_t want = 0;
+            for (int q = 0; q < n; ++q) want |= (uint8_t)(1u << ((i + (size_t)q) % 8));
+            EXPECT(bits[i] == want, "op::Reducer<BitOR,uint8_t> at %zu", i);
+        }
+    }
+
     // ---- Reducer<Pair, pair_reduce> (api.h:135-146): struct items, known answers
     {
         std::vector<Pair> p(33);

@@ -159,6 +159,53 @@ def test_cpp_header_compiles():
     assert "known-answer OK" in p.stdout
 
 
+def test_header_op_reducer_matches_reference(tmp_path):
+    """include/rdc.h's op::Reducer<OP,DType> and op::X::Reduce (mpi.h:84-120)
+    fold the same bytes as the reference's own header compiled (oracle/_ref
+    ref_reducer) for every (dtype, op) the reference defines, on random
+    values plus the edge cases: NaN on either side, signed zeros, +-inf,
+    integer overflow (wraps) and extremes."""
+    from oracle import oracle as O
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    so = str(tmp_path / "libop_reducer_shim.so")
+    subprocess.check_call(["g++", "-std=c++11", "-O2", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "op_reducer_shim.cc"), "-o", so,
+                           "-L", os.path.join(ROOT, "rdc_amd"), "-lrdc_amd", "-Wl,-rpath," + os.path.join(ROOT, "rdc_amd")])
+    H = ctypes.CDLL(so)
+    vp = ctypes.c_void_p
+    H.hdr_reducer.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+    kt = (ctypes.c_int * 4)()
+    H.hdr_op_types(kt)
+    assert list(kt) == [O.OP_MAX, O.OP_MIN, O.OP_SUM, O.OP_BITOR]
+    R = O.ref()
+    rng = np.random.default_rng(41)
+    n = 4099
+    checked = 0
+    for dt in range(10):
+        npd = O.NP_DTYPE[dt]
+        ops = (O.OP_MAX, O.OP_MIN, O.OP_SUM) + (() if dt in (O.DT_FLOAT32, O.DT_FLOAT64) else (O.OP_BITOR,))
+        for op in ops:
+            if dt in (O.DT_FLOAT32, O.DT_FLOAT64):
+                s = (rng.standard_normal(n) * 1e3).astype(npd)
+                d = (rng.standard_normal(n) * 1e3).astype(npd)
+                special = np.array([np.nan, 1.0, -0.0, 0.0, np.inf, -np.inf, np.nan, 3.0], dtype=npd)
+                s[:8] = special
+                d[:8] = special[::-1]
+            else:
+                info = np.iinfo(npd)
+                s = rng.integers(info.min, info.max, n, dtype=npd, endpoint=True)
+                d = rng.integers(info.min, info.max, n, dtype=npd, endpoint=True)
+                s[:4] = [info.max, info.min, info.max, 0]
+                d[:4] = [info.max, info.min, info.min, info.max]
+            want, got = d.copy(), d.copy()
+            assert R.ref_reducer(s.ctypes.data, want.ctypes.data, n, dt, op) == 0
+            assert H.hdr_reducer(s.ctypes.data, got.ctypes.data, n, dt, op) == 0
+            assert got.tobytes() == want.tobytes(), (dt, op)
+            checked += 1
+    assert checked == 38  # 8 integer types x 4 ops + 2 float types x 3 ops
+
+
 def test_pinned_empty_is_reduced_in_place():
     """rdc_amd.pinned_empty: page-aligned host memory behind a pinned Buffer
     (registration itself needs a GPU); allreduce's copy rule (rdc/core.py:

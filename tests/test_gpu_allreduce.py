@@ -169,6 +169,66 @@ def test_group_repeated_calls(group3):
             assert same_bits(got[r], want, O.DT_FLOAT32), (it, count, algo)
 
 
+@pytest.mark.parametrize("start", [(1 << 23) - 2, (1 << 32) - 3, (1 << 40) + 5])
+def test_group_launch_counter_far_past_zeroed_flags(start, algo_counts=((2, 300007), (1, 300007), (3, 70001),
+                                                                         (4, 4099), (0, 1 << 20))):
+    """Hand-off flags are zeroed once, when the channel is made; the launch
+    counter keeps growing.  On a FRESH group (every flag slot still 0) with
+    the counter started at 2^23 - 2, 2^32 - 3 and 2^40 + 5 — past where a
+    24-bit or 32-bit counter compare would read a never-written 0 as
+    "reached"  — mesh, ring, one-shot, tree and auto launches on
+    slots no earlier launch wrote stay bit-exact, broadcast and allgather
+    too, and the counter advances by one per launch across 2^23 / 2^32."""
+    import ctypes
+    from rdc_amd._lib import _LIB
+    g = make_group(3, 24 << 20)
+    try:
+        for c in g:
+            assert _LIB.RdcCommSetLaunchCounter(c.handle, start) == 0, _LIB.RdcGetLastError()
+        rng = np.random.default_rng(start & 0xFFFF)
+        launches = 0
+        for algo, count in algo_counts:
+            inputs = [rng.standard_normal(count).astype(np.float32) for _ in range(3)]
+            want = (O.expected_tree if algo == 4 else O.expected_allreduce)(inputs, O.DT_FLOAT32, O.OP_SUM)
+            got = run_group(g, inputs, O.DT_FLOAT32, O.OP_SUM, algo)
+            for r in range(3):
+                assert same_bits(got[r], want, O.DT_FLOAT32), (start, algo, count, r)
+            v = ctypes.c_uint64()
+            assert _LIB.RdcCommLaunchCounter(g[0].handle, ctypes.byref(v)) == 0
+            assert v.value > start + launches, (start, algo, v.value)
+            launches = v.value - start
+        data = [rng.integers(0, 256, (3 << 20) + 5, dtype=np.uint8) for _ in range(3)]
+        bufs = [to_dev(d, r) for r, d in enumerate(data)]
+        torch.cuda.synchronize()
+        for r in range(3):
+            assert _LIB.RdcCommBroadcast(g[r].handle, ptr(bufs[r], r), data[0].size, 2,
+                                         ctypes.c_void_p(g.streams[r].cuda_stream)) == 0
+        for r in range(3):
+            g[r].check(ctypes.c_void_p(g.streams[r].cuda_stream))
+            assert from_dev(bufs[r], r, data[0].size, O.DT_UINT8).tobytes() == data[2].tobytes()
+        sizes = [1 << 20, 7, (2 << 20) + 1]
+        data = [rng.integers(0, 256, s, dtype=np.uint8) for s in sizes]
+        bufs = [[to_dev(data[c] if c == r else np.zeros(sizes[c], np.uint8), 0) for c in range(3)] for r in range(3)]
+        torch.cuda.synchronize()
+        for r in range(3):
+            ptrs = (ctypes.c_void_p * 3)(*[bufs[r][c].data_ptr() for c in range(3)])
+            assert _LIB.RdcCommAllgather(g[r].handle, ptrs, (ctypes.c_size_t * 3)(*sizes),
+                                         ctypes.c_void_p(g.streams[r].cuda_stream)) == 0
+        for r in range(3):
+            g[r].check(ctypes.c_void_p(g.streams[r].cuda_stream))
+            for c in range(3):
+                assert from_dev(bufs[r][c], 0, sizes[c], O.DT_UINT8).tobytes() == data[c].tobytes()
+        counters = []
+        for c in g:
+            v = ctypes.c_uint64()
+            assert _LIB.RdcCommLaunchCounter(c.handle, ctypes.byref(v)) == 0
+            counters.append(v.value)
+        assert len(set(counters)) == 1 and counters[0] >= start + len(algo_counts) + 2, counters
+    finally:
+        for c in g:
+            c.destroy()
+
+
 @pytest.mark.parametrize("algo", ["mesh", "ring", "oneshot"])
 def test_group_graph_capture_replay(group2, algo):
     """Launch sequence numbers live on the device, so a captured allreduce

@@ -91,6 +91,27 @@ PARITY_KEYS = ("cfg3_mesh", "cfg3_ring", "cfg4_fp16", "cfg5_buckets", "oneshot_5
                "tree_order", "broadcast_nonzero_root", "allgather_varsize")
 
 
+def test_bench_self_launches_its_ranks():
+    """`python bench.py --gpus 2` with no launcher (WORLD_SIZE unset) starts
+    its two ranks itself (a torch.distributed.run child): exactly one JSON
+    line, n_gpus 2, and every bit-exact check after the timed region true —
+    so a driver that starts the N-GPU bench like the N = 1 one still
+    measures N ranks."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--bytes", str(16 << 20), "--extra-steps", "0", "--rccl-steps", "0", "--cpu-seconds", "0",
+           "--autotune-reps", "0"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["bytes_per_gpu"] == 16 << 20
+    chk = out["oracle_check"]
+    assert all(chk.get(k) is True for k in PARITY_KEYS), chk
+
+
 def test_bench_tiny_extras_budget():
     """--extras-budget-s bounds everything after the timed region: with a
     1-second budget the headline line is still printed, every extra is listed
@@ -211,9 +232,11 @@ def test_cpp_buffer_surface(buffer_api_exe, tmp_path, world, mincount):
         assert p.returncode == 0 and "rank %d: buffer api OK" % r in outs[r], report
     tree = mincount is not None
     N = 1001
-    for name, seed in (("typed_sum", 0x5EED3000), ("custom_sum", 0x5EED3100), ("reducer_sum", 0x5EED3200)):
+    for name, seed, op in (("typed_sum", 0x5EED3000, O.OP_SUM), ("custom_sum", 0x5EED3100, O.OP_SUM),
+                           ("reducer_sum", 0x5EED3200, O.OP_SUM), ("op_reducer_sum", 0x5EED3400, O.OP_SUM),
+                           ("op_reducer_max", 0x5EED3500, O.OP_MAX)):
         xs = [O.fill(N, O.DT_FLOAT32, seed, r) for r in range(world)]
-        want = (O.expected_tree if tree else O.expected_allreduce)(xs, O.DT_FLOAT32, O.OP_SUM)
+        want = (O.expected_tree if tree else O.expected_allreduce)(xs, O.DT_FLOAT32, op)
         for r in range(world):
             got = np.fromfile(str(tmp_path / ("%s_rank%d.bin" % (name, r))), dtype=np.float32)
             assert got.tobytes() == want.tobytes(), (name, r)

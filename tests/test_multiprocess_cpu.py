@@ -298,3 +298,32 @@ def test_launcher_queue_budget(tmp_path, monkeypatch):
     assert visible_gpu_count(str(dri)) == 2 and visible_gpu_count(str(tmp_path / "none")) is None
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3")
     assert visible_gpu_count(str(dri)) == 1
+
+
+def test_bench_self_launch_command(monkeypatch):
+    """`python bench.py --gpus N` without a launcher: the
+    child it starts is the driver's own N > 1 form — torch.distributed.run,
+    one node, N processes, rendezvous on 127.0.0.1 — running this bench.py
+    with the same arguments; nothing is started at N = 1 or inside a rank."""
+    import argparse
+    import bench
+    cmd = bench.self_launch_cmd(8, ["--gpus", "8", "--steps", "20"], 29555)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert cmd[3:10] == ["--nnodes=1", "--nproc-per-node", "8", "--master-addr", "127.0.0.1", "--master-port",
+                         "29555"]
+    assert cmd[10] == os.path.join(ROOT, "bench.py") and cmd[11:] == ["--gpus", "8", "--steps", "20"]
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    assert bench.maybe_self_launch(argparse.Namespace(gpus=8), []) is None   # already a rank
+    monkeypatch.delenv("WORLD_SIZE")
+    assert bench.maybe_self_launch(argparse.Namespace(gpus=1), []) is None   # N = 1 runs in place
+
+
+def test_bench_self_launch_forwards_exit_code():
+    """The self-launched ranks' exit status is bench.py's: here (no GPU) both
+    ranks fail, so bench.py fails and prints no JSON line."""
+    env = clean_env()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup",
+                        "1", "--bytes", "4096"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode != 0
+    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert "torch.distributed" in p.stderr or "ChildFailedError" in p.stderr or "local_rank" in p.stderr, p.stderr[-2000:]
