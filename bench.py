@@ -79,6 +79,19 @@ def load_traffic(kernel_key):
         return None
 
 
+def hbm_model(lib, world, count, dt_enum, algo_name):
+    """RdcPlanHbmBytes for the schedule the timed launches used: per-rank
+    (max) and all-rank loads / stores of one allreduce, or None."""
+    algo = {"ring": 1, "mesh": 2, "oneshot": 3, "tree": 4}.get(algo_name)
+    if algo is None:
+        return None
+    out = (ctypes.c_uint64 * 5)()
+    if lib.RdcPlanHbmBytes(world, count, dt_enum, algo, out) != 0:
+        return None
+    return {"read": int(out[0]), "write": int(out[1]), "read_sum": int(out[2]), "write_sum": int(out[3]),
+            "egress": int(out[4])}
+
+
 def cpu_baseline(nbytes_workload, seconds):
     """Reference op::Reducer<Sum,float> (oracle/_ref, the reference's own header
     compiled -O2) or, if absent, the C oracle port, single thread, on a bounded
@@ -918,12 +931,29 @@ def main():
             meas = probe["one_link_one_direction_GBps"] if algo_name == "ring" else probe["all_links_egress_GBps"]
             roof["peak_measured"] = meas
             roof["frac_of_measured"] = round(busbw / meas, 4)
+        # HBM side of the same launches: the committed byte model of the
+        # schedule (RdcPlanHbmBytes = rdc_plan.cpp ModelHbmBytes: bytes the
+        # kernels load and store, per rank) over the kernel time
+        hm = hbm_model(_LIB, world, count if args.buckets == 1 else S // esz, dt_enum, algo_name)
+        if hm is not None:
+            per_gpu = -(-world // max(1, gpus_here)) if shared else 1   # ranks on one GPU
+            moved = hm["read_sum"] + hm["write_sum"] if (shared and gpus_here == 1) else \
+                per_gpu * (hm["read"] + hm["write"])
+            ach = moved / (kern_ms * 1e-3) / 1e9
+            hb = {"model": "rdc_plan.cpp ModelHbmBytes (RdcPlanHbmBytes): loads + stores the schedule's kernels "
+                           "issue, remote stores counted at the issuing rank",
+                  "read_bytes_per_rank": hm["read"], "write_bytes_per_rank": hm["write"], "ranks_on_gpu": per_gpu,
+                  "bytes_per_step": int(moved), "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                  "frac": round(ach / HBM_PEAK_GBPS, 4),
+                  "traffic": load_traffic("%s_%s_n%d_%d" % (algo_name, DT_SHORT[args.dtype], world, S))}
+            roof["shared_hbm" if shared else "hbm"] = hb
         if shared:
             # every rank's bytes move through ONE HBM: no xGMI link is timed,
             # so no xGMI fraction is meaningful (round 1 printed 7.996 here)
             roof.update({"bound": "shared-hbm", "peak": None, "frac": None, "frac_of_bidir_ring_roofline": None,
                          "frac_of_measured": None,
-                         "note": "%d ranks share %d GPU(s): rehearsal of the protocol, not an xGMI measurement"
+                         "note": "%d ranks share %d GPU(s): rehearsal of the protocol, not an xGMI measurement; "
+                                 "roofline.shared_hbm is the one HBM all ranks' bytes move through"
                                  % (world, gpus_here)})
         workload = "in-place allreduce(sum) of a %d MiB %s buffer per GPU, %s schedule" % (S >> 20, args.dtype,
                                                                                         algo_name)
@@ -968,6 +998,13 @@ def main():
                                 "frac_of_one_link_peak": None if shared else round(rb / XGMI_LINK_DIR_GBPS, 4),
                                 "note": "reference ring schedule (k_ring) on the same buffer, timed after the "
                                         "main region; bit-identical result"}
+        hm = hbm_model(_LIB, world, count, dt_enum, "ring")
+        if hm is not None:
+            moved = hm["read_sum"] + hm["write_sum"] if (shared and gpus_here == 1) else hm["read"] + hm["write"]
+            ach = moved / (ring_cmp * 1e-3) / 1e9
+            out["ring_schedule"]["shared_hbm" if shared else "hbm"] = {
+                "bytes_per_step": int(moved), "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "traffic": load_traffic("ring_%s_n%d_%d" % (DT_SHORT[args.dtype], world, S))}
     if tuned is not None:
         out["autotune"] = tuned
     if roles is not None:

@@ -319,6 +319,14 @@ int RdcPlanHostPieces(size_t bytes, uint64_t* bounds, int max_bounds, int* out_n
  * RDC_ALGO_MESH (2) (negative on bad arguments).
  * oneshot_bytes = RDC_ONESHOT_BYTES (0 = the default size / rank-aware rule). */
 int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_bytes);
+/* HBM byte model of one allreduce of `count` elements over n ranks with
+ * schedule `algo` (1 ring, 2 mesh, 3 one-shot, 4 tree): the bytes the kernels
+ * load and store, counted per access as their loops issue them, a remote
+ * store counted at the rank that issues it.  out5 = {read bytes, write bytes
+ * (both the most of any rank), read bytes, write bytes (both summed over the
+ * ranks), link egress bytes (the most of any rank)}.  bench.py's N > 1
+ * roofline divides this by the measured time. */
+int RdcPlanHbmBytes(int n, size_t count, int dtype, int algo, uint64_t* out5);
 int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int algo, size_t tile_bytes,
                      int max_blocks, uint64_t* out, int max_pieces, int* out_pieces);
 

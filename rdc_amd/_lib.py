@@ -76,6 +76,7 @@ def _load():
         "RdcFill": (i, [vp, sz, i, u64, i, vp]),
         "RdcMemcpy": (i, [vp, vp, sz]),
         "RdcPlanLayout": (i, [i, sz, ctypes.POINTER(u64)]),
+        "RdcPlanHbmBytes": (i, [i, sz, i, i, ctypes.POINTER(u64)]),
         "RdcPlanAutoAlgo": (i, [i, sz, sz, sz]),
         "RdcPlanHostPieces": (i, [sz, ctypes.POINTER(ctypes.c_uint64), i, ctypes.POINTER(i)]),
         "RdcPlanAllreduce": (i, [i, sz, i, sz, i, sz, i, ctypes.POINTER(u64), i, ctypes.POINTER(ctypes.c_int)]),

@@ -730,6 +730,21 @@ int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_by
     return rc != 0 ? rc : algo;
 }
 
+int RdcPlanHbmBytes(int n, size_t count, int dtype, int algo, uint64_t* out5) {
+    return guard([&] {
+        const size_t esz = rdc_dtype_size(dtype);
+        if (n < 1 || n > RDC_MAX_RANKS || esz == 0 || !out5 ||
+            (algo != RDC_ALGO_RING && algo != RDC_ALGO_MESH && algo != RDC_ALGO_ONESHOT && algo != RDC_ALGO_TREE))
+            throw std::invalid_argument("rdc: bad argument");
+        const HbmBytes h = ModelHbmBytes(n, count, esz, algo);
+        out5[0] = h.read_max;
+        out5[1] = h.write_max;
+        out5[2] = h.read_sum;
+        out5[3] = h.write_sum;
+        out5[4] = h.egress_max;
+    });
+}
+
 int RdcPlanHostPieces(size_t bytes, uint64_t* bounds, int max_bounds, int* out_n) {
     return guard([&] {
         if (!bounds || !out_n || max_bounds < 2) throw std::invalid_argument("rdc: bad argument");

@@ -365,6 +365,63 @@ int PlanTreeProgram(int n, int* dst, int* src) {
     return k;
 }
 
+// Bytes one rank's kernels load and store for an allreduce of `count`
+// elements (16-B lanes and element-wise edges alike, each byte once per
+// access), per the kernels' loops (rdc_kernels_impl.h), with chunk c =
+// utils::Split(0, count, n) = len[c] bytes:
+//   ring (TryReduceScatterRing + TryAllgatherRing):
+//     RS step j: send chunk (r+1+j)%n (load user, store into prev's scratch),
+//                receive chunk (r+2+j)%n (load scratch + user, store user);
+//     AG step j: send chunk (r+j)%n (load user, store into prev's scratch),
+//                receive chunk (r+1+j)%n (load scratch, store user)
+//   mesh: scatter every other chunk to its owner (load user, store remote);
+//         fold own chunk (load n-1 slots + user, store user + n-1 remote);
+//         gather every other chunk (load own AG slot, store user)
+//   one-shot / tree: push the whole buffer to n-1 peers (each push loads the
+//         user bytes again), fold every element over the n inputs (load
+//         n-1 slots + user, store user)
+// A remote store is counted at the rank that issues it (the counters of the
+// issuing GPU's L2 see it); egress = those remote bytes.
+HbmBytes ModelHbmBytes(int n, uint64_t count, size_t esz, int algo) {
+    HbmBytes h;
+    if (n < 2 || count == 0) return h;
+    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+    SplitRanges((int64_t)count, n, cb, ce);
+    uint64_t len[RDC_MAX_RANKS];
+    for (int c = 0; c < n; ++c) len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
+    const uint64_t S = count * esz;
+    for (int r = 0; r < n; ++r) {  // every rank; the rank-averaged figure is reported
+        uint64_t rd = 0, wr = 0, eg = 0;
+        if (algo == RDC_ALGO_RING) {
+            for (int j = 0; j + 1 < n; ++j) {
+                const uint64_t cs = len[(r + 1 + j) % n], cr = len[(r + 2 + j) % n];
+                rd += cs + 2 * cr;
+                wr += cs + cr;
+                eg += cs;
+                const uint64_t as = len[(r + j) % n], ar = len[(r + 1 + j) % n];
+                rd += as + ar;
+                wr += as + ar;
+                eg += as;
+            }
+        } else if (algo == RDC_ALGO_MESH) {
+            const uint64_t others = S - len[r];
+            rd += others + (uint64_t)n * len[r] + others;
+            wr += others + (uint64_t)n * len[r] + others;
+            eg += others + (uint64_t)(n - 1) * len[r];
+        } else {  // one-shot / tree order
+            rd += (uint64_t)(n - 1) * S + (uint64_t)n * S;
+            wr += (uint64_t)(n - 1) * S + S;
+            eg += (uint64_t)(n - 1) * S;
+        }
+        h.read_max = std::max(h.read_max, rd);
+        h.write_max = std::max(h.write_max, wr);
+        h.read_sum += rd;
+        h.write_sum += wr;
+        h.egress_max = std::max(h.egress_max, eg);
+    }
+    return h;
+}
+
 std::vector<int> GroupCoalesced(const uint64_t* counts, int nbuf, size_t esz, uint64_t fuse_bytes) {
     std::vector<int> bounds;
     bounds.push_back(0);

@@ -150,4 +150,12 @@ CoalescedPlan PlanCoalesced(int n, const uint64_t* counts, int nbuf, size_t esz,
 // Returns group boundaries: group g = buffers [bounds[g], bounds[g+1]).
 std::vector<int> GroupCoalesced(const uint64_t* counts, int nbuf, size_t esz, uint64_t fuse_bytes);
 
+// HBM byte model of one allreduce (rdc_plan.cpp ModelHbmBytes): bytes the
+// kernels load / store, per rank (max over ranks) and summed over ranks,
+// plus the most remote-store (link egress) bytes of any rank
+struct HbmBytes {
+    uint64_t read_max = 0, write_max = 0, read_sum = 0, write_sum = 0, egress_max = 0;
+};
+HbmBytes ModelHbmBytes(int n, uint64_t count, size_t esz, int algo);
+
 }  // namespace rdc_amd

@@ -308,3 +308,39 @@ def test_host_pipeline_knobs_parse_units():
     lens = [y - x for x, y in zip(c[16 << 20], c[16 << 20][1:])]
     assert lens[:3] == [256 << 10, 512 << 10, 1 << 20] and max(lens) <= 2 << 20 and sum(lens) == 16 << 20
     assert [y - x for x, y in zip(c[4 << 20], c[4 << 20][1:])] == [2 << 20, 2 << 20]
+
+
+def hbm(n, count, dtype, algo):
+    from rdc_amd._lib import _LIB
+    out = (ctypes.c_uint64 * 5)()
+    assert _LIB.RdcPlanHbmBytes(n, count, dtype, algo, out) == 0
+    return dict(read=out[0], write=out[1], read_sum=out[2], write_sum=out[3], egress=out[4])
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 8, 16])
+def test_hbm_byte_model_closed_forms(n):
+    """The committed per-schedule HBM byte model (RdcPlanHbmBytes, rdc_plan.cpp
+    ModelHbmBytes) bench.py's N > 1 roofline uses.  Closed forms, S = buffer
+    bytes: ring 5(n-1)/n S loaded + 4(n-1)/n S stored per rank; mesh
+    (3n-2)/n S each way; one-shot (2n-1) S loaded + n S stored; egress
+    2(n-1)/n S for ring and mesh (what the link roofline counts) and (n-1) S
+    for the one-shot.  Ragged Split chunks: the rank sums keep the closed
+    forms exactly."""
+    for count in (n * 4096, n * 4096 + n - 1, 1001):
+        S = 4 * count
+        ring, mesh, one = hbm(n, count, 6, 1), hbm(n, count, 6, 2), hbm(n, count, 6, 3)
+        assert ring["read_sum"] == 5 * (n - 1) * S and ring["write_sum"] == 4 * (n - 1) * S
+        assert mesh["read_sum"] == mesh["write_sum"] == (3 * n - 2) * S
+        assert one["read_sum"] == n * (2 * n - 1) * S and one["write_sum"] == n * n * S
+        assert hbm(n, count, 6, 4) == one
+        if count % n == 0:
+            assert ring["read"] * n == 5 * (n - 1) * S and ring["write"] * n == 4 * (n - 1) * S
+            assert mesh["read"] * n == (3 * n - 2) * S
+            assert ring["egress"] * n == mesh["egress"] * n == 2 * (n - 1) * S
+        assert one["egress"] == (n - 1) * S
+    # n = 2, 1 GiB: the ring loads 2.5 S and stores 2 S per rank (4.5 S, DESIGN.md)
+    r2 = hbm(2, 1 << 28, 6, 1)
+    assert r2["read"] + r2["write"] == 9 * (1 << 30) // 2
+    assert hbm(8, 1 << 28, 6, 2)["read"] * 8 == 22 * (1 << 30)   # mesh 5.5 S per rank at n = 8, both ways
+    from rdc_amd._lib import _LIB
+    assert _LIB.RdcPlanHbmBytes(2, 10, 6, 0, (ctypes.c_uint64 * 5)()) != 0   # auto is not a schedule
