@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bytes", type=int, default=1 << 30, help="buffer size per GPU")
     ap.add_argument("--dtype", default="float32", choices=sorted(DTYPES))
-    ap.add_argument("--algo", default="auto", choices=["auto", "mesh", "ring", "oneshot"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "mesh", "mesh_pull", "ring", "oneshot"])
     ap.add_argument("--buckets", type=int, default=1,
                     help="N>1: split the buffer into this many equal buckets (cfg5: --buckets 1024)")
     ap.add_argument("--unfused", action="store_true", help="buckets as separate allreduce calls (no coalescing)")
@@ -82,7 +82,7 @@ def load_traffic(kernel_key):
 def hbm_model(lib, world, count, dt_enum, algo_name):
     """RdcPlanHbmBytes for the schedule the timed launches used: per-rank
     (max) and all-rank loads / stores of one allreduce, or None."""
-    algo = {"ring": 1, "mesh": 2, "oneshot": 3, "tree": 4}.get(algo_name)
+    algo = {"ring": 1, "mesh": 2, "oneshot": 3, "tree": 4, "mesh_pull": 5}.get(algo_name)
     if algo is None:
         return None
     out = (ctypes.c_uint64 * 5)()
@@ -326,7 +326,7 @@ def parity_checks(lib, comm, S, world, rank, sp, dist, torch, out, budget=None):
     """Bit-exact checks at the bench's own shapes (after all timing), each on
     fresh synthetic inputs, every key its own boolean (AND over ranks):
 
-    * cfg3_mesh / cfg3_ring / cfg4_fp16: ONE allreduce of the whole S-byte
+    * cfg3_mesh / cfg3_ring / cfg3_mesh_pull / cfg4_fp16: ONE allreduce of the whole S-byte
       buffer.  Every rank hashes its WHOLE result (sha256) and the ranks
       compare digests; rank r compares Split chunk r of its result, every
       element, with the oracle's ring order.  Identical digests + every chunk
@@ -391,7 +391,7 @@ def parity_checks(lib, comm, S, world, rank, sp, dist, torch, out, budget=None):
         return True
 
     for name, dt, algo, tdt in (("cfg3_mesh", 6, 2, torch.float32), ("cfg3_ring", 6, 1, torch.float32),
-                                ("cfg4_fp16", 10, 0, torch.float16)):
+                                ("cfg3_mesh_pull", 6, 5, torch.float32), ("cfg4_fp16", 10, 0, torch.float16)):
         if not should_run(name, 20):
             continue
         t0 = time.perf_counter()
@@ -571,8 +571,9 @@ def trace_roles(lib, comm, buf, count, dt_enum, sp, dist, torch):
     grid, s, r, g, tile, algo = [int(x) for x in ll]
     t = tr[:2 * grid].cpu().numpy().view(np.uint64).reshape(grid, 2).astype(np.float64)
     t0 = t[:, 0].min()
-    names = {1: "ring", 2: "mesh", 3: "oneshot"}
-    roles = {"all": (0, grid)} if algo != 2 else {"scatter": (0, s), "reduce": (s, s + r), "gather": (s + r, grid)}
+    names = {1: "ring", 2: "mesh", 3: "oneshot", 5: "mesh_pull"}
+    roles = {"all": (0, grid)} if algo not in (2, 5) else {"scatter": (0, s), "reduce": (s, s + r),
+                                                           "gather": (s + r, grid)}
     vals = []
     for lo, hi in roles.values():
         seg = t[lo:hi]
@@ -580,7 +581,7 @@ def trace_roles(lib, comm, buf, count, dt_enum, sp, dist, torch):
     v = torch.tensor(vals, dtype=torch.float64)
     dist.all_reduce(v, op=dist.ReduceOp.MAX)
     out = {"schedule": names.get(algo, str(algo)), "grid": grid, "tile_bytes": tile,
-           "blocks": {"scatter": s, "reduce": r, "gather": g} if algo == 2 else {"all": grid}}
+           "blocks": {"scatter": s, "reduce": r, "gather": g} if algo in (2, 5) else {"all": grid}}
     for i, k in enumerate(roles):
         out[k + "_us"] = {"first_start": round(float(v[3 * i]), 1), "last_end": round(float(v[3 * i + 1]), 1),
                           "mean_block_busy": round(float(v[3 * i + 2]), 1)}
@@ -691,7 +692,7 @@ def main():
         dist.init_process_group("gloo")
         rdc_amd.init([])          # RANK/WORLD_SIZE + MASTER_ADDR:MASTER_PORT+1 bootstrap
         comm = rdc_amd.get_comm("main")
-        algo = {"auto": 0, "ring": 1, "mesh": 2, "oneshot": 3}[args.algo]
+        algo = {"auto": 0, "ring": 1, "mesh": 2, "oneshot": 3, "mesh_pull": 5}[args.algo]
         K = max(1, args.buckets)
         if K == 1:
             buf = torch.empty(count, dtype=tdtype, device="cuda")
@@ -790,7 +791,7 @@ def main():
     if world > 1:  # the schedule and launch shape the library used for the timed launches
         ll = (ctypes.c_uint64 * 6)()
         if _LIB.RdcCommLastLaunch(comm.handle, ll) == 0:
-            timed_algo = {1: "ring", 2: "mesh", 3: "oneshot", 4: "tree"}.get(int(ll[5]))
+            timed_algo = {1: "ring", 2: "mesh", 3: "oneshot", 4: "tree", 5: "mesh_pull"}.get(int(ll[5]))
             timed_launch = {"schedule": timed_algo, "grid": int(ll[0]), "scatter_blocks": int(ll[1]),
                             "reduce_blocks": int(ll[2]), "gather_blocks": int(ll[3]), "tile_bytes": int(ll[4])}
     if world > 1:
@@ -920,7 +921,7 @@ def main():
         algo_name = args.algo
         if algo_name == "auto":  # the schedule the library launched in the timed region (RdcCommLastLaunch)
             algo_name = timed_algo or "mesh"
-        peak = XGMI_LINK_DIR_GBPS * (1 if algo_name == "ring" else (world - 1))
+        peak = XGMI_LINK_DIR_GBPS * (1 if algo_name == "ring" else (world - 1))  # mesh / mesh_pull: every link
         roof = {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 1), "unit": "GB/s",
                 "frac": round(busbw / peak, 4), "traffic": None,
                 "kernel": "k_%s<Sum,%s>" % (algo_name, args.dtype),
@@ -944,8 +945,13 @@ def main():
                            "issue, remote stores counted at the issuing rank",
                   "read_bytes_per_rank": hm["read"], "write_bytes_per_rank": hm["write"], "ranks_on_gpu": per_gpu,
                   "bytes_per_step": int(moved), "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                  "frac": round(ach / HBM_PEAK_GBPS, 4),
-                  "traffic": load_traffic("%s_%s_n%d_%d" % (algo_name, DT_SHORT[args.dtype], world, S))}
+                  "frac": round(ach / HBM_PEAK_GBPS, 4)}
+            # rank 0's own L2-to-memory bytes (rocprofv3 PMC, FETCH_SIZE x 2 +
+            # WRITE_SIZE, the other ranks unprofiled: tools/pmc_rank0.sh),
+            # committed per (schedule, dtype, n, S) in profiles/traffic.json
+            tr = load_traffic("%s_%s_n%d_%d" % (algo_name, DT_SHORT[args.dtype], world, S))
+            hb["traffic_per_rank"] = tr
+            hb["traffic_over_model"] = round(tr / (hm["read"] + hm["write"]), 4) if tr else None
             roof["shared_hbm" if shared else "hbm"] = hb
         if shared:
             # every rank's bytes move through ONE HBM: no xGMI link is timed,
@@ -1004,7 +1010,7 @@ def main():
             ach = moved / (ring_cmp * 1e-3) / 1e9
             out["ring_schedule"]["shared_hbm" if shared else "hbm"] = {
                 "bytes_per_step": int(moved), "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
-                "traffic": load_traffic("ring_%s_n%d_%d" % (DT_SHORT[args.dtype], world, S))}
+                "traffic_per_rank": load_traffic("ring_%s_n%d_%d" % (DT_SHORT[args.dtype], world, S))}
     if tuned is not None:
         out["autotune"] = tuned
     if roles is not None:

@@ -40,7 +40,7 @@ extern "C" {
  * key=val override environment variables (communicator_manager.cc:87-104).
  * Keys: RDC_RANK, RDC_WORLD_SIZE|rdc_world_size, RDC_TRACKER_URI,
  * RDC_TRACKER_PORT, rdc_reduce_ring_mincount, RDC_DEVICE, RDC_SCRATCH_BYTES,
- * RDC_ALGO (mesh|ring|oneshot), RDC_NBLOCKS, RDC_TILE_BYTES, RDC_TIMEOUT, RDC_ONESHOT_BYTES,
+ * RDC_ALGO (mesh|mesh_pull|ring|oneshot), RDC_NBLOCKS, RDC_TILE_BYTES, RDC_TIMEOUT, RDC_ONESHOT_BYTES,
  * RDC_FUSE_BYTES, RDC_FUSE_BYTES_DIRECT, RDC_COALESCE_FUSED, RDC_HOST_ZC_BYTES,
  * RDC_BCAST_SPLIT_BYTES, RDC_P2P_SLOT_BYTES.
  * Falls back to torchrun's RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT
@@ -163,7 +163,10 @@ int RdcCommIRecv(void** wc, void* comm, void* buf, size_t bytes, int src, void* 
  * (hipStream_t; NULL = default stream).  Asynchronous: errors raised inside
  * the kernels (a peer that never joins) surface at RdcCommCheck. */
 int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op, void* stream);
-/* algo: 0 auto, 1 ring (the reference schedule), 2 mesh (all links), 3 one-shot (small buffers:
+/* algo: 0 auto, 1 ring (the reference schedule), 2 mesh (all links, pushed by remote stores),
+ * 5 pull-mode mesh (the same exchange by remote loads: ranks stage their chunks in their own
+ * scratch, owners load and fold, peers load the results; RdcCommAutotune times it against
+ * the push mesh), 3 one-shot (small buffers:
  * every rank pushes the whole buffer to every peer, one hand-off); auto = one-shot when
  * the one-shot while bytes <= 8 MiB and its extra egress over the mesh,
  * (n-1)(n-2)/n x bytes, is <= 4 MiB (n = 2: 8 MiB, n = 8: 0.76 MiB; with
@@ -222,7 +225,8 @@ int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, dou
 int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t tile_bytes);
 
 /* Autotune (collective: every rank of `comm`, same arguments, no collective in
- * flight; blocks the host): time the ring, the mesh and (where it fits half a
+ * flight; blocks the host): time the ring, the mesh pushed and pulled (RDC_ALGO_MESH_PULL) and
+ * (where it fits half a
  * slot) the one-shot schedule, then the launch shapes of the fastest, for
  * `bytes` of `dtype` on this node — mesh: role split, then grid, then
  * tiles per reduce block; ring: grid, then tiles per block (a granularity, so
@@ -237,13 +241,14 @@ int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t t
  * shape, RdcCommTune clears every autotuned one, and nothing is tuned while
  * RDC_ALGO forces a schedule; with RDC_TUNE_FILE set, rank 0 appends the
  * winner there and later communicators of the same rank and CU count start
- * from it).  cand (room for max_cand; 16 suffices)
+ * from it).  cand (room for max_cand; 24 suffices)
  * receives every timed candidate with its slowest-rank ms; *ncand their count,
  * *best the chosen index (-1 and nothing changed for sizes that take the
  * tree order, rdc_reduce_ring_mincount).  Results stay bit-identical whatever wins.  No
  * reference counterpart (the reference's schedule has no launch shape). */
 typedef struct {
-    int algo;                           /* RDC_ALGO_RING (1), RDC_ALGO_MESH (2), RDC_ALGO_ONESHOT (3) */
+    int algo;                           /* RDC_ALGO_RING (1), RDC_ALGO_MESH (2), RDC_ALGO_ONESHOT (3),
+                                           RDC_ALGO_MESH_PULL (5) */
     int mesh_s16, mesh_r16, max_blocks; /* max_blocks 0 = automatic grid */
     int tiles_per_block;                /* 0 = default (mesh 2 per reduce block, ring 1) */
     double ms;                          /* per allreduce: median over rounds of the slowest rank's time */
@@ -320,9 +325,9 @@ int RdcPlanHostPieces(size_t bytes, uint64_t* bounds, int max_bounds, int* out_n
  * oneshot_bytes = RDC_ONESHOT_BYTES (0 = the default size / rank-aware rule). */
 int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_bytes);
 /* HBM byte model of one allreduce of `count` elements over n ranks with
- * schedule `algo` (1 ring, 2 mesh, 3 one-shot, 4 tree): the bytes the kernels
- * load and store, counted per access as their loops issue them, a remote
- * store counted at the rank that issues it.  out5 = {read bytes, write bytes
+ * schedule `algo` (1 ring, 2 mesh, 3 one-shot, 4 tree, 5 pull-mode mesh): the
+ * bytes the kernels load and store, counted per access as their loops issue
+ * them, a remote store or load counted at the rank that issues it.  out5 = {read bytes, write bytes
  * (both the most of any rank), read bytes, write bytes (both summed over the
  * ranks), link egress bytes (the most of any rank)}.  bench.py's N > 1
  * roofline divides this by the measured time. */

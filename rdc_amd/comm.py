@@ -51,8 +51,9 @@ class WorkComp(object):
 def _is_tensor(x):
     return hasattr(x, "data_ptr") and hasattr(x, "is_cuda")
 
-ALGO_AUTO, ALGO_RING, ALGO_MESH, ALGO_ONESHOT, ALGO_TREE = 0, 1, 2, 3, 4
-_ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "mesh": ALGO_MESH, "oneshot": ALGO_ONESHOT, "tree": ALGO_TREE}
+ALGO_AUTO, ALGO_RING, ALGO_MESH, ALGO_ONESHOT, ALGO_TREE, ALGO_MESH_PULL = 0, 1, 2, 3, 4, 5
+_ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "mesh": ALGO_MESH, "oneshot": ALGO_ONESHOT, "tree": ALGO_TREE,
+          "mesh_pull": ALGO_MESH_PULL}
 
 
 class Comm(object):
@@ -215,7 +216,7 @@ class Comm(object):
                                         ctypes.byref(best)))
 
         def row(c):
-            return {"schedule": {1: "ring", 2: "mesh", 3: "oneshot"}.get(c.algo, c.algo),
+            return {"schedule": {1: "ring", 2: "mesh", 3: "oneshot", 5: "mesh_pull"}.get(c.algo, c.algo),
                     "split": [c.mesh_s16, c.mesh_r16], "grid": c.max_blocks or "auto",
                     "tiles_per_block": c.tiles_per_block or "auto", "ms": round(c.ms, 4),
                     "spread_ms": [round(c.ms_min, 4), round(c.ms_max, 4)]}

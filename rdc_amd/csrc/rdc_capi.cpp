@@ -83,8 +83,8 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_SCRATCH_BYTES" || k == "rdc_reduce_buffer") m.cfg.scratch_bytes = parse_unit(val);
     else if (k == "RDC_ALGO") {
         std::string v(val);
-        m.cfg.algo = v == "ring" ? RDC_ALGO_RING : v == "mesh" ? RDC_ALGO_MESH : v == "oneshot" ? RDC_ALGO_ONESHOT
-                                                                                                : RDC_ALGO_AUTO;
+        m.cfg.algo = v == "ring" ? RDC_ALGO_RING : v == "mesh" ? RDC_ALGO_MESH : v == "mesh_pull" ? RDC_ALGO_MESH_PULL
+                     : v == "oneshot" ? RDC_ALGO_ONESHOT : RDC_ALGO_AUTO;
         // (the tree is chosen by size through rdc_reduce_ring_mincount, as in the reference)
     } else if (k == "RDC_NBLOCKS") m.cfg.max_blocks = atoi(val);
     else if (k == "RDC_TILE_BYTES") m.cfg.tile_bytes = parse_unit(val);
@@ -514,7 +514,7 @@ int RdcAllreduceCoalescedOn(void* comm, void** bufs, const size_t* counts, int n
 int RdcCommAllreduceCoalesced(void* comm, void* const* dev_bufs, const size_t* counts, int nbuf, int dtype, int op,
                               int algo, void* stream) {
     return guard([&] {
-        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_TREE) throw std::invalid_argument("rdc: bad algo");
+        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_MESH_PULL) throw std::invalid_argument("rdc: bad algo");
         as_comm(comm)->AllreduceCoalesced(dev_bufs, counts, nbuf, dtype, op, static_cast<hipStream_t>(stream), algo);
     });
 }
@@ -548,7 +548,7 @@ int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op,
 
 int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream) {
     return guard([&] {
-        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_TREE) throw std::invalid_argument("rdc: bad algo");
+        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_MESH_PULL) throw std::invalid_argument("rdc: bad algo");
         as_comm(comm)->Allreduce(dev_buf, count, dtype, op, static_cast<hipStream_t>(stream), algo);
     });
 }
@@ -734,7 +734,8 @@ int RdcPlanHbmBytes(int n, size_t count, int dtype, int algo, uint64_t* out5) {
     return guard([&] {
         const size_t esz = rdc_dtype_size(dtype);
         if (n < 1 || n > RDC_MAX_RANKS || esz == 0 || !out5 ||
-            (algo != RDC_ALGO_RING && algo != RDC_ALGO_MESH && algo != RDC_ALGO_ONESHOT && algo != RDC_ALGO_TREE))
+            (algo != RDC_ALGO_RING && algo != RDC_ALGO_MESH && algo != RDC_ALGO_ONESHOT && algo != RDC_ALGO_TREE &&
+             algo != RDC_ALGO_MESH_PULL))
             throw std::invalid_argument("rdc: bad argument");
         const HbmBytes h = ModelHbmBytes(n, count, esz, algo);
         out5[0] = h.read_max;

@@ -146,7 +146,8 @@ std::vector<TuneEntry> read_tune_file(const std::string& path) {
         if (sscanf(line, "rdc-tune %d %d %d %d %d %d %d %d %d %d %lf", &ver, &e.n, &e.cus, &e.rpg, &e.cls, &e.algo,
                    &e.s16, &e.r16, &e.grid, &e.tpb, &ms) == 11 &&
             ver == 2 && e.rpg >= 1 && e.cls >= 0 && e.cls < 64 &&
-            (e.algo == RDC_ALGO_RING || e.algo == RDC_ALGO_MESH || e.algo == RDC_ALGO_ONESHOT) && e.s16 >= 1 &&
+            (e.algo == RDC_ALGO_RING || e.algo == RDC_ALGO_MESH || e.algo == RDC_ALGO_MESH_PULL ||
+             e.algo == RDC_ALGO_ONESHOT) && e.s16 >= 1 &&
             e.r16 >= 1 && e.s16 + e.r16 <= 15 && e.grid >= 0 && e.tpb >= 0)
             out.push_back(e);
     }
@@ -758,7 +759,7 @@ int Communicator::PickAlgo(int algo, uint64_t bytes) const {
         // rule's mesh / ring / one-shot choice (never a tree-order size; a
         // one-shot that does not fit half a slot falls back below)
         if (algo == RDC_ALGO_MESH || algo == RDC_ALGO_RING || algo == RDC_ALGO_ONESHOT) {
-            const auto it = tuned_algo_.find(SizeClass(bytes));
+            const auto it = tuned_algo_.find(SizeClass(bytes));  // may be RDC_ALGO_MESH_PULL
             if (it != tuned_algo_.end()) algo = it->second;
         }
     }
@@ -935,7 +936,8 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
                                 uint64_t total, size_t esz, int algo, hipStream_t stream, const PackUnit* units,
                                 int nunits) {
     algo = PickAlgo(algo, total);
-    if (units && algo != RDC_ALGO_MESH && algo != RDC_ALGO_RING)
+    const bool mesh_like = algo == RDC_ALGO_MESH || algo == RDC_ALGO_MESH_PULL;
+    if (units && !mesh_like && algo != RDC_ALGO_RING)
         throw std::logic_error("rdc: unit-table launch needs the mesh or ring schedule");
     if (algo == RDC_ALGO_ONESHOT) {
         const Piece p = PlanOneshotRanges(n_, off, len, total, layout(), cfg_.tile_bytes,
@@ -964,12 +966,11 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
     }
     const Shape sh = ShapeFor(total, algo);
     const int grid_cap =
-        algo == RDC_ALGO_MESH ? LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : 2 * cus_min_,
-                                           ks.occupancy(RDC_KIND_MESH, n_))
-                              : LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : cus_min_,
-                                           ks.occupancy(RDC_KIND_RING, n_));
-    const std::vector<Piece> plan =
-        PlanAllreduceRanges(n_, off, len, esz, layout(), algo, sh.tile_bytes, grid_cap, sh.split);
+        mesh_like ? LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : 2 * cus_min_, ks.occupancy(RDC_KIND_MESH, n_))
+                  : LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : cus_min_, ks.occupancy(RDC_KIND_RING, n_));
+    // the pull mode plans exactly as the push mode (same roles, same tiles)
+    const std::vector<Piece> plan = PlanAllreduceRanges(n_, off, len, esz, layout(), mesh_like ? RDC_ALGO_MESH : algo,
+                                                        sh.tile_bytes, grid_cap, sh.split);
     for (const Piece& p : plan) {
         CollArgs a;
         FillArgsCommon(&a);
@@ -1003,6 +1004,7 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
             a.nb_reduce = p.nb_reduce;
             a.nb_gather = p.nb_gather;
             a.kind = RDC_KIND_MESH;
+            a.pull = algo == RDC_ALGO_MESH_PULL ? 1 : 0;
             hip_check(ks.mesh(a, grid, stream), "launch mesh allreduce");
         }
     }
@@ -1152,7 +1154,7 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
             // what Autotune measured — run over the unit table: mesh and ring
             // read and write the user buffers in place, no staging image
             const int pick = PickAlgo(algo, bytes);
-            if (live >= 2 && (pick == RDC_ALGO_MESH || pick == RDC_ALGO_RING)) {
+            if (live >= 2 && (pick == RDC_ALGO_MESH || pick == RDC_ALGO_MESH_PULL || pick == RDC_ALGO_RING)) {
                 const PackEntry& e = PackTable(bufs + b0, counts + b0, b1 - b0, esz, stream);
                 LaunchRanges(ks, nullptr, e.off, e.len, e.total, esz, pick, stream, e.dtable, e.nunits);
             } else {
@@ -1278,7 +1280,7 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     const uint64_t total = (uint64_t)count * esz;
     if (n_ == 1 || count == 0 || total <= cfg_.ring_mincount || cfg_.algo != RDC_ALGO_AUTO) return 0;
     const int rule = AutoAlgo(n_, total, layout(), cfg_.oneshot_push_max);
-    if (rule != RDC_ALGO_MESH && rule != RDC_ALGO_RING && rule != RDC_ALGO_ONESHOT) return 0;
+    if (rule != RDC_ALGO_MESH && rule != RDC_ALGO_RING && rule != RDC_ALGO_ONESHOT) return 0;  // (never pull)
     const bool oneshot_fits = OneshotEligible(n_, total, layout(), (uint64_t)-1);
     hip_check(hipSetDevice(device_), "hipSetDevice");
     void* buf = nullptr;
@@ -1373,29 +1375,32 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
         // (one hand-off, (n-1) x the egress) where it fits
         int lo = nc;
         add(rule, s0, r0, g0, t0);
-        for (int a : {RDC_ALGO_RING, RDC_ALGO_MESH, RDC_ALGO_ONESHOT})
+        // (the mesh twice: pushed by remote stores and pulled by remote loads —
+        // which direction the links serve faster is this node's answer)
+        for (int a : {RDC_ALGO_RING, RDC_ALGO_MESH, RDC_ALGO_MESH_PULL, RDC_ALGO_ONESHOT})
             if (a != rule && (a != RDC_ALGO_ONESHOT || oneshot_fits)) add(a, s0, r0, g0, t0);
         int w = stage(lo);
         if (cand[w].algo == RDC_ALGO_ONESHOT) {
             // no roles or tiles to shape: the schedule is the result
-        } else if (cand[w].algo == RDC_ALGO_MESH) {
+        } else if (cand[w].algo == RDC_ALGO_MESH || cand[w].algo == RDC_ALGO_MESH_PULL) {
             static const int kSplits[][2] = {{4, 8}, {3, 9}, {5, 8}, {6, 6}, {3, 10}, {2, 10}, {5, 7}};
+            const int ma = cand[w].algo;
             lo = nc;
-            add(RDC_ALGO_MESH, cand[w].s16, cand[w].r16, cand[w].grid, cand[w].tpb);
+            add(ma, cand[w].s16, cand[w].r16, cand[w].grid, cand[w].tpb);
             for (const auto& sp : kSplits)
-                if (sp[0] != cand[lo].s16 || sp[1] != cand[lo].r16) add(RDC_ALGO_MESH, sp[0], sp[1], cand[lo].grid, 0);
+                if (sp[0] != cand[lo].s16 || sp[1] != cand[lo].r16) add(ma, sp[0], sp[1], cand[lo].grid, 0);
             w = stage(lo);
             const int s16 = cand[w].s16, r16 = cand[w].r16;
             lo = nc;
-            add(RDC_ALGO_MESH, s16, r16, cand[w].grid, cand[w].tpb);
+            add(ma, s16, r16, cand[w].grid, cand[w].tpb);
             for (int bpc : {1, 2, 3, 4})  // (grid 0 = automatic = 2 per CU)
-                if (bpc * cus != (cand[lo].grid ? cand[lo].grid : 2 * cus)) add(RDC_ALGO_MESH, s16, r16, bpc * cus, 0);
+                if (bpc * cus != (cand[lo].grid ? cand[lo].grid : 2 * cus)) add(ma, s16, r16, bpc * cus, 0);
             w = stage(lo);
             const int grid = cand[w].grid;
             lo = nc;
-            add(RDC_ALGO_MESH, s16, r16, grid, cand[w].tpb);
+            add(ma, s16, r16, grid, cand[w].tpb);
             for (int tpb : {1, 2, 4, 8})  // (tpb 0 = the default, 2 per reduce block)
-                if (tpb != (cand[lo].tpb ? cand[lo].tpb : 2)) add(RDC_ALGO_MESH, s16, r16, grid, tpb);
+                if (tpb != (cand[lo].tpb ? cand[lo].tpb : 2)) add(ma, s16, r16, grid, tpb);
             w = stage(lo);
         } else {
             lo = nc;

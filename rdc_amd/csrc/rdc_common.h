@@ -28,8 +28,10 @@ enum {
     RDC_ALGO_RING = 1,  // the reference's ring: n-1 reduce-scatter + n-1 allgather steps
     RDC_ALGO_MESH = 2,  // direct all-links exchange, same per-chunk accumulation order
     RDC_ALGO_ONESHOT = 3,  // small buffers: every rank pushes all of it, every rank folds (one hand-off)
-    RDC_ALGO_TREE = 4      // the reference's tree ORDER (TryAllreduceTree, buffers <= rdc_reduce_ring_mincount),
+    RDC_ALGO_TREE = 4,     // the reference's tree ORDER (TryAllreduceTree, buffers <= rdc_reduce_ring_mincount),
                            // moved like the one-shot: every rank folds all n inputs in the tree's order
+    RDC_ALGO_MESH_PULL = 5  // the mesh moved by remote LOADS: ranks stage their chunks in their own scratch,
+                            // owners pull and fold, peers pull the results (same fold order)
 };
 
 // launch kinds (recorded on the device: the next launch reads the previous kind)
@@ -100,6 +102,7 @@ struct CollArgs {
     uint32_t* launch_kind;               // local: kind of the last completed launch
     uint32_t tag;                        // communicator's tag on its channel: bits 0-7 of every seq
     int kind;                            // this launch's RDC_KIND_*
+    int pull;                            // mesh: 1 = pull mode (RDC_ALGO_MESH_PULL, mesh_pull_body)
     int bcast_split;                     // broadcast: root -> forwarder per tile -> other ranks (n >= 3)
     uint64_t half_bytes;                 // one-shot: offset of the slot half used by odd seq
     uint64_t total_bytes;                // one-shot: whole buffer bytes

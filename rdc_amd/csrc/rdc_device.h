@@ -163,6 +163,28 @@ __device__ __forceinline__ void st_elem_wt(void* p, T v) {
 // slots: streaming `nt` stores) or a peer's scratch (write-through, above).
 enum { kDstLocal = 0, kDstPeer = 1 };
 
+// System-scope loads for bytes READ FROM a peer's scratch (pull-mode mesh):
+// `sc0 sc1` loads are coherent at system scope whatever memory type the
+// driver gave the IPC import, so a line of the peer's memory cached in this
+// XCD's L2 by an earlier launch (an NC import) is not returned stale — the
+// load-side twin of the write-through stores above.  16-B form through a
+// wave-uniform descriptor, narrow form as relaxed system-scope atomic loads.
+__device__ __forceinline__ v4u ld16_sys(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kWtAux);
+}
+template <typename W>
+__device__ __forceinline__ W ld_sys(const W* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// one element of type T (any 1/2/4/8-byte type) read at system scope
+template <typename T>
+__device__ __forceinline__ T ld_elem_sys(const void* p) {
+    typedef typename std::conditional<sizeof(T) == 1, uint8_t,
+            typename std::conditional<sizeof(T) == 2, uint16_t,
+            typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type>::type>::type W;
+    return __builtin_bit_cast(T, ld_sys(reinterpret_cast<const W*>(p)));
+}
+
 // ------------------------------------------------------------- hand-off ----
 // Hand-off flags are 64-bit words holding a launch's sequence number:
 //   seq = (counter << kTagBits) | tag
@@ -373,6 +395,66 @@ __device__ __forceinline__ void block_copy(char* __restrict__ dst, const char* _
     else if ((x & 3) == 0) block_copy_words<DST, uint32_t>(dst, src, len);
     else if ((x & 1) == 0) block_copy_words<DST, uint16_t>(dst, src, len);
     else block_copy_words<DST, uint8_t>(dst, src, len);
+}
+
+// dst (this GPU's memory) = src (a PEER's scratch), every load at system
+// scope (ld16_sys / ld_sys): the pull-mode mesh's gather.  Congruent mod 16:
+// 16-B lanes through one descriptor per window of U x blockDim vectors (8 KiB
+// x U in flight per 256-thread block); otherwise the widest common word.
+template <typename W>
+__device__ __forceinline__ void block_pull_words(char* dst, const char* src, uint64_t len) {
+    const uint64_t mis = (uint64_t)(uintptr_t)src & (sizeof(W) - 1);
+    uint64_t head = mis ? sizeof(W) - mis : 0;
+    if (head > len) head = len;
+    const uint64_t nw = (len - head) / sizeof(W);
+    const uint64_t tail_start = head + nw * sizeof(W);
+    const unsigned tid = threadIdx.x;
+    if (tid < head) dst[tid] = (char)ld_sys(reinterpret_cast<const uint8_t*>(src) + tid);
+    if (tid < len - tail_start)
+        dst[tail_start + tid] = (char)ld_sys(reinterpret_cast<const uint8_t*>(src) + tail_start + tid);
+    const W* s = reinterpret_cast<const W*>(src + head);
+    W* d = reinterpret_cast<W*>(dst + head);
+    for (uint64_t i = tid; i < nw; i += blockDim.x) d[i] = ld_sys(s + i);
+}
+
+__device__ __forceinline__ void block_copy_pull(char* __restrict__ dst, const char* __restrict__ src, uint64_t len) {
+    const uintptr_t x = ((uintptr_t)dst ^ (uintptr_t)src) & 15;
+    if (x != 0) {
+        if ((x & 7) == 0) block_pull_words<uint64_t>(dst, src, len);
+        else if ((x & 3) == 0) block_pull_words<uint32_t>(dst, src, len);
+        else if ((x & 1) == 0) block_pull_words<uint16_t>(dst, src, len);
+        else block_pull_words<uint8_t>(dst, src, len);
+        return;
+    }
+    const uint64_t mis = (uint64_t)(uintptr_t)src & 15;
+    uint64_t head = mis ? (16 - mis) : 0;
+    if (head > len) head = len;
+    const uint64_t nvec = (len - head) >> 4;
+    const uint64_t tail_start = head + (nvec << 4);
+    const unsigned tid = threadIdx.x;
+    if (tid < head) dst[tid] = (char)ld_sys(reinterpret_cast<const uint8_t*>(src) + tid);
+    if (tid < len - tail_start)
+        dst[tail_start + tid] = (char)ld_sys(reinterpret_cast<const uint8_t*>(src) + tail_start + tid);
+    const v4u* s = reinterpret_cast<const v4u*>(src + head);
+    v4u* d = reinterpret_cast<v4u*>(dst + head);
+    constexpr int U = 8;
+    const uint64_t step = (uint64_t)blockDim.x;
+    for (uint64_t ib = 0; ib < nvec; ib += U * step) {
+        const __amdgpu_buffer_rsrc_t rs = wt_rsrc(s + ib);
+        const uint64_t i = ib + tid;
+        if (ib + U * step <= nvec) {
+            v4u v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ld16_sys(rs, (uint32_t)((tid + u * step) * 16));
+#pragma unroll
+            for (int u = 0; u < U; ++u) st16_nt(d + i + u * step, v[u]);
+        } else {
+            for (int u = 0; u < U; ++u) {
+                if (i + u * step >= nvec) break;
+                st16_nt(d + i + u * step, ld16_sys(rs, (uint32_t)((tid + u * step) * 16)));
+            }
+        }
+    }
 }
 
 }  // namespace rdc_amd

@@ -360,6 +360,182 @@ __device__ void mesh_body(const CollArgs& a, uint64_t seq) {
     }
 }
 
+// ================================================== pull-mode mesh ===
+// The same owner-computes exchange and fold order as k_mesh, moved by REMOTE
+// LOADS instead of remote stores (algo RDC_ALGO_MESH_PULL, an autotune
+// candidate beside push: which direction xGMI serves faster is measured, not
+// assumed — bench.py's xgmi_probe times both):
+//   stage  : every other chunk c's tile t -> MY OWN scratch, RS slot c
+//            (local write-through stores), then owner c's flag (row r, t);
+//   reduce : owner r loads its chunk's tile from every peer's RS slot r
+//            (system-scope loads over the link), folds in the ring order of
+//            chunk r, stores the user tile and MY AG slot r (local), then
+//            every peer's flag (row n + r, t);
+//   gather : tile t of chunk c loaded from owner c's AG slot c (remote).
+// Every element still folds x[r-1], x[r-2], ..., x[r] — bit-identical to the
+// ring.  Scratch reuse across launches needs no gate in either direction: a
+// rank finishes a launch only after gathering every tile of every chunk,
+// which each owner folds only after loading every staged tile of it, and an
+// owner overwrites its AG slot for tile t only after folding the NEXT
+// launch's tile t, which needs every peer's next-launch stage.
+template <int OP, typename T, int NMAX>
+__device__ void pull_fold_range(const CollArgs& a, char* own, const char* const* src, char* res, uint64_t tlen) {
+    const int n = a.n, r = a.rank;
+    const unsigned tid = threadIdx.x;
+    auto fold_elem = [&](uint64_t e) {
+        auto val = [&](int q) -> T {
+            return q == r ? *reinterpret_cast<const T*>(own + e) : ld_elem_sys<T>(src[q] + e);
+        };
+        T acc = val((r - 1 + n) % n);
+        for (int k = 2; k <= n; ++k) acc = OpF<OP>::apply(val((r - k + n) % n), acc);
+        *reinterpret_cast<T*>(own + e) = acc;
+        st_elem_wt<T>(res + e, acc);
+    };
+    const int q0 = (r + 1) % n;  // every src[q] and res share one alignment (slot base + mis)
+    if ((((uintptr_t)own ^ (uintptr_t)src[q0]) & 15) != 0) {
+        for (uint64_t e = (uint64_t)tid * sizeof(T); e < tlen; e += (uint64_t)kBlock * sizeof(T)) fold_elem(e);
+        return;
+    }
+    const uint64_t mis16 = (uint64_t)(uintptr_t)own & 15;
+    uint64_t head = mis16 ? 16 - mis16 : 0;
+    if (head > tlen) head = tlen;
+    const uint64_t nvec = (tlen - head) >> 4;
+    const uint64_t tail = head + (nvec << 4);
+    {
+        const uint64_t nh = head / sizeof(T), nt = (tlen - tail) / sizeof(T);
+        if (tid < nh) fold_elem(tid * sizeof(T));
+        else if (tid >= 64 && tid - 64 < nt) fold_elem(tail + (tid - 64) * sizeof(T));
+    }
+    constexpr int U = NMAX <= 8 ? 2 : 1;
+    const uint64_t stride = kBlock;
+    for (uint64_t ib = 0; ib < nvec; ib += U * stride) {
+        const uint64_t i = ib + tid;
+        v4u v[U][NMAX];
+        bool live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) live[u] = i + u * stride < nvec;
+#pragma unroll
+        for (int k = 1; k <= NMAX; ++k) {
+            if (k <= n) {
+                const int q = (r - k + n) % n;  // x[r-1], x[r-2], ..., x[r]
+                if (q == r) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (live[u]) v[u][k - 1] = ld16(own + head + (i + u * stride) * 16);
+                } else {
+                    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(src[q] + head + ib * 16);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (live[u]) v[u][k - 1] = ld16_sys(rs, (uint32_t)((tid + u * stride) * 16));
+                }
+            }
+        }
+        const __amdgpu_buffer_rsrc_t res_rs = wt_rsrc(res + head + ib * 16);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!live[u]) continue;
+            v4u acc = v[u][0];
+#pragma unroll
+            for (int k = 2; k <= NMAX; ++k)
+                if (k <= n) acc = reduce16<OP, T>(v[u][k - 1], acc);
+            st16(own + head + (i + u * stride) * 16, acc);
+            st16_wt(res_rs, (uint32_t)((tid + u * stride) * 16), acc);
+        }
+    }
+}
+
+template <int OP, typename T, int NMAX>
+__device__ void mesh_pull_body(const CollArgs& a, uint64_t seq) {
+    const int n = a.n, r = a.rank;
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    int b = blockIdx.x;
+    int tmax = 0;
+    for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
+    __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
+
+    if (b < a.nb_scatter) {
+        // ---- stage: my copy of chunk c's tile t -> my RS slot c, then owner c's flag
+        const int items = (n - 1) * tmax;
+        for (int it = b; it < items; it += a.nb_scatter) {
+            const int t = it / (n - 1);
+            const int c = (r + 1 + it % (n - 1)) % n;
+            if (t >= a.tiles[c]) continue;
+            const uint64_t toff = (uint64_t)t * a.tile_bytes;
+            uint64_t tlen = a.len[c] - toff;
+            if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+            char* dst = a.rs[r] + (uint64_t)c * a.slot_bytes + a.mis[c];
+            if (a.units)
+                for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
+                    block_copy<kDstPeer>(dst + (p - a.off[c]), usr, l);
+                });
+            else
+                block_copy<kDstPeer>(dst + toff, a.user + a.off[c] + toff, tlen);
+            block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, seq, a.uc);
+        }
+        return;
+    }
+    b -= a.nb_scatter;
+    if (b < a.nb_reduce) {
+        // ---- reduce: chunk r, tile t, once all n-1 peers staged it
+        __shared__ const char* s_src[RDC_MAX_RANKS];
+        for (int t = b; t < a.tiles[r]; t += a.nb_reduce) {
+            if (threadIdx.x < (unsigned)(n - 1)) {
+                const int p = (r + 1 + threadIdx.x) % n;
+                s_flags[threadIdx.x] = a.flags[r] + (uint64_t)p * a.max_tiles + t;
+            }
+            __syncthreads();
+            if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return;
+            const uint64_t toff = (uint64_t)t * a.tile_bytes;
+            uint64_t tlen = a.len[r] - toff;
+            if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+            const uint64_t slot_r = (uint64_t)r * a.slot_bytes;
+            if (a.units) {
+                for_unit_pieces(a, a.off[r] + toff, a.off[r] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
+                    const uint64_t co = a.mis[r] + (p - a.off[r]);
+                    if (threadIdx.x < (unsigned)n) s_src[threadIdx.x] = a.rs[threadIdx.x] + slot_r + co;
+                    __syncthreads();
+                    pull_fold_range<OP, T, NMAX>(a, usr, s_src, a.ag[r] + slot_r + co, l);
+                    __syncthreads();  // s_src is rewritten for the next piece
+                });
+            } else {
+                const uint64_t co = a.mis[r] + toff;
+                if (threadIdx.x < (unsigned)n) s_src[threadIdx.x] = a.rs[threadIdx.x] + slot_r + co;
+                __syncthreads();
+                pull_fold_range<OP, T, NMAX>(a, a.user + a.off[r] + toff, s_src, a.ag[r] + slot_r + co, tlen);
+            }
+            if (threadIdx.x < (unsigned)(n - 1)) {
+                const int p = (r + 1 + threadIdx.x) % n;
+                s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
+            }
+            block_publish(s_flags, n - 1, seq, a.uc);
+            __syncthreads();
+        }
+        return;
+    }
+    b -= a.nb_reduce;
+    // ---- gather: owner c's result tile t (its AG slot c) -> my user buffer
+    const int items = (n - 1) * tmax;
+    for (int it = b; it < items; it += a.nb_gather) {
+        const int t = it / (n - 1);
+        const int c = (r + 1 + it % (n - 1)) % n;
+        if (t >= a.tiles[c]) continue;
+        if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
+        __syncthreads();
+        if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_AG, a.uc)) return;
+        const uint64_t toff = (uint64_t)t * a.tile_bytes;
+        uint64_t tlen = a.len[c] - toff;
+        if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+        const char* src = a.ag[c] + (uint64_t)c * a.slot_bytes + a.mis[c];
+        if (a.units)
+            for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
+                block_copy_pull(usr, src + (p - a.off[c]), l);
+            });
+        else
+            block_copy_pull(a.user + a.off[c] + toff, src + toff, tlen);
+        __syncthreads();
+    }
+}
+
 // ======================================================= ring allreduce ===
 // own[i] = OP(own[i], recv[i]) — reducer(src=reducebuf, dst=sendrecvbuf)
 // (communicator_collective.cc:174-176), element-wise head/tail + 16-B body.
@@ -817,7 +993,10 @@ template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
     const uint64_t t0 = wall_clock64();
     const uint64_t seq = launch_seq(a);
-    if (!channel_failed(a)) mesh_body<OP, T, NMAX>(a, seq);
+    if (!channel_failed(a)) {
+        if (a.pull) mesh_pull_body<OP, T, NMAX>(a, seq);
+        else mesh_body<OP, T, NMAX>(a, seq);
+    }
     trace_block(a, t0);
     launch_done(a, seq);
 }

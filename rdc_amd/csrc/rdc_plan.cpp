@@ -377,11 +377,15 @@ int PlanTreeProgram(int n, int* dst, int* src) {
 //   mesh: scatter every other chunk to its owner (load user, store remote);
 //         fold own chunk (load n-1 slots + user, store user + n-1 remote);
 //         gather every other chunk (load own AG slot, store user)
+//   mesh (pull): stage every other chunk in own scratch (load user, store
+//         local); fold own chunk (load n-1 peers' staged tiles remotely +
+//         user, store user + own AG slot); gather (load owners' AG, store user)
 //   one-shot / tree: push the whole buffer to n-1 peers (each push loads the
 //         user bytes again), fold every element over the n inputs (load
 //         n-1 slots + user, store user)
-// A remote store is counted at the rank that issues it (the counters of the
-// issuing GPU's L2 see it); egress = those remote bytes.
+// A remote store or load is counted at the rank that issues it (the counters
+// of the issuing GPU's L2 see it); egress = bytes that leave this rank's
+// memory for a peer (its remote stores; for the pull mode, what peers load).
 HbmBytes ModelHbmBytes(int n, uint64_t count, size_t esz, int algo) {
     HbmBytes h;
     if (n < 2 || count == 0) return h;
@@ -408,6 +412,14 @@ HbmBytes ModelHbmBytes(int n, uint64_t count, size_t esz, int algo) {
             rd += others + (uint64_t)n * len[r] + others;
             wr += others + (uint64_t)n * len[r] + others;
             eg += others + (uint64_t)(n - 1) * len[r];
+        } else if (algo == RDC_ALGO_MESH_PULL) {
+            // stage others locally; fold loads n-1 peers' staged tiles (remote
+            // loads, counted here: this GPU's L2 issues them) + user, stores
+            // user + own AG slot; gather loads owners' results (remote)
+            const uint64_t others = S - len[r];
+            rd += others + (uint64_t)n * len[r] + others;
+            wr += others + 2 * len[r] + others;
+            eg += others + (uint64_t)(n - 1) * len[r];  // what peers load from this rank's memory
         } else {  // one-shot / tree order
             rd += (uint64_t)(n - 1) * S + (uint64_t)n * S;
             wr += (uint64_t)(n - 1) * S + S;

@@ -76,7 +76,7 @@ def run_group(comms, inputs, dtype, op, algo, pads=None):
     return [from_dev(bufs[r], pads[r] * esz, count, dtype) for r in range(n)]
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3])
+@pytest.mark.parametrize("algo", [1, 2, 3, 5])
 @pytest.mark.parametrize("dtype,op", VALID)
 def test_group3_all_types(group3, dtype, op, algo):
     rng = np.random.default_rng(77 + dtype * 8 + op)
@@ -161,7 +161,7 @@ def test_group_repeated_calls(group3):
     rng = np.random.default_rng(9)
     for it in range(40):
         count = int(rng.integers(1, 70000))
-        algo = int(rng.integers(0, 4))
+        algo = int(rng.choice([0, 1, 2, 3, 5]))
         inputs = [rng.standard_normal(count).astype(np.float32) for _ in range(3)]
         want = O.expected_allreduce(inputs, O.DT_FLOAT32, O.OP_SUM)
         got = run_group(group3, inputs, O.DT_FLOAT32, O.OP_SUM, algo)
@@ -229,7 +229,7 @@ def test_group_launch_counter_far_past_zeroed_flags(start, algo_counts=((2, 3000
             c.destroy()
 
 
-@pytest.mark.parametrize("algo", ["mesh", "ring", "oneshot"])
+@pytest.mark.parametrize("algo", ["mesh", "ring", "oneshot", "mesh_pull"])
 def test_group_graph_capture_replay(group2, algo):
     """Launch sequence numbers live on the device, so a captured allreduce
     replays correctly (graph per rank, several replays with fresh inputs)."""
@@ -396,6 +396,10 @@ def test_mp_allreduce(world):
         {"count": 1 << 20, "dtype": 10, "op": 2},
         {"count": 3 << 20, "dtype": 7, "op": 1, "algo": 1},
         {"count": 5 << 20, "dtype": 6, "op": 2, "algo": 2},     # 20 MiB > scratch: 2 pieces
+        {"count": 5 << 20, "dtype": 6, "op": 2, "algo": 5},     # the pull-mode mesh, 2 pieces
+        {"count": 1001, "dtype": 6, "op": 2, "algo": 5, "pad": 4},
+        {"count": 100003, "dtype": 10, "op": 1, "algo": 5, "pad_per_rank": 2},
+        {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1024, 7, 0, 100003, 1, 65536], "algo": 5},
         {"count": 77777, "dtype": 1, "op": 3, "comm": "second"},
         {"count": 70000, "dtype": 11, "op": 2, "reps": 3},
         {"count": 123457, "dtype": 0, "kind": "broadcast", "root": world - 1},
@@ -688,7 +692,7 @@ def fuzz_cases(seed, world, n=40):
         elif kind == "allreduce":
             dt, op = rng.choice(pairs)
             count = max(1, int(2 ** rng.uniform(0, 24.6)))
-            c = {"count": count, "dtype": dt, "op": op, "algo": rng.choice([0, 1, 2, 3]), "seed": 0x5EED0000 + sd}
+            c = {"count": count, "dtype": dt, "op": op, "algo": rng.choice([0, 1, 2, 3, 5]), "seed": 0x5EED0000 + sd}
             if rng.random() < 0.5:  # the ranks' buffers differ mod 16 (element-aligned)
                 c["pad_per_rank"] = esz[dt] * rng.choice([1, 2, 3])
             cases.append(c)
@@ -699,7 +703,7 @@ def fuzz_cases(seed, world, n=40):
             dt, op = rng.choice([(6, 2), (2, 0), (10, 2), (7, 1)])
             counts = [max(0, int(2 ** rng.uniform(-1, 19))) for _ in range(rng.randint(1, 12))]
             cases.append({"count": 0, "dtype": dt, "op": op, "kind": "coalesced", "counts": counts,
-                          "algo": rng.choice([0, 1, 2, 3]), "seed": 0x5EED0000 + sd})
+                          "algo": rng.choice([0, 1, 2, 3, 5]), "seed": 0x5EED0000 + sd})
     return cases
 
 
@@ -740,8 +744,8 @@ def test_mp_across_devices(world):
     hand-offs after its timed region)."""
     if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
         pytest.skip("needs 2 or more GPUs")
-    cases = [{"count": 1001, "dtype": 6, "op": 2, "algo": a} for a in (0, 1, 2, 3)]
-    cases += [{"count": (16 << 20) + 5, "dtype": 6, "op": 2, "algo": a} for a in (1, 2)]
+    cases = [{"count": 1001, "dtype": 6, "op": 2, "algo": a} for a in (0, 1, 2, 3, 5)]
+    cases += [{"count": (16 << 20) + 5, "dtype": 6, "op": 2, "algo": a} for a in (1, 2, 5)]
     cases += [{"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"},
               {"count": (40 << 20) + 3, "dtype": 1, "op": 0, "kind": "host_allreduce"},
               {"count": (3 << 20) + 5, "dtype": 0, "kind": "broadcast", "root": world - 1}]
@@ -791,7 +795,8 @@ def test_mp_full_size_cfg3_cfg4_eight_ranks():
         pytest.skip("no GPU")
     cases = [{"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 2, "digest": True},
              {"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 1, "digest": True, "last_launch": True},
-             {"count": (1 << 30) // 2, "dtype": 10, "op": 2, "algo": 2, "digest": True}]
+             {"count": (1 << 30) // 2, "dtype": 10, "op": 2, "algo": 2, "digest": True},
+             {"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 5, "digest": True}]
     tmp = run_mp(8, cases, timeout=600, env_extra={"RDC_SCRATCH_BYTES": "4080M"})
     want = {6: full_digest((1 << 30) // 4, 6, 8), 10: full_digest((1 << 30) // 2, 10, 8)}
     for i, c in enumerate(cases):
@@ -813,7 +818,9 @@ def test_mp_cfg5_exact_shape_eight_ranks():
     import hashlib
     K, per = 1024, 1 << 18
     cases = [{"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [per] * K, "reps": 2,
-              "digest": True}]
+              "digest": True},
+             {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [per] * K, "reps": 2,
+              "digest": True, "algo": 5}]   # the pull-mode mesh over the same unit table
     tmp = run_mp(8, cases, timeout=600, env_extra={"RDC_SCRATCH_BYTES": "4080M"})
     h = hashlib.sha256()
     for b in range(K):
@@ -821,8 +828,9 @@ def test_mp_cfg5_exact_shape_eight_ranks():
         for _ in range(2):
             O.allreduce_ring(xs, 6, 2)
         h.update(xs[0].tobytes())
-    for r in range(8):
-        assert open(os.path.join(tmp, "case0_rank%d.sha" % r)).read() == h.hexdigest(), r
+    for i in range(2):
+        for r in range(8):
+            assert open(os.path.join(tmp, "case%d_rank%d.sha" % (i, r))).read() == h.hexdigest(), (i, r)
 
 
 def test_mp_forced_oversized_grid_four_ranks():
@@ -886,7 +894,7 @@ def test_mp_full_grid_beside_resident_service():
 def test_mp_autotune_agrees_and_stays_bit_exact(world):
     """RdcCommAutotune (bench.py runs it before the timed region at N > 1):
     every rank keeps the same winner (times agreed by a MAX allreduce), the
-    stages cover the schedules (ring, mesh, one-shot where it fits) and then
+    stages cover the schedules (ring, mesh, pull-mode mesh, one-shot where it fits) and then
     the winner's shape (mesh split / grid / tiles per reduce block, or ring
     grid / tiles per block),
     and the allreduces on the chosen shape stay bit-exact."""
@@ -910,12 +918,12 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
     small = [json.load(open(os.path.join(tmp, "case0_rank%d.tune" % r))) for r in range(world)]
     assert all(t == small[0] for t in small), small
-    # a one-shot size: the rule's schedule (the one-shot) first, then ring and mesh; the
-    # winner's shape if it has one
-    sched = [c["schedule"] for c in small[0]["candidates"][:3]]
-    assert sched[0] == "oneshot" and sorted(sched) == ["mesh", "oneshot", "ring"], small[0]
+    # a one-shot size: the rule's schedule (the one-shot) first, then ring, mesh and the
+    # pull-mode mesh; the winner's shape if it has one
+    sched = [c["schedule"] for c in small[0]["candidates"][:4]]
+    assert sched[0] == "oneshot" and sorted(sched) == ["mesh", "mesh_pull", "oneshot", "ring"], small[0]
     if small[0]["chosen"]["schedule"] == "oneshot":
-        assert len(small[0]["candidates"]) == 3, small[0]
+        assert len(small[0]["candidates"]) == 4, small[0]
     tunes = [json.load(open(os.path.join(tmp, "case1_rank%d.tune" % r))) for r in range(world)]
     assert all(t == tunes[0] for t in tunes), tunes  # identical bits on every rank
     t = tunes[0]
@@ -923,15 +931,17 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
     assert t["chosen"] is not None and t["chosen"] in cands, t
     # every candidate timed in 3 rounds: median inside its spread
     assert all(c["spread_ms"][0] <= c["ms"] <= c["spread_ms"][1] for c in cands), t
-    # stage 0: the rule's schedule first (ring at n = 2, mesh from n = 3), the other one, the
-    # one-shot where it fits; then (mesh) 7 splits, 4 grids, 4 tilings or (ring) 2 grids, 5
-    # tilings, each later stage re-timing its predecessor's winner first
+    # stage 0: the rule's schedule first (ring at n = 2, mesh from n = 3), the other two of
+    # ring / mesh / pull-mode mesh, the one-shot where it fits; then (either mesh) 7 splits,
+    # 4 grids, 4 tilings or (ring) 2 grids, 5 tilings, each later stage re-timing its
+    # predecessor's winner first
     rule = "ring" if world == 2 else "mesh"
-    s0 = 3 if cands[2]["schedule"] == "oneshot" else 2
-    assert cands[0]["schedule"] == rule and {c["schedule"] for c in cands[:2]} == {"ring", "mesh"}, t
+    s0 = 4 if cands[3]["schedule"] == "oneshot" else 3
+    assert cands[0]["schedule"] == rule and {c["schedule"] for c in cands[:3]} == {"ring", "mesh", "mesh_pull"}, t
     if t["chosen"]["schedule"] != "oneshot":
-        last = 4 if t["chosen"]["schedule"] == "mesh" else 5
-        assert len(cands) == s0 + (15 if t["chosen"]["schedule"] == "mesh" else 7), t
+        mesh_like = t["chosen"]["schedule"] in ("mesh", "mesh_pull")
+        last = 4 if mesh_like else 5
+        assert len(cands) == s0 + (15 if mesh_like else 7), t
         assert all(c["schedule"] == t["chosen"]["schedule"] for c in cands[s0:]), t
         # the last stage's incumbent stays unless another beats it by more than 3 %
         fin = cands[-last:]
@@ -1013,16 +1023,18 @@ def test_mp_mixed_schedule_chain():
     across processes."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    cases = [{"count": 20011, "dtype": 6, "op": 2, "kind": "algo_chain", "algos": [3, 3, 2, 3, 1, 3, 3, 2, 2, 1, 3]}]
+    cases = [{"count": 20011, "dtype": 6, "op": 2, "kind": "algo_chain", "algos": [3, 3, 2, 3, 1, 3, 3, 2, 2, 1, 3]},
+             # the pull-mode mesh between every other schedule, back to back
+             {"count": 300007, "dtype": 6, "op": 2, "kind": "algo_chain", "algos": [5, 5, 3, 5, 1, 5, 2, 5, 3, 3, 5]}]
     tmp = run_mp(3, cases)
-    c = cases[0]
-    inputs = [O.fill(c["count"], 6, 0x5EED0000, r) for r in range(3)]
-    bufs = [x.copy() for x in inputs]
-    for _ in c["algos"]:
-        O.allreduce_ring(bufs, 6, 2)
-    for r in range(3):
-        got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
-        assert got.tobytes() == np.frombuffer(bufs[r].tobytes(), dtype=np.uint8).tobytes(), r
+    for i, c in enumerate(cases):
+        inputs = [O.fill(c["count"], 6, 0x5EED0000, r) for r in range(3)]
+        bufs = [x.copy() for x in inputs]
+        for _ in c["algos"]:
+            O.allreduce_ring(bufs, 6, 2)
+        for r in range(3):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(bufs[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
 
 
 # ------------------------------------------------------- coalesced (buckets)
@@ -1050,7 +1062,7 @@ def run_group_coalesced(comms, bufsets, dtype, op, algo, pads):
 BUCKETS = [[1024] * 6, [1, 2, 3, 1001, 0, 7], [4099, 1 << 16, 3], [0, 0, 5], [17, 100003, 1, 2]]
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+@pytest.mark.parametrize("algo", [0, 1, 2, 3, 5])
 @pytest.mark.parametrize("dtype,op", [(6, 2), (10, 2), (11, 2), (7, 1), (2, 0), (0, 3), (4, 2)])
 def test_group3_coalesced(group3, dtype, op, algo):
     """Coalesced allreduce == one reference allreduce per bucket, bit for bit:
@@ -1067,7 +1079,7 @@ def test_group3_coalesced(group3, dtype, op, algo):
                 assert same_bits(got[r][b], want, dtype), (counts, algo, b, r)
 
 
-@pytest.mark.parametrize("algo", [2, 1])
+@pytest.mark.parametrize("algo", [2, 1, 5])
 @pytest.mark.parametrize("fused,tile", [("1", "16K"), ("1", "0"), ("0", "16K")])
 def test_group_coalesced_mesh_unit_table(fused, tile, algo):
     """The mesh (algo 2) and the ring (algo 1) on a coalesced list move bytes

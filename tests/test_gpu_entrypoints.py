@@ -87,7 +87,7 @@ def test_bench_torchrun_two_ranks():
 
 # every hand-off kind the timed lines use, verified bit-exact in bench.py's
 # parity_checks
-PARITY_KEYS = ("cfg3_mesh", "cfg3_ring", "cfg4_fp16", "cfg5_buckets", "oneshot_512KiB", "service_host_4KiB",
+PARITY_KEYS = ("cfg3_mesh", "cfg3_ring", "cfg3_mesh_pull", "cfg4_fp16", "cfg5_buckets", "oneshot_512KiB", "service_host_4KiB",
                "tree_order", "broadcast_nonzero_root", "allgather_varsize")
 
 

@@ -324,8 +324,9 @@ def test_hbm_byte_model_closed_forms(n):
     bytes: ring 5(n-1)/n S loaded + 4(n-1)/n S stored per rank; mesh
     (3n-2)/n S each way; one-shot (2n-1) S loaded + n S stored; egress
     2(n-1)/n S for ring and mesh (what the link roofline counts) and (n-1) S
-    for the one-shot.  Ragged Split chunks: the rank sums keep the closed
-    forms exactly."""
+    for the one-shot; the pull-mode mesh loads what the mesh loads and
+    stores 2n S over the ranks.  Ragged Split chunks: the rank sums keep the
+    closed forms exactly."""
     for count in (n * 4096, n * 4096 + n - 1, 1001):
         S = 4 * count
         ring, mesh, one = hbm(n, count, 6, 1), hbm(n, count, 6, 2), hbm(n, count, 6, 3)
@@ -333,6 +334,9 @@ def test_hbm_byte_model_closed_forms(n):
         assert mesh["read_sum"] == mesh["write_sum"] == (3 * n - 2) * S
         assert one["read_sum"] == n * (2 * n - 1) * S and one["write_sum"] == n * n * S
         assert hbm(n, count, 6, 4) == one
+        pull = hbm(n, count, 6, 5)   # pull-mode mesh: same loads, one local result copy instead of n-1 remote
+        assert pull["read_sum"] == mesh["read_sum"] and pull["write_sum"] == 2 * n * S
+        assert pull["egress"] == mesh["egress"]
         if count % n == 0:
             assert ring["read"] * n == 5 * (n - 1) * S and ring["write"] * n == 4 * (n - 1) * S
             assert mesh["read"] * n == (3 * n - 2) * S
