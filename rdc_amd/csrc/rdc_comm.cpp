@@ -475,12 +475,33 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         }
     }
     mine.channel = cand ? cand->id : 0;
+    // a NEW channel may run the small-allreduce service only if no other
+    // channel of this process on this device may (one resident service block
+    // per process and GPU, LaunchGrid); agreed below (AND over ranks).  The
+    // slot is reserved under the lock when it is offered, so two threads
+    // creating communicators on one device at once cannot both take it; the
+    // reservation passes to the new channel, or is released (shared channel,
+    // a rank without the slot, an error on the way).
+    struct SvcSlot {
+        int device;
+        bool held = false;
+        explicit SvcSlot(int d) : device(d) {}
+        void release() {
+            if (!held) return;
+            std::lock_guard<std::mutex> lk(svc_registry().mu);
+            --svc_registry().channels[device];
+            held = false;
+        }
+        ~SvcSlot() { release(); }
+    } svc_slot(device);
     {
-        // a NEW channel may run the small-allreduce service only if no other
-        // channel of this process on this device may (one resident service
-        // block per process and GPU, LaunchGrid); agreed below (AND over ranks)
         std::lock_guard<std::mutex> lk(svc_registry().mu);
-        mine.svc_ok = (SmallService::Enabled() && svc_registry().channels[device] == 0) ? 1 : 0;
+        int& used = svc_registry().channels[device];
+        if (SmallService::Enabled() && used == 0) {
+            ++used;
+            svc_slot.held = true;
+        }
+        mine.svc_ok = svc_slot.held ? 1 : 0;
     }
     gethostname(mine.host, sizeof(mine.host) - 1);
     if (hipDeviceGetPCIBusId(mine.pci, sizeof(mine.pci) - 1, device) != hipSuccess) {
@@ -563,13 +584,13 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     // round 2: IPC handles of a new channel (unless shared) and of this
     // communicator's point-to-point region
     dbg("[rdc %d] %s\n", c->rank_, share ? "sharing the channel" : "alloc");
+    if (share || !svc_all) svc_slot.release();
     if (share) {
         c->Attach(cand);
     } else {
         c->AllocChannel();
-        if (svc_all) {
-            std::lock_guard<std::mutex> lk(svc_registry().mu);
-            ++svc_registry().channels[device];
+        if (svc_all) {  // the reserved slot now belongs to the channel (released by ~Channel)
+            svc_slot.held = false;
             c->ch_->svc_enabled = true;
             c->ch_->svc_counted = true;
         }

@@ -44,23 +44,28 @@ bool tracing() {
 }
 }  // namespace
 
-// {integer}{B,K,M,G} as the reference's ParseUnit (communicator_manager.cc:14-42);
+// {integer}{B,K,M,G} as the reference's ParseUnit (communicator_manager.cc:14-42)
+// into *out; false when unset or malformed (a warning names a malformed value)
+static bool env_bytes_parse(const char* name, size_t* out) {
+    const char* e = getenv(name);
+    if (!e || !*e) return false;
+    unsigned long long amt = 0;
+    char unit = 0, extra = 0;
+    const int k = sscanf(e, "%llu%c%c", &amt, &unit, &extra);
+    bool ok = k == 1 || (k == 2 && (unit == 'B' || unit == 'K' || unit == 'M' || unit == 'G'));
+    if (ok) {
+        const int shift = k == 1 || unit == 'B' ? 0 : unit == 'K' ? 10 : unit == 'M' ? 20 : 30;
+        *out = (size_t)amt << shift;
+    } else {
+        fprintf(stderr, "rdc: ignoring malformed %s=%s (expected an integer with an optional B/K/M/G unit)\n",
+                name, e);
+    }
+    return ok;
+}
 // 0 when unset or malformed
 static size_t env_bytes(const char* name) {
-    const char* e = getenv(name);
-    if (!e || !*e) return 0;
-    unsigned long long amt = 0;
-    char unit = 0;
-    const int k = sscanf(e, "%llu%c", &amt, &unit);
-    if (k == 1) return (size_t)amt;
-    if (k != 2) return 0;
-    switch (unit) {
-        case 'B': return (size_t)amt;
-        case 'K': return (size_t)amt << 10;
-        case 'M': return (size_t)amt << 20;
-        case 'G': return (size_t)amt << 30;
-        default: return 0;
-    }
+    size_t v = 0;
+    return env_bytes_parse(name, &v) ? v : 0;
 }
 
 size_t HostPieceBytes() {
@@ -77,8 +82,8 @@ size_t HostPieceBytes() {
 // 1 MiB; 4 MiB 0.46-0.49 vs 0.50-0.51; profiles/r03/host_inline_ab/)
 size_t HostInlineBytes() {
     static const size_t v = [] {
-        const char* e = getenv("RDC_HOST_INLINE_BYTES");
-        return e && *e ? env_bytes("RDC_HOST_INLINE_BYTES") : (size_t)16 << 20;
+        size_t x = 0;  // an explicit 0 keeps every host buffer in the pipeline; malformed = the default
+        return env_bytes_parse("RDC_HOST_INLINE_BYTES", &x) ? x : (size_t)16 << 20;
     }();
     return v;
 }
@@ -378,9 +383,14 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
             (void)hipEventSynchronize(h2d_done_[0]);  // the H2D still reads the caller's buffer
             throw;
         }
-        hip_check(hipMemcpyAsync(h, dev_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
-        hip_check(hipEventRecord(in_done_[0], comm_stream), "record");
-        SpinEvent(in_done_[0], "host allreduce");
+        try {
+            hip_check(hipMemcpyAsync(h, dev_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
+            hip_check(hipEventRecord(in_done_[0], comm_stream), "record");
+            SpinEvent(in_done_[0], "host allreduce");
+        } catch (...) {
+            (void)hipStreamSynchronize(comm_stream);  // no DMA into the caller's buffer outlives the call
+            throw;
+        }
         c->RaiseIfError(c->HostErrorWord());
         return;
     }
@@ -403,13 +413,13 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
             hip_check(hipMemcpyAsync(h + lo, dev_ + lo, hi - lo, hipMemcpyDeviceToHost, d2h_), "D2H");
         }
         hip_check(hipEventRecord(in_done_[0], d2h_), "record");
+        SpinEvent(in_done_[0], "host allreduce");
     } catch (...) {
         // no DMA into or out of the caller's buffer may outlive the call
         (void)hipStreamSynchronize(h2d_);
         (void)hipStreamSynchronize(d2h_);
         throw;
     }
-    SpinEvent(in_done_[0], "host allreduce");
     c->Check(comm_stream);  // a device-side failure surfaces here
 }
 

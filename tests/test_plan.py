@@ -308,6 +308,13 @@ def test_host_pipeline_knobs_parse_units():
     lens = [y - x for x, y in zip(c[16 << 20], c[16 << 20][1:])]
     assert lens[:3] == [256 << 10, 512 << 10, 1 << 20] and max(lens) <= 2 << 20 and sum(lens) == 16 << 20
     assert [y - x for x, y in zip(c[4 << 20], c[4 << 20][1:])] == [2 << 20, 2 << 20]
+    # an explicit 0 pipelines everything above one piece; a malformed value
+    # keeps the 16 MiB default (it used to act as 0)
+    z = host_pieces(sizes, {"RDC_HOST_PIECE_BYTES": "2M", "RDC_HOST_INLINE_BYTES": "0"})
+    assert len(z[4 << 20]) - 1 == 2 and len(z[16 << 20]) - 1 > 1
+    for bad in ("abc", "16 M", "4Q", "12MB"):
+        m = host_pieces(sizes, {"RDC_HOST_PIECE_BYTES": "2M", "RDC_HOST_INLINE_BYTES": bad})
+        assert m == a, bad
 
 
 def hbm(n, count, dtype, algo):
