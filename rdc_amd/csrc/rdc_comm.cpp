@@ -840,7 +840,7 @@ Communicator::Shape Communicator::ShapeFor(uint64_t total, int algo) const {
 
 // The mesh keeps more remote stores in flight with two blocks per CU (k_mesh:
 // 100 VGPRs, 4 blocks per CU fit): 1 GiB on 2 ranks 1.86 -> 1.65-1.69 ms at
-// 384-512 blocks (tools/mesh_sweep*.sh).  Ranks sharing a GPU get their share
+// 384-512 blocks (round-1 sweeps, profiles/r01/; tools/gpu_run.sh ab:).  Ranks sharing a GPU get their share
 // of the resident blocks through LaunchGrid.
 int Communicator::mesh_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_blocks : 2 * cus_min_; }
 

@@ -49,7 +49,7 @@ void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blo
         // ring: each block walks 2(n-1) hand-offs per tile, so one tile per
         // block.  mesh: ~2 tiles per reduce block, at least 64 KiB — every
         // tile costs a flag hand-off per role, and the tile sweep on one GPU
-        // (tools/tile_sweep.sh, profiles/r01/mesh_tile_sweep_group2.log)
+        // (profiles/r01/mesh_tile_sweep_group2.log)
         // found 4 tiles per reduce block too fine below 64 MB (16 MB:
         // 0.115 ms at 22 KiB tiles vs 0.071-0.075 ms at 64-128 KiB), and
         // 16 KiB floors slow at 4 MB (0.044 vs 0.034 ms at 64 KiB).

@@ -39,7 +39,7 @@ struct Piece {
 };
 
 // Mesh role split of the grid in sixteenths: scatter s16/16, reduce r16/16,
-// gather the rest (default 4 / 8 / 4: tools/mesh_split_sweep.sh, 2 ranks on one GPU,
+// gather the rest (default 4 / 8 / 4: profiles/r02/ split sweep, 2 ranks on one GPU,
 // 1 GiB 1.69 -> 1.54 ms at 512 blocks against 6 / 6 / 4 — the reduce role has
 // the most work per byte: n loads, n stores).
 struct MeshSplit {

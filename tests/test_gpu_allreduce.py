@@ -24,7 +24,8 @@ torch = pytest.importorskip("torch")
 
 # Ranks of a single-process group that share one GPU must run concurrently:
 # each gets ONE stream for the whole module, created up front, so every rank
-# sits on its own hardware queue (conftest sets GPU_MAX_HW_QUEUES=16).
+# sits on its own hardware queue (the box exports GPU_MAX_HW_QUEUES=4, HIP's
+# default; groups here have at most 3 ranks).
 # Creating fresh streams per call would eventually put two ranks on one
 # queue, serialising a waiting kernel in front of the one it waits for.
 class Group(list):
