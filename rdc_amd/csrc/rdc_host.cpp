@@ -397,6 +397,17 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
     // RDC_HOST_REG_AHEAD=a > 0: piece k's H2D waits for piece k-a's allreduce
     // (stream-ordered), so the input DMA runs at most a pieces ahead
     static const int ahead = env_int("RDC_HOST_REG_AHEAD", 0);
+    static const bool etrace = env_int("RDC_HOST_EVENT_TRACE", 0) != 0;
+    const auto h0 = std::chrono::steady_clock::now();
+    if (etrace)
+        while ((int)tev_.size() < 6 * K) {
+            hipEvent_t e;
+            hip_check(hipEventCreate(&e), "event");
+            tev_.push_back(e);
+        }
+    auto mark = [&](int k, int what, hipStream_t s) {
+        if (etrace) hip_check(hipEventRecord(tev_[(size_t)(6 * k + what)], s), "record");
+    };
     try {
         for (int k = 0; k < K; ++k) {
             const uint64_t lo = bounds[(size_t)k], hi = bounds[(size_t)k + 1];
@@ -404,13 +415,19 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
             piece_ranges(lo, hi, n, cb, ce, esz, roff, rlen);
             if (ahead > 0 && k >= ahead)
                 hip_check(hipStreamWaitEvent(h2d_, ar_done_[(size_t)(k - ahead)], 0), "wait");
+            mark(k, 0, h2d_);
             hip_check(hipMemcpyAsync(dev_ + lo, h + lo, hi - lo, hipMemcpyHostToDevice, h2d_), "H2D");
             hip_check(hipEventRecord(h2d_done_[(size_t)k], h2d_), "record");
+            mark(k, 1, h2d_);
             hip_check(hipStreamWaitEvent(comm_stream, h2d_done_[(size_t)k], 0), "wait");
+            mark(k, 2, comm_stream);
             c->AllreduceRanges(dev_ + lo, roff, rlen, dtype, op, comm_stream);
             hip_check(hipEventRecord(ar_done_[(size_t)k], comm_stream), "record");
+            mark(k, 3, comm_stream);
             hip_check(hipStreamWaitEvent(d2h_, ar_done_[(size_t)k], 0), "wait");
+            mark(k, 4, d2h_);
             hip_check(hipMemcpyAsync(h + lo, dev_ + lo, hi - lo, hipMemcpyDeviceToHost, d2h_), "D2H");
+            mark(k, 5, d2h_);
         }
         hip_check(hipEventRecord(in_done_[0], d2h_), "record");
         SpinEvent(in_done_[0], "host allreduce");
@@ -420,7 +437,38 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
         (void)hipStreamSynchronize(d2h_);
         throw;
     }
+    if (etrace)
+        TraceRegistered(K, bounds, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0)
+                                       .count());
     c->Check(comm_stream);  // a device-side failure surfaces here
+}
+
+// One line per call: the span from the first H2D's start to the last D2H's
+// end, each engine's busy time (sum of its pieces) and its idle time inside
+// the span, the allreduce time per piece, and the host's wall time for the
+// call — JSON after the tag, for tools to parse.
+void HostPath::TraceRegistered(int K, const std::vector<uint64_t>& bounds, double host_ms) {
+    hip_check(hipEventSynchronize(tev_[(size_t)(6 * K - 1)]), "trace sync");
+    auto at = [&](int k, int w) {
+        float ms = 0;
+        hip_check(hipEventElapsedTime(&ms, tev_[0], tev_[(size_t)(6 * k + w)]), "elapsed");
+        return (double)ms;
+    };
+    double busy[3] = {0, 0, 0};
+    std::string pieces;
+    for (int k = 0; k < K; ++k) {
+        const double t[6] = {at(k, 0), at(k, 1), at(k, 2), at(k, 3), at(k, 4), at(k, 5)};
+        for (int e = 0; e < 3; ++e) busy[e] += t[2 * e + 1] - t[2 * e];
+        char buf[160];
+        snprintf(buf, sizeof(buf), "%s[%llu,%.3f,%.3f,%.3f,%.3f,%.3f,%.3f]", k ? "," : "",
+                 (unsigned long long)(bounds[(size_t)k + 1] - bounds[(size_t)k]), t[0], t[1], t[2], t[3], t[4], t[5]);
+        pieces += buf;
+    }
+    const double span = at(K - 1, 5);
+    fprintf(stderr,
+            "[rdc host-reg] {\"pieces\": %d, \"span_ms\": %.3f, \"host_ms\": %.3f, \"busy_ms\": {\"h2d\": %.3f, "
+            "\"allreduce\": %.3f, \"d2h\": %.3f}, \"piece\": [%s]}\n",
+            K, span, host_ms, busy[0], busy[1], busy[2], pieces.c_str());
 }
 
 void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, int op, hipStream_t comm_stream) {

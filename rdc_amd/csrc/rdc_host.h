@@ -84,6 +84,11 @@ private:
     void AllreduceRegistered(Communicator* c, char* host, size_t count, int dtype, int op, hipStream_t comm_stream,
                              const std::vector<uint64_t>& bounds, const int64_t* cb, const int64_t* ce);
     std::vector<hipEvent_t> h2d_done_;  // registered path: one per piece
+    // RDC_HOST_EVENT_TRACE=1 (diagnostics): timing events around every
+    // piece's H2D, allreduce and D2H of the registered path, summarised per
+    // call on stderr — a complete timeline (every copy has its events)
+    std::vector<hipEvent_t> tev_;
+    void TraceRegistered(int K, const std::vector<uint64_t>& bounds, double host_ms);
 
     int device_;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
