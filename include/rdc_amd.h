@@ -319,6 +319,14 @@ int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4);
  * RDC_HOST_PIECE_RAMP): bounds[0..*out_n) = {0, ..., bytes}, piece k = [bounds[k],
  * bounds[k+1]) (one piece up to 16 MiB).  Writes at most max_bounds entries. */
 int RdcPlanHostPieces(size_t bytes, uint64_t* bounds, int max_bounds, int* out_n);
+/* The ranges of one host-path piece [lo, hi) (byte offsets of a buffer of
+ * `count` elements of `dtype`) over n ranks: off[q], len[q] (relative to lo)
+ * owned by rank q and folded in the ring order of Split chunk fold[q].
+ * balanced 0: the piece's bytes of chunk q go to rank q (fold[q] = q);
+ * balanced 1: each chunk's bytes are cut over the ranks in proportion to
+ * their length (RDC_HOST_BALANCE; the default with one rank per GPU). */
+int RdcPlanHostPieceRanges(int n, size_t count, int dtype, uint64_t lo, uint64_t hi, int balanced, uint64_t* off,
+                           uint64_t* len, int* fold);
 /* The automatic schedule for an allreduce of `bytes` over n ranks: returns
  * RDC_ALGO_ONESHOT (3), RDC_ALGO_RING (1, n = 2 beyond the one-shot) or
  * RDC_ALGO_MESH (2) (negative on bad arguments).

@@ -77,6 +77,8 @@ def _load():
         "RdcMemcpy": (i, [vp, vp, sz]),
         "RdcPlanLayout": (i, [i, sz, ctypes.POINTER(u64)]),
         "RdcPlanHbmBytes": (i, [i, sz, i, i, ctypes.POINTER(u64)]),
+        "RdcPlanHostPieceRanges": (i, [i, sz, i, u64, u64, i, ctypes.POINTER(u64), ctypes.POINTER(u64),
+                                       ctypes.POINTER(ctypes.c_int)]),
         "RdcPlanAutoAlgo": (i, [i, sz, sz, sz]),
         "RdcPlanHostPieces": (i, [sz, ctypes.POINTER(ctypes.c_uint64), i, ctypes.POINTER(i)]),
         "RdcPlanAllreduce": (i, [i, sz, i, sz, i, sz, i, ctypes.POINTER(u64), i, ctypes.POINTER(ctypes.c_int)]),

@@ -746,6 +746,21 @@ int RdcPlanHbmBytes(int n, size_t count, int dtype, int algo, uint64_t* out5) {
     });
 }
 
+int RdcPlanHostPieceRanges(int n, size_t count, int dtype, uint64_t lo, uint64_t hi, int balanced, uint64_t* off,
+                           uint64_t* len, int* fold) {
+    return guard([&] {
+        const size_t esz = rdc_dtype_size(dtype);
+        if (n < 1 || n > RDC_MAX_RANKS || esz == 0 || !off || !len || !fold || lo > hi || hi > (uint64_t)count * esz ||
+            lo % esz || hi % esz)
+            throw std::invalid_argument("rdc: bad argument");
+        int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+        SplitRanges((int64_t)count, n, cb, ce);
+        int8_t f[RDC_MAX_RANKS];
+        HostPieceRanges(lo, hi, n, cb, ce, esz, balanced != 0, off, len, f);
+        for (int q = 0; q < n; ++q) fold[q] = f[q];
+    });
+}
+
 int RdcPlanHostPieces(size_t bytes, uint64_t* bounds, int max_bounds, int* out_n) {
     return guard([&] {
         if (!bounds || !out_n || max_bounds < 2) throw std::invalid_argument("rdc: bad argument");

@@ -793,6 +793,7 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     memset(a, 0, sizeof(*a));
     a->n = n_;
     a->rank = rank_;
+    for (int c = 0; c < RDC_MAX_RANKS; ++c) a->fold[c] = (int8_t)c;
     a->slot_bytes = slot_bytes_;
     a->max_tiles = max_tiles_;
     for (int p = 0; p < n_; ++p) {
@@ -883,7 +884,7 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
 }
 
 void Communicator::AllreduceRanges(void* buf, const uint64_t* off, const uint64_t* len, int dtype, int op,
-                                   hipStream_t stream) {
+                                   hipStream_t stream, const int8_t* fold) {
     KernelSet ks;
     if (!get_kernels(dtype, op, &ks))
         throw std::invalid_argument("rdc: unsupported (dtype, op) = (" + std::to_string(dtype) + ", " +
@@ -907,7 +908,14 @@ void Communicator::AllreduceRanges(void* buf, const uint64_t* off, const uint64_
     const bool contiguous = first == 0 && sum == total;
     int algo = contiguous ? PickAlgo(RDC_ALGO_AUTO, total) : PickAlgo(RDC_ALGO_AUTO);
     if (algo == RDC_ALGO_ONESHOT && !contiguous) algo = RDC_ALGO_MESH;
-    LaunchRanges(ks, static_cast<char*>(buf), off, len, total, esz, algo, stream);
+    bool identity = true;
+    if (fold)
+        for (int c = 0; c < n_; ++c) {
+            if (fold[c] < 0 || fold[c] >= n_) throw std::invalid_argument("rdc: fold chunk out of range");
+            identity = identity && fold[c] == c;
+        }
+    if (!identity && algo == RDC_ALGO_RING) algo = RDC_ALGO_MESH;  // the ring's order is its schedule
+    LaunchRanges(ks, static_cast<char*>(buf), off, len, total, esz, algo, stream, nullptr, 0, identity ? nullptr : fold);
 }
 
 // The reference's small-buffer path (TryAllreduceTree: TryReduceTree to rank
@@ -955,8 +963,9 @@ void Communicator::LaunchTree(const KernelSet& ks, char* buf, uint64_t total, hi
 // off[c]+len[c]), folded in the ring order of c).
 void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* off, const uint64_t* len,
                                 uint64_t total, size_t esz, int algo, hipStream_t stream, const PackUnit* units,
-                                int nunits) {
+                                int nunits, const int8_t* fold) {
     algo = PickAlgo(algo, total);
+    if (fold && algo == RDC_ALGO_RING) throw std::logic_error("rdc: a fold order needs an owner-computes schedule");
     const bool mesh_like = algo == RDC_ALGO_MESH || algo == RDC_ALGO_MESH_PULL;
     if (units && !mesh_like && algo != RDC_ALGO_RING)
         throw std::logic_error("rdc: unit-table launch needs the mesh or ring schedule");
@@ -967,6 +976,7 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         FillArgsCommon(&a);
         a.kind = RDC_KIND_ONESHOT;
         a.user = buf;
+        if (fold) memcpy(a.fold, fold, (size_t)n_);
         memcpy(a.off, p.off, sizeof(a.off));
         memcpy(a.len, p.len, sizeof(a.len));
         memcpy(a.tiles, p.tiles, sizeof(a.tiles));
@@ -1001,6 +1011,7 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
             notify_ = nullptr;
         }
         a.user = buf;
+        if (fold) memcpy(a.fold, fold, (size_t)n_);
         memcpy(a.off, p.off, sizeof(a.off));
         memcpy(a.len, p.len, sizeof(a.len));
         memcpy(a.mis, p.mis, sizeof(a.mis));

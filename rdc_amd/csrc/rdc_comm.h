@@ -122,10 +122,13 @@ public:
     // (bit-identical), moved as fused launches over a chunk-major staging image
     void AllreduceCoalesced(void* const* bufs, const size_t* counts, int nbuf, int dtype, int op,
                             hipStream_t stream, int algo = RDC_ALGO_AUTO);
-    // allreduce of explicit chunk byte ranges of buf (chunk c = [off[c], off[c]+len[c]),
-    // folded in chunk c's ring order): one piece of a larger buffer (host path pipeline)
+    // allreduce of explicit byte ranges of buf, range c = [off[c], off[c]+len[c])
+    // owned by rank c and folded in the ring order of Split chunk fold[c]
+    // (fold null: c): one piece of a larger buffer (host path pipeline).  A
+    // fold other than the identity needs an owner-computes schedule (mesh,
+    // pull mesh, one-shot): a ring pick becomes the mesh.
     void AllreduceRanges(void* buf, const uint64_t* off, const uint64_t* len, int dtype, int op,
-                         hipStream_t stream);
+                         hipStream_t stream, const int8_t* fold = nullptr);
     void Broadcast(void* buf, size_t bytes, int root, hipStream_t stream);
     // bufs[c] (device) holds sizes[c] bytes; bufs[rank] is this rank's data
     void Allgather(void* const* bufs, const uint64_t* sizes, hipStream_t stream);
@@ -261,7 +264,8 @@ private:
     int PickAlgo(int algo, uint64_t bytes) const;
     // units != null: coalesced mesh over a device PackUnit table (off/len = packed chunk ranges)
     void LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* off, const uint64_t* len, uint64_t total,
-                      size_t esz, int algo, hipStream_t stream, const PackUnit* units = nullptr, int nunits = 0);
+                      size_t esz, int algo, hipStream_t stream, const PackUnit* units = nullptr, int nunits = 0,
+                      const int8_t* fold = nullptr);
     struct PackEntry {
         PackUnit* dtable = nullptr;  // device unit table (user addresses)
         int nunits = 0;

@@ -86,6 +86,9 @@ struct CollArgs {
     uint64_t off[RDC_MAX_RANKS];         // byte offset of chunk c's piece in `user`
     uint64_t len[RDC_MAX_RANKS];         // byte length of chunk c's piece
     uint32_t mis[RDC_MAX_RANKS];         // off[c] % 16: scratch image alignment (rank-independent)
+    int8_t fold[RDC_MAX_RANKS];          // range c is folded in the ring order of Split chunk fold[c]
+                                         //   (= c for a whole buffer; host pieces cut one chunk's range
+                                         //   into n ranges, one per owner, all folding in its order)
     uint64_t slot_bytes;                 // scratch slot stride
     uint32_t max_tiles;                  // flag array row stride
     char* rs[RDC_MAX_RANKS];             // rank p's reduce-scatter scratch region

@@ -340,15 +340,18 @@ void HostPath::AllreduceSmall(Communicator* c, char* h, size_t count, size_t S, 
 }
 
 namespace {
-// the intersection of piece [lo, hi) with every Split chunk, relative to lo
-void piece_ranges(uint64_t lo, uint64_t hi, int n, const int64_t* cb, const int64_t* ce, size_t esz, uint64_t* roff,
-                  uint64_t* rlen) {
-    for (int q = 0; q < n; ++q) {
-        const uint64_t a = std::max<uint64_t>(lo, (uint64_t)cb[q] * esz);
-        const uint64_t b = std::min<uint64_t>(hi, (uint64_t)ce[q] * esz);
-        roff[q] = b > a ? a - lo : 0;
-        rlen[q] = b > a ? b - a : 0;
-    }
+// RDC_HOST_BALANCE=1 / 0 forces balanced / chunk-owned piece ranges; by
+// default balanced with one rank per GPU (each rank's own links and HBM),
+// chunk-owned where ranks share a GPU (the one-GPU rehearsals measured that
+// layout, profiles/r03/host_contiguous_pieces/)
+bool balance_pieces(const Communicator* c) {
+    static const int env = env_int("RDC_HOST_BALANCE", -1);
+    return env >= 0 ? env != 0 : c->ranks_per_gpu() == 1;
+}
+
+void host_piece_ranges(const Communicator* c, uint64_t lo, uint64_t hi, const int64_t* cb, const int64_t* ce,
+                       size_t esz, uint64_t* roff, uint64_t* rlen, int8_t* fold) {
+    HostPieceRanges(lo, hi, c->size(), cb, ce, esz, balance_pieces(c), roff, rlen, fold);
 }
 }  // namespace
 
@@ -363,7 +366,6 @@ void piece_ranges(uint64_t lo, uint64_t hi, int n, const int64_t* cb, const int6
 void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int dtype, int op,
                                    hipStream_t comm_stream, const std::vector<uint64_t>& bounds, const int64_t* cb,
                                    const int64_t* ce) {
-    const int n = c->size();
     const size_t esz = rdc_dtype_size(dtype);
     const size_t S = count * esz;
     const int K = (int)bounds.size() - 1;
@@ -412,7 +414,8 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
         for (int k = 0; k < K; ++k) {
             const uint64_t lo = bounds[(size_t)k], hi = bounds[(size_t)k + 1];
             uint64_t roff[RDC_MAX_RANKS], rlen[RDC_MAX_RANKS];
-            piece_ranges(lo, hi, n, cb, ce, esz, roff, rlen);
+            int8_t fold[RDC_MAX_RANKS];
+            host_piece_ranges(c, lo, hi, cb, ce, esz, roff, rlen, fold);
             if (ahead > 0 && k >= ahead)
                 hip_check(hipStreamWaitEvent(h2d_, ar_done_[(size_t)(k - ahead)], 0), "wait");
             mark(k, 0, h2d_);
@@ -421,7 +424,7 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
             mark(k, 1, h2d_);
             hip_check(hipStreamWaitEvent(comm_stream, h2d_done_[(size_t)k], 0), "wait");
             mark(k, 2, comm_stream);
-            c->AllreduceRanges(dev_ + lo, roff, rlen, dtype, op, comm_stream);
+            c->AllreduceRanges(dev_ + lo, roff, rlen, dtype, op, comm_stream, fold);
             hip_check(hipEventRecord(ar_done_[(size_t)k], comm_stream), "record");
             mark(k, 3, comm_stream);
             hip_check(hipStreamWaitEvent(d2h_, ar_done_[(size_t)k], 0), "wait");
@@ -551,7 +554,8 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
             d.off[0] = lo;
             d.len[0] = bytes;
             uint64_t roff[RDC_MAX_RANKS], rlen[RDC_MAX_RANKS];
-            piece_ranges(lo, hi, n, cb, ce, esz, roff, rlen);
+            int8_t fold[RDC_MAX_RANKS];
+            host_piece_ranges(c, lo, hi, cb, ce, esz, roff, rlen, fold);
             // the slot's previous H2D has been consumed before we overwrite it
             const double t0 = tracing() ? trace_now() : 0;
             if (k >= kSlots) hip_check(hipEventSynchronize(in_done_[slot]), "wait H2D slot");
@@ -563,7 +567,7 @@ void HostPath::Allreduce(Communicator* c, void* host, size_t count, int dtype, i
             hip_check(hipMemcpyAsync(dev_ + lo, pin_in_[slot], bytes, hipMemcpyHostToDevice, h2d_), "H2D");
             hip_check(hipEventRecord(in_done_[slot], h2d_), "record");
             hip_check(hipStreamWaitEvent(comm_stream, in_done_[slot], 0), "wait");
-            c->AllreduceRanges(dev_ + lo, roff, rlen, dtype, op, comm_stream);
+            c->AllreduceRanges(dev_ + lo, roff, rlen, dtype, op, comm_stream, fold);
             hip_check(hipEventRecord(d.ready, comm_stream), "record");
             {
                 std::lock_guard<std::mutex> lk(dmu_);

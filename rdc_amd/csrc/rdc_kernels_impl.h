@@ -134,11 +134,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce_unaligned(char* dst, const ch
 template <int OP, typename T>
 __device__ __forceinline__ void mesh_fold_elem(const CollArgs& a, char* own, const char* slot0, uint64_t soff,
                                                uint64_t e) {
-    const int n = a.n, r = a.rank;
-    int q = (r - 1 + n) % n;
+    const int n = a.n, r = a.rank, f = a.fold[r];  // the ring order of chunk f
+    int q = (f - 1 + n) % n;
     T acc = *reinterpret_cast<const T*>((q == r ? (const char*)own : slot0 + q * a.slot_bytes) + e);
     for (int k = 2; k <= n; ++k) {
-        q = (r - k + n) % n;
+        q = (f - k + n) % n;
         const T v = *reinterpret_cast<const T*>((q == r ? (const char*)own : slot0 + q * a.slot_bytes) + e);
         acc = OpF<OP>::apply(v, acc);
     }
@@ -152,7 +152,7 @@ __device__ __forceinline__ void mesh_fold_elem(const CollArgs& a, char* own, con
 // goes to every peer's allgather region at byte offset soff.
 template <int OP, typename T, int NMAX>
 __device__ void mesh_reduce_range(const CollArgs& a, char* own, const char* slot0, uint64_t soff, uint64_t tlen) {
-    const int n = a.n, r = a.rank;
+    const int n = a.n, r = a.rank, f = a.fold[r];
     const unsigned tid = threadIdx.x;
     if ((((uintptr_t)own ^ (uintptr_t)slot0) & 15) != 0) {
         // this rank's buffer is not 16-B aligned: exact, element by element
@@ -190,7 +190,7 @@ __device__ void mesh_reduce_range(const CollArgs& a, char* own, const char* slot
 #pragma unroll
         for (int k = 1; k <= NMAX; ++k) {
             if (k <= n) {  // (a `break` here stops full unrolling: v would live in scratch)
-                const int q = (r - k + n) % n;  // k-th value in ring order: x[r-1], x[r-2], ..., x[r]
+                const int q = (f - k + n) % n;  // k-th value in ring order: x[f-1], x[f-2], ..., x[f]
                 const char* src = (q == r ? (const char*)own : slot0 + q * a.slot_bytes) + head;
 #pragma unroll
                 for (int u = 0; u < U; ++u)
@@ -380,14 +380,14 @@ __device__ void mesh_body(const CollArgs& a, uint64_t seq) {
 // launch's tile t, which needs every peer's next-launch stage.
 template <int OP, typename T, int NMAX>
 __device__ void pull_fold_range(const CollArgs& a, char* own, const char* const* src, char* res, uint64_t tlen) {
-    const int n = a.n, r = a.rank;
+    const int n = a.n, r = a.rank, f = a.fold[r];  // the ring order of chunk f
     const unsigned tid = threadIdx.x;
     auto fold_elem = [&](uint64_t e) {
         auto val = [&](int q) -> T {
             return q == r ? *reinterpret_cast<const T*>(own + e) : ld_elem_sys<T>(src[q] + e);
         };
-        T acc = val((r - 1 + n) % n);
-        for (int k = 2; k <= n; ++k) acc = OpF<OP>::apply(val((r - k + n) % n), acc);
+        T acc = val((f - 1 + n) % n);
+        for (int k = 2; k <= n; ++k) acc = OpF<OP>::apply(val((f - k + n) % n), acc);
         *reinterpret_cast<T*>(own + e) = acc;
         st_elem_wt<T>(res + e, acc);
     };
@@ -417,7 +417,7 @@ __device__ void pull_fold_range(const CollArgs& a, char* own, const char* const*
 #pragma unroll
         for (int k = 1; k <= NMAX; ++k) {
             if (k <= n) {
-                const int q = (r - k + n) % n;  // x[r-1], x[r-2], ..., x[r]
+                const int q = (f - k + n) % n;  // x[f-1], x[f-2], ..., x[f]
                 if (q == r) {
 #pragma unroll
                     for (int u = 0; u < U; ++u)
@@ -859,7 +859,7 @@ __device__ void oneshot_body(const CollArgs& a, uint64_t seq) {
                 if (a.len[c] == 0) continue;
                 const uint64_t clo = a.off[c] > lo ? a.off[c] : lo;
                 const uint64_t chi = a.off[c] + a.len[c] < hi ? a.off[c] + a.len[c] : hi;
-                if (clo < chi) oneshot_fold_range<OP, T, NMAX>(fv, c, clo, chi);
+                if (clo < chi) oneshot_fold_range<OP, T, NMAX>(fv, a.fold[c], clo, chi);
             }
         }
         __syncthreads();

@@ -434,6 +434,73 @@ HbmBytes ModelHbmBytes(int n, uint64_t count, size_t esz, int algo) {
     return h;
 }
 
+// the intersection of piece [lo, hi) with every Split chunk, relative to lo:
+// range q = the piece's bytes of chunk q, owned by rank q (its ring order)
+static void piece_ranges(uint64_t lo, uint64_t hi, int n, const int64_t* cb, const int64_t* ce, size_t esz, uint64_t* roff,
+                  uint64_t* rlen, int8_t* fold) {
+    for (int q = 0; q < n; ++q) {
+        const uint64_t a = std::max<uint64_t>(lo, (uint64_t)cb[q] * esz);
+        const uint64_t b = std::min<uint64_t>(hi, (uint64_t)ce[q] * esz);
+        roff[q] = b > a ? a - lo : 0;
+        rlen[q] = b > a ? b - a : 0;
+        fold[q] = (int8_t)q;
+    }
+}
+
+// The same piece as n BALANCED ranges.  A contiguous piece lies in one or two
+// Split chunks, so with piece_ranges one owner folds (nearly) all of it and
+// every other rank only copies — on one GPU per rank that puts the piece's
+// whole exchange on the owner's links.  Here the bytes of each chunk the
+// piece meets are cut into parts over the ranks (in proportion to their
+// length, at least one rank per chunk); every part is folded by its rank in
+// the ring order of the chunk it belongs to (fold), so every element keeps
+// its reference bits.  false (use piece_ranges) when the piece meets more
+// chunks than there are ranks.
+static bool balanced_ranges(uint64_t lo, uint64_t hi, int n, const int64_t* cb, const int64_t* ce, size_t esz,
+                     uint64_t* roff, uint64_t* rlen, int8_t* fold) {
+    int segc[RDC_MAX_RANKS], m = 0;
+    uint64_t sega[RDC_MAX_RANKS], segb[RDC_MAX_RANKS];
+    for (int q = 0; q < n; ++q) {
+        const uint64_t a = std::max<uint64_t>(lo, (uint64_t)cb[q] * esz);
+        const uint64_t b = std::min<uint64_t>(hi, (uint64_t)ce[q] * esz);
+        if (b > a) {
+            segc[m] = q;
+            sega[m] = a;
+            segb[m] = b;
+            ++m;
+        }
+    }
+    if (m == 0 || m > n) return false;
+    int k[RDC_MAX_RANKS];
+    for (int s = 0; s < m; ++s) k[s] = 1;
+    for (int extra = n - m; extra > 0; --extra) {  // the next rank to the segment with the most bytes per rank
+        int best = 0;
+        for (int s = 1; s < m; ++s)
+            if ((segb[s] - sega[s]) * (uint64_t)k[best] > (segb[best] - sega[best]) * (uint64_t)k[s]) best = s;
+        ++k[best];
+    }
+    int i = 0;
+    for (int s = 0; s < m; ++s) {
+        const uint64_t E = (segb[s] - sega[s]) / esz, base = E / (uint64_t)k[s], rem = E % (uint64_t)k[s];
+        uint64_t at = sega[s];
+        for (int j = 0; j < k[s]; ++j, ++i) {
+            const uint64_t cnt = base + ((uint64_t)j < rem ? 1 : 0);
+            roff[i] = at - lo;
+            rlen[i] = cnt * esz;
+            fold[i] = (int8_t)segc[s];
+            at += cnt * esz;
+        }
+    }
+    return true;
+}
+
+
+void HostPieceRanges(uint64_t lo, uint64_t hi, int n, const int64_t* cb, const int64_t* ce, size_t esz, bool balanced,
+                     uint64_t* roff, uint64_t* rlen, int8_t* fold) {
+    if (!balanced || !balanced_ranges(lo, hi, n, cb, ce, esz, roff, rlen, fold))
+        piece_ranges(lo, hi, n, cb, ce, esz, roff, rlen, fold);
+}
+
 std::vector<int> GroupCoalesced(const uint64_t* counts, int nbuf, size_t esz, uint64_t fuse_bytes) {
     std::vector<int> bounds;
     bounds.push_back(0);

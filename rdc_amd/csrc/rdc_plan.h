@@ -150,6 +150,14 @@ CoalescedPlan PlanCoalesced(int n, const uint64_t* counts, int nbuf, size_t esz,
 // Returns group boundaries: group g = buffers [bounds[g], bounds[g+1]).
 std::vector<int> GroupCoalesced(const uint64_t* counts, int nbuf, size_t esz, uint64_t fuse_bytes);
 
+// One host-path piece [lo, hi) (rdc_host.cpp) as the n ranges of its
+// allreduce: range q = [lo + roff[q], + rlen[q]) owned by rank q, folded in
+// the ring order of Split chunk fold[q].  Chunk-owned (the piece's bytes of
+// chunk q to rank q) or, `balanced`, each chunk's bytes cut over the ranks.
+// (cb, ce: the Split element ranges; esz: element bytes.)
+void HostPieceRanges(uint64_t lo, uint64_t hi, int n, const int64_t* cb, const int64_t* ce, size_t esz, bool balanced,
+                     uint64_t* roff, uint64_t* rlen, int8_t* fold);
+
 // HBM byte model of one allreduce (rdc_plan.cpp ModelHbmBytes): bytes the
 // kernels load / store, per rank (max over ranks) and summed over ranks,
 // plus the most remote-store (link egress) bytes of any rank

@@ -607,21 +607,23 @@ HOST_SWEEP_BYTES = [
 ]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_mp_host_size_sweep(world):
+@pytest.mark.parametrize("world,balance", [(2, "0"), (3, "0"), (3, "1"), (5, "1")])
+def test_mp_host_size_sweep(world, balance):
     """Host buffers at every boundary of the host path (rdc_host.cpp: service,
     copy-pool parts, zero-copy / staged small path, inline piece, pipeline
     with and without the ramp) +-1 element, 1-byte and 4-byte elements, every
     byte of every rank's result against the oracle.  A copy cut whose parts
     did not cover the buffer (bytes % parts left over) once dropped the last
-    bytes of a piece: only sizes like these see it."""
+    bytes of a piece: only sizes like these see it.  RDC_HOST_BALANCE=1: the
+    pieces' balanced ranges (every rank folds a part of each piece in its
+    chunk's ring order; the default with one rank per GPU)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cases = []
     for k, nb in enumerate(HOST_SWEEP_BYTES):
         cases.append({"count": nb, "dtype": 1, "op": (0, 2)[k % 2], "kind": "host_allreduce", "seed": 0x5EEDA000 + k})
         cases.append({"count": nb // 4 + 1, "dtype": 6, "op": 2, "kind": "host_allreduce", "seed": 0x5EEDB000 + k})
-    tmp = run_mp(world, cases, timeout=400)
+    tmp = run_mp(world, cases, timeout=400, env_extra={"RDC_HOST_BALANCE": balance})
     for i, c in enumerate(cases):
         want = expected_for(c, world)
         for r in range(world):
@@ -635,8 +637,8 @@ def test_mp_host_size_sweep(world):
 REGISTERED_BYTES = [(1 << 20) + 4, (3 << 20) + 7, 16777217, (33 << 20) + 4097, (64 << 20) + 4095]
 
 
-@pytest.mark.parametrize("world,pinned", [(2, True), (3, True), (3, "even")])
-def test_mp_host_registered(world, pinned):
+@pytest.mark.parametrize("world,pinned,balance", [(2, True, "0"), (3, True, "0"), (3, "even", "0"), (4, True, "1")])
+def test_mp_host_registered(world, pinned, balance):
     """Host buffers inside a registered RdcNewBuffer(pinned=1) range
     (rdc/buffer.py:34-38) DMA in place (HostPath::AllreduceRegistered): the
     inline piece, the pipeline with and without the ramp, ragged last pieces,
@@ -651,7 +653,7 @@ def test_mp_host_registered(world, pinned):
                       "seed": 0x5EEDC000 + k})
         cases.append({"count": nb // 4 + 1, "dtype": 6, "op": 2, "kind": "host_allreduce", "pinned": pinned,
                       "host_offset": 4 * (k % 2), "seed": 0x5EEDD000 + k})
-    tmp = run_mp(world, cases, timeout=400)
+    tmp = run_mp(world, cases, timeout=400, env_extra={"RDC_HOST_BALANCE": balance})
     for i, c in enumerate(cases):
         want = expected_for(c, world)
         for r in range(world):
@@ -712,7 +714,7 @@ def fuzz_cases(seed, world, n=40):
     (2, 21, {}),
     (3, 22, {"RDC_SCRATCH_BYTES": "8M", "RDC_TILE_BYTES": "16K"}),   # many pieces and tiles per call
     (2, 23, {"RDC_SCRATCH_BYTES": "4M", "RDC_NBLOCKS": "7"}),        # odd grid, tiny scratch
-    (4, 24, {}),
+    (4, 24, {"RDC_HOST_BALANCE": "1"}),     # host pieces as balanced ranges (one-rank-per-GPU default)
     (3, 25, {"RDC_ALGO": "ring"}),          # host pipeline pieces and auto calls on the ring
     (5, 26, {"RDC_SCRATCH_BYTES": "16M"}),
 ])

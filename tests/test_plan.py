@@ -355,3 +355,52 @@ def test_hbm_byte_model_closed_forms(n):
     assert hbm(8, 1 << 28, 6, 2)["read"] * 8 == 22 * (1 << 30)   # mesh 5.5 S per rank at n = 8, both ways
     from rdc_amd._lib import _LIB
     assert _LIB.RdcPlanHbmBytes(2, 10, 6, 0, (ctypes.c_uint64 * 5)()) != 0   # auto is not a schedule
+
+
+def piece_ranges(n, count, dtype, lo, hi, balanced):
+    from rdc_amd._lib import _LIB
+    off, ln, fold = (ctypes.c_uint64 * 16)(), (ctypes.c_uint64 * 16)(), (ctypes.c_int * 16)()
+    assert _LIB.RdcPlanHostPieceRanges(n, count, dtype, lo, hi, balanced, off, ln, fold) == 0
+    return [(off[q], ln[q], fold[q]) for q in range(n)]
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8, 16])
+def test_host_piece_ranges_keep_every_element_in_its_chunk_order(n):
+    """A host-path piece's ranges (rdc_plan.cpp HostPieceRanges): every byte of
+    the piece lies in exactly one range, and that range folds in the ring
+    order of the element's own Split chunk — chunk-owned (range q = the
+    piece's bytes of chunk q) or balanced (each chunk's bytes cut over the
+    ranks, at least one rank per chunk, parts within a chunk differing by at
+    most one element), which is what keeps the balanced layout bit-exact."""
+    rng = np.random.default_rng(n)
+    for _ in range(60):
+        esz = int(rng.choice([1, 4, 8]))
+        dtype = {1: 1, 4: 6, 8: 7}[esz]
+        count = int(rng.integers(n, 1 << 22))
+        a, b = sorted(int(x) for x in rng.integers(0, count + 1, 2))
+        lo, hi = a * esz, b * esz
+        split = O.split(count, n)
+        for balanced in (0, 1):
+            rs = piece_ranges(n, count, dtype, lo, hi, balanced)
+            covered = sorted((o, l, f) for o, l, f in rs if l)
+            at = 0
+            for o, l, f in covered:
+                assert o == at, (n, count, lo, hi, balanced, rs)
+                e0, e1 = (lo + o) // esz, (lo + o + l) // esz  # global elements of this range
+                cb, ce = split[f]
+                assert cb <= e0 and e1 <= ce, (n, count, lo, hi, balanced, rs)
+                at += l
+            assert at == hi - lo
+            if not balanced:
+                assert [f for _, _, f in rs] == list(range(n))
+            else:
+                chunks = [q for q in range(n) if max(lo, split[q][0] * esz) < min(hi, split[q][1] * esz)]
+                if chunks:
+                    assert {f for _, l, f in rs if l} == set(chunks)
+                    for q in chunks:
+                        parts = [l // esz for _, l, f in rs if f == q]
+                        assert len(parts) >= 1 and max(parts) - min(parts) <= 1, (q, parts)
+                    assert len([1 for _, l, _ in rs if l]) == min(n, (hi - lo) // esz) or len(chunks) > 1
+    # chunk 3 of an 8-rank buffer of 8 Mi fp32 (4 MiB) as one piece: 8 equal parts in its order
+    rs = piece_ranges(8, 8 << 20, 6, 4 * (3 << 20), 4 * (4 << 20), 1)
+    assert [l for _, l, _ in rs] == [512 << 10] * 8 and {f for _, _, f in rs} == {3}
