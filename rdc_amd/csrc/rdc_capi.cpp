@@ -361,6 +361,7 @@ void allreduce_sync(Manager& m, Communicator* c, void* sendrecv, size_t count, i
     // host-resident buffer: pieces of every chunk through pinned slots, H2D /
     // allreduce / D2H overlapped on three streams
     if (!m.host) m.host.reset(new HostPath(c->device(), m.host_zc_bytes));
+    m.host->Warm(s);
     m.host->Allreduce(c, sendrecv, count, dtype, op, s);
 }
 
@@ -869,7 +870,19 @@ int RdcNewBuffer(void** out, void* addr, size_t size, int pinned) {
             (void)hipGetLastError();
             // host allreduces inside the range DMA straight from / into it
             // (HostPath::AllreduceRegistered)
-            if (b->registered) HostRegistryAdd(addr, size);
+            if (b->registered) {
+                HostRegistryAdd(addr, size);
+                // the copy path that will DMA this range comes up now, not
+                // inside the first allreduce of it (HostPath::Warm)
+                Manager& m = M();
+                std::lock_guard<std::recursive_mutex> lk(m.mu);
+                auto it = m.comms.find("main");
+                if (m.inited && it != m.comms.end() && it->second->size() > 1) {
+                    Communicator* c = it->second.get();
+                    if (!m.host) m.host.reset(new HostPath(c->device(), m.host_zc_bytes));
+                    m.host->Warm(manager_stream(m, c->device()));
+                }
+            }
         }
         *out = b.release();
     });

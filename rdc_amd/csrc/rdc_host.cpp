@@ -207,6 +207,28 @@ HostPath::~HostPath() {
     if (d2h_) (void)hipStreamDestroy(d2h_);
 }
 
+void HostPath::Warm(hipStream_t comm_stream) {
+    if (warm_ || env_int("RDC_HOST_WARM", 1) == 0) return;
+    warm_ = true;
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    constexpr size_t kMax = (size_t)16 << 20;
+    Reserve(0, kMax, 0, comm_stream);
+    char* pin = nullptr;
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin), kMax, hipHostMallocDefault), "hipHostMalloc");
+    try {
+        for (hipStream_t s : {h2d_, d2h_, comm_stream})
+            for (size_t b : {(size_t)64 << 10, (size_t)1 << 20, kMax}) {
+                hip_check(hipMemcpyAsync(dev_, pin, b, hipMemcpyHostToDevice, s), "warm H2D");
+                hip_check(hipMemcpyAsync(pin, dev_, b, hipMemcpyDeviceToHost, s), "warm D2H");
+                hip_check(hipStreamSynchronize(s), "warm sync");
+            }
+    } catch (...) {
+        (void)hipHostFree(pin);
+        throw;
+    }
+    hip_check(hipHostFree(pin), "hipHostFree");
+}
+
 // Growing waits only for this path's own streams and the communicator's
 // stream (the previous call's copies and launches that may still use the old
 // buffers), never for the whole device: in a single-process group the other

@@ -61,6 +61,15 @@ public:
     ~HostPath();
     // in place; synchronous (returns after the result is back in `host`)
     void Allreduce(Communicator* c, void* host, size_t count, int dtype, int op, hipStream_t comm_stream);
+    // Bring up the copy path before the first timed call: H2D and D2H copies
+    // of 64 KiB / 1 MiB / 16 MiB on every stream the host path copies on.
+    // The first copies a process makes through the DMA engines stall ~7 ms
+    // each while the runtime brings its SDMA queues up (measured: the first
+    // two 64 MiB registered calls at n = 2 took 17 and 6.2 ms, every later
+    // one ~4.3 ms; with HSA_ENABLE_SDMA=0 no call stalls;
+    // profiles/r04/host_registered_events/).  Idempotent; RDC_HOST_WARM=0
+    // skips it.
+    void Warm(hipStream_t comm_stream);
 
 private:
     static constexpr int kSlots = 3;
@@ -91,6 +100,7 @@ private:
     void TraceRegistered(int K, const std::vector<uint64_t>& bounds, double host_ms);
 
     int device_;
+    bool warm_ = false;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
     char* pin_small_ = nullptr;      // kSmall bytes + the error word
     hipEvent_t small_done_ = nullptr;  // the staged small path's D2H

@@ -6,6 +6,7 @@ allreduce, D2H copy, synchronise (RdcAllreduce on a numpy buffer).
     python tools/host_path.py [bytes] [iters]          # N = 1: H2D + reduce + D2H
     RDC_BENCH_PINNED=1 ...: the buffer is a registered RdcNewBuffer(pinned=1)
     range (page-aligned mmap), so the library DMAs it in place
+    (RDC_BENCH_THP=1: madvise(MADV_HUGEPAGE) on that mmap first)
 
 Prints one JSON line (rank 0) with GB/s = S / t per call (max over ranks).
 """
@@ -36,7 +37,10 @@ def main():
     if pinned:
         import mmap
         span = (S + mmap.PAGESIZE - 1) // mmap.PAGESIZE * mmap.PAGESIZE
-        backing = np.frombuffer(mmap.mmap(-1, span), dtype=np.uint8)
+        mm = mmap.mmap(-1, span)
+        if os.environ.get("RDC_BENCH_THP") == "1":  # transparent huge pages behind the registered range
+            mm.madvise(mmap.MADV_HUGEPAGE)
+        backing = np.frombuffer(mm, dtype=np.uint8)
         backing[:S].view(np.float32)[:] = host
         host = backing[:S].view(np.float32)
     p = host.ctypes.data_as(ctypes.c_void_p)
