@@ -67,7 +67,7 @@ void dbg(const char* fmt, int rank, const char* what) {
     }
 }
 
-constexpr int kPlanKeys = 17;  // PlanKey below; sizes PeerInfo::plan
+constexpr int kPlanKeys = 18;  // PlanKey below; sizes PeerInfo::plan
 
 struct PeerInfo {
     uint64_t channel;   // id of the live channel this rank would share (0 = none)
@@ -107,7 +107,7 @@ void PlanKey(const CommConfig& c, uint64_t tune_hash, uint64_t (&k)[kPlanKeys]) 
                                    (uint64_t)c.scratch_bytes, (uint64_t)SmallService::Enabled(),
                                    (uint64_t)SmallService::ShareMax(),
                                    (uint64_t)HostPieceBytes() | ((uint64_t)HostPieceRamp() << 63), tune_hash,
-                                   (uint64_t)HostInlineBytes()};
+                                   (uint64_t)HostInlineBytes(), (uint64_t)(HostBalanceSetting() + 1)};
     memcpy(k, v, sizeof(v));
 }
 const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_ONESHOT_BYTES",
@@ -115,7 +115,7 @@ const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYT
                                         "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "RDC_MESH_SPLIT",
                                         "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES", "RDC_HOST_SERVICE",
                                         "RDC_HOST_SERVICE_SHARE_MAX", "RDC_HOST_PIECE_BYTES / RDC_HOST_PIECE_RAMP",
-                                        "RDC_TUNE_FILE (set or not)", "RDC_HOST_INLINE_BYTES"};
+                                        "RDC_TUNE_FILE (set or not)", "RDC_HOST_INLINE_BYTES", "RDC_HOST_BALANCE"};
 
 // Autotune results kept across runs (RDC_TUNE_FILE): one line per winner,
 // "rdc-tune 2 <ranks> <cus> <ranks per gpu> <size class> <algo> <s16> <r16>

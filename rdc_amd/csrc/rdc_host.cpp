@@ -68,6 +68,11 @@ static size_t env_bytes(const char* name) {
     return env_bytes_parse(name, &v) ? v : 0;
 }
 
+int HostBalanceSetting() {
+    static const int v = env_int("RDC_HOST_BALANCE", -1);
+    return v < 0 ? -1 : (v != 0 ? 1 : 0);
+}
+
 size_t HostPieceBytes() {
     static const size_t v = [] {
         const size_t x = env_bytes("RDC_HOST_PIECE_BYTES");
@@ -152,13 +157,15 @@ void HostRegistryRemove(const void* p) {
     g_reg.erase((uintptr_t)p);
 }
 
-bool HostRegistryCovers(const void* p, size_t bytes) {
+bool HostRegistryCovers(const void* p, size_t bytes, const void** base) {
     const uintptr_t a = (uintptr_t)p;
     std::lock_guard<std::mutex> lk(g_reg_mu);
     auto it = g_reg.upper_bound(a);  // the first range starting after a
     if (it == g_reg.begin()) return false;
     --it;
-    return a - it->first <= it->second && bytes <= it->second - (a - it->first);
+    const bool in = a - it->first <= it->second && bytes <= it->second - (a - it->first);
+    if (in && base) *base = reinterpret_cast<const void*>(it->first);
+    return in;
 }
 
 uint64_t HostRegisteredCalls() { return g_reg_calls.load(std::memory_order_relaxed); }
@@ -367,7 +374,7 @@ namespace {
 // chunk-owned where ranks share a GPU (the one-GPU rehearsals measured that
 // layout, profiles/r03/host_contiguous_pieces/)
 bool balance_pieces(const Communicator* c) {
-    static const int env = env_int("RDC_HOST_BALANCE", -1);
+    const int env = HostBalanceSetting();
     return env >= 0 ? env != 0 : c->ranks_per_gpu() == 1;
 }
 
@@ -398,6 +405,10 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
         h2d_done_.push_back(e);
     }
     g_reg_calls.fetch_add(1, std::memory_order_relaxed);
+    if (RegisteredZeroCopy()) {
+        AllreduceRegisteredZeroCopy(c, h, count, dtype, op, comm_stream, bounds, cb, ce);
+        return;
+    }
     if (K == 1) {  // the inline piece's collective: the whole buffer
         hip_check(hipMemcpyAsync(dev_, h, S, hipMemcpyHostToDevice, comm_stream), "H2D");
         hip_check(hipEventRecord(h2d_done_[0], comm_stream), "record");
@@ -466,6 +477,50 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
         TraceRegistered(K, bounds, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0)
                                        .count());
     c->Check(comm_stream);  // a device-side failure surfaces here
+}
+
+// RDC_HOST_REG_ZC=1: the registered path runs every piece's collective on
+// the caller's pages themselves (the kernels load their inputs from and store
+// their results to host memory over PCIe): no device image, no H2D / D2H
+// DMA.  The pieces and their collectives are the staged path's (the same
+// AllreduceRanges calls), so zero-copy, registered-DMA and staged ranks still
+// meet in one call.  A plan key (rdc_comm.cpp kPlanKeys), agreed at creation.
+bool RegisteredZeroCopy() {
+    static const bool on = env_int("RDC_HOST_REG_ZC", 0) != 0;
+    return on;
+}
+
+void HostPath::AllreduceRegisteredZeroCopy(Communicator* c, char* h, size_t count, int dtype, int op,
+                                           hipStream_t comm_stream, const std::vector<uint64_t>& bounds,
+                                           const int64_t* cb, const int64_t* ce) {
+    const size_t esz = rdc_dtype_size(dtype);
+    const int K = (int)bounds.size() - 1;
+    // the device address of the caller's pages: the registration's, plus the offset
+    const void* base = nullptr;
+    if (!HostRegistryCovers(h, count * esz, &base)) throw std::logic_error("rdc: zero-copy of an unregistered range");
+    void* dbase = nullptr;
+    hip_check(hipHostGetDevicePointer(&dbase, const_cast<void*>(base), 0), "hipHostGetDevicePointer");
+    char* hd = static_cast<char*>(dbase) + (h - static_cast<const char*>(base));
+    uint32_t token = 0;
+    try {
+        for (int k = 0; k < K; ++k) {
+            const uint64_t lo = bounds[(size_t)k], hi = bounds[(size_t)k + 1];
+            if (k == K - 1) token = c->ArmNotify();  // the call's last launch signals the host
+            if (K == 1) {
+                c->Allreduce(hd, count, dtype, op, comm_stream);
+            } else {
+                uint64_t roff[RDC_MAX_RANKS], rlen[RDC_MAX_RANKS];
+                int8_t fold[RDC_MAX_RANKS];
+                host_piece_ranges(c, lo, hi, cb, ce, esz, roff, rlen, fold);
+                c->AllreduceRanges(hd + lo, roff, rlen, dtype, op, comm_stream, fold);
+            }
+        }
+    } catch (...) {
+        if (token) c->WaitNotify(token, comm_stream);  // disarms
+        (void)hipStreamSynchronize(comm_stream);      // no kernel still touches the caller's pages
+        throw;
+    }
+    c->WaitNotify(token, comm_stream);
 }
 
 // One line per call: the span from the first H2D's start to the last D2H's

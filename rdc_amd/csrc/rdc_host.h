@@ -50,7 +50,12 @@ std::vector<uint64_t> HostPieceBounds(uint64_t S);
 // until RdcDelBuffer, as with any registration.
 void HostRegistryAdd(const void* p, size_t bytes);
 void HostRegistryRemove(const void* p);
-bool HostRegistryCovers(const void* p, size_t bytes);
+// RDC_HOST_BALANCE: -1 unset (balanced host pieces with one rank per GPU), 0 off, 1 on
+int HostBalanceSetting();
+// *base (may be null) = the registered range's start
+bool HostRegistryCovers(const void* p, size_t bytes, const void** base = nullptr);
+// RDC_HOST_REG_ZC=1: registered host buffers are reduced in place over PCIe (no DMA)
+bool RegisteredZeroCopy();
 // host allreduces of this process that took the registered path
 uint64_t HostRegisteredCalls();
 
@@ -92,6 +97,10 @@ private:
     // straight from / into a registered user buffer, all stream-ordered
     void AllreduceRegistered(Communicator* c, char* host, size_t count, int dtype, int op, hipStream_t comm_stream,
                              const std::vector<uint64_t>& bounds, const int64_t* cb, const int64_t* ce);
+    // RDC_HOST_REG_ZC: every piece's collective on the caller's registered pages
+    void AllreduceRegisteredZeroCopy(Communicator* c, char* host, size_t count, int dtype, int op,
+                                     hipStream_t comm_stream, const std::vector<uint64_t>& bounds,
+                                     const int64_t* cb, const int64_t* ce);
     std::vector<hipEvent_t> h2d_done_;  // registered path: one per piece
     // RDC_HOST_EVENT_TRACE=1 (diagnostics): timing events around every
     // piece's H2D, allreduce and D2H of the registered path, summarised per

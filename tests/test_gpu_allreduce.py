@@ -637,8 +637,9 @@ def test_mp_host_size_sweep(world, balance):
 REGISTERED_BYTES = [(1 << 20) + 4, (3 << 20) + 7, 16777217, (33 << 20) + 4097, (64 << 20) + 4095]
 
 
-@pytest.mark.parametrize("world,pinned,balance", [(2, True, "0"), (3, True, "0"), (3, "even", "0"), (4, True, "1")])
-def test_mp_host_registered(world, pinned, balance):
+@pytest.mark.parametrize("world,pinned,balance,zc", [(2, True, "0", "0"), (3, True, "0", "0"), (3, "even", "0", "0"),
+                                                     (4, True, "1", "0"), (2, True, "0", "1"), (3, "even", "1", "1")])
+def test_mp_host_registered(world, pinned, balance, zc):
     """Host buffers inside a registered RdcNewBuffer(pinned=1) range
     (rdc/buffer.py:34-38) DMA in place (HostPath::AllreduceRegistered): the
     inline piece, the pipeline with and without the ramp, ragged last pieces,
@@ -653,7 +654,9 @@ def test_mp_host_registered(world, pinned, balance):
                       "seed": 0x5EEDC000 + k})
         cases.append({"count": nb // 4 + 1, "dtype": 6, "op": 2, "kind": "host_allreduce", "pinned": pinned,
                       "host_offset": 4 * (k % 2), "seed": 0x5EEDD000 + k})
-    tmp = run_mp(world, cases, timeout=400, env_extra={"RDC_HOST_BALANCE": balance})
+    # zc: RDC_HOST_REG_ZC=1, the registered ranks' pieces reduced in place over PCIe ("even": beside
+    # staged ranks in one call, pieces and collectives identical)
+    tmp = run_mp(world, cases, timeout=400, env_extra={"RDC_HOST_BALANCE": balance, "RDC_HOST_REG_ZC": zc})
     for i, c in enumerate(cases):
         want = expected_for(c, world)
         for r in range(world):
@@ -1245,7 +1248,8 @@ except Exception as e:  # the expected path
 
 
 @pytest.mark.parametrize("key,value", [("RDC_TILE_BYTES", "1M"), ("RDC_HOST_SERVICE", "0"),
-                                       ("RDC_HOST_SERVICE_SHARE_MAX", "2"), ("RDC_HOST_PIECE_BYTES", "4194304")])
+                                       ("RDC_HOST_SERVICE_SHARE_MAX", "2"), ("RDC_HOST_PIECE_BYTES", "4194304"),
+                                       ("RDC_HOST_BALANCE", "1")])
 def test_mp_plan_disagreement_is_refused(key, value):
     """Ranks whose launch-plan parameters differ (one rank's env) are refused
     at communicator creation with the parameter named, on every rank: a
