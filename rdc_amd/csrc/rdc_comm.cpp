@@ -67,7 +67,7 @@ void dbg(const char* fmt, int rank, const char* what) {
     }
 }
 
-constexpr int kPlanKeys = 18;  // PlanKey below; sizes PeerInfo::plan
+constexpr int kPlanKeys = 19;  // PlanKey below; sizes PeerInfo::plan
 
 struct PeerInfo {
     uint64_t channel;   // id of the live channel this rank would share (0 = none)
@@ -107,7 +107,8 @@ void PlanKey(const CommConfig& c, uint64_t tune_hash, uint64_t (&k)[kPlanKeys]) 
                                    (uint64_t)c.scratch_bytes, (uint64_t)SmallService::Enabled(),
                                    (uint64_t)SmallService::ShareMax(),
                                    (uint64_t)HostPieceBytes() | ((uint64_t)HostPieceRamp() << 63), tune_hash,
-                                   (uint64_t)HostInlineBytes(), (uint64_t)(HostBalanceSetting() + 1)};
+                                   (uint64_t)HostInlineBytes(), (uint64_t)(HostBalanceSetting() + 1),
+                                   SmallService::HxBytes()};
     memcpy(k, v, sizeof(v));
 }
 const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_ONESHOT_BYTES",
@@ -115,7 +116,8 @@ const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYT
                                         "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "RDC_MESH_SPLIT",
                                         "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES", "RDC_HOST_SERVICE",
                                         "RDC_HOST_SERVICE_SHARE_MAX", "RDC_HOST_PIECE_BYTES / RDC_HOST_PIECE_RAMP",
-                                        "RDC_TUNE_FILE (set or not)", "RDC_HOST_INLINE_BYTES", "RDC_HOST_BALANCE"};
+                                        "RDC_TUNE_FILE (set or not)", "RDC_HOST_INLINE_BYTES", "RDC_HOST_BALANCE",
+                                        "RDC_HOST_SERVICE_HX_BYTES"};
 
 // Autotune results kept across runs (RDC_TUNE_FILE): one line per winner,
 // "rdc-tune 2 <ranks> <cus> <ranks per gpu> <size class> <algo> <s16> <r16>
@@ -171,18 +173,20 @@ std::vector<TuneEntry> shared_tune_table(Bootstrap* bs) {
     return std::vector<TuneEntry>(msg.e, msg.e + std::max(0, std::min(msg.count, kTuneEntriesMax)));
 }
 
-// The point-to-point control block (rdc_p2p.h) in POSIX shared memory: rank 0
-// creates it, every rank maps it, rank 0 unlinks the name once all mapped.
-std::shared_ptr<P2PCtl> map_p2p_ctl(Bootstrap* bs) {
+// `bytes` of POSIX shared memory every rank of bs maps and registers for its
+// device (hipHostRegister `flags`): rank 0 creates it, every rank maps it,
+// rank 0 unlinks the name once all mapped (nothing is left in /dev/shm).
+// Collective over bs.  Zero-filled.
+std::shared_ptr<char> map_shared_host(Bootstrap* bs, size_t bytes, const char* what, unsigned flags) {
     char name[64];
     memset(name, 0, sizeof(name));
     int fd = -1;
     std::string err;
     if (bs->rank() == 0) {
         static std::atomic<int> counter{0};
-        snprintf(name, sizeof(name), "/rdc_p2p_%d_%d", (int)getpid(), counter++);
+        snprintf(name, sizeof(name), "/rdc_%s_%d_%d", what, (int)getpid(), counter++);
         fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
-        if (fd < 0 || ftruncate(fd, sizeof(P2PCtl)) != 0) {
+        if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) {
             err = std::string("rdc: cannot create shared memory ") + name + ": " + strerror(errno);
             if (fd >= 0) {
                 close(fd);
@@ -193,29 +197,41 @@ std::shared_ptr<P2PCtl> map_p2p_ctl(Bootstrap* bs) {
         }
     }
     bs->broadcast(name, sizeof(name), 0);
-    if (!name[0]) throw std::runtime_error(err.empty() ? "rdc: rank 0 could not create the p2p control block" : err);
+    if (!name[0])
+        throw std::runtime_error(err.empty() ? std::string("rdc: rank 0 could not create shared memory for ") + what
+                                             : err);
     if (bs->rank() != 0) {
         fd = shm_open(name, O_RDWR, 0600);
         if (fd < 0) throw std::runtime_error(std::string("rdc: cannot open shared memory ") + name + ": " + strerror(errno));
     }
-    void* p = mmap(nullptr, sizeof(P2PCtl), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);
     if (p == MAP_FAILED) throw std::runtime_error(std::string("rdc: cannot map shared memory: ") + strerror(errno));
-    // registered for device access: the p2p copy kernels publish posted /
-    // consumed themselves (rdc_p2p.h)
-    if (hipHostRegister(p, sizeof(P2PCtl), hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+    if (hipHostRegister(p, bytes, flags) != hipSuccess) {
         (void)hipGetLastError();
-        munmap(p, sizeof(P2PCtl));
-        throw std::runtime_error("rdc: cannot register the p2p control block for device access");
+        munmap(p, bytes);
+        throw std::runtime_error(std::string("rdc: cannot register shared memory for ") + what + " for device access");
     }
-    std::shared_ptr<P2PCtl> ctl(static_cast<P2PCtl*>(p), [](P2PCtl* q) {
+    std::shared_ptr<char> mem(static_cast<char*>(p), [bytes](char* q) {
         (void)hipHostUnregister(q);
-        munmap(q, sizeof(P2PCtl));
+        munmap(q, bytes);
     });
     bs->barrier();
     if (bs->rank() == 0) shm_unlink(name);
-    return ctl;
+    return mem;
 }
+
+// The point-to-point control block (rdc_p2p.h), registered for device access:
+// the p2p copy kernels publish posted / consumed themselves
+std::shared_ptr<P2PCtl> map_p2p_ctl(Bootstrap* bs) {
+    std::shared_ptr<char> mem =
+        map_shared_host(bs, sizeof(P2PCtl), "p2p", hipHostRegisterMapped | hipHostRegisterPortable);
+    return std::shared_ptr<P2PCtl>(mem, reinterpret_cast<P2PCtl*>(mem.get()));
+}
+
+// the small-allreduce service's host exchange region (rdc_service.h); MTYPE
+// UC on the GPU side like the mailbox, so the block's loads see the hosts' stores
+size_t svc_hx_bytes(int n) { return (size_t)2 * (size_t)n * RDC_SVC_HX_RANK_BYTES; }
 
 }  // namespace
 
@@ -636,6 +652,9 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     }
     if (!share) c->Alias();  // the aliases now include the peers' mappings
     c->p2p_ctl_ = map_p2p_ctl(bs);
+    if (!share && svc_all && SmallService::HxBytes() > 0)  // the same branch on every rank (agreed above)
+        ch->svc_hx = map_shared_host(bs, svc_hx_bytes(c->n_), "svc",
+                                     hipHostRegisterMapped | hipHostRegisterPortable | hipExtHostRegisterUncached);
     dbg("[rdc %d] %s\n", c->rank_, "peers mapped");
     c->owns_peers_ipc_ = true;
     bs->barrier();
@@ -678,6 +697,17 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
     for (auto& c : cs) {
         c->share_max_ = share;
         c->cus_min_ = cus;
+    }
+    if (SmallService::Enabled() && SmallService::HxBytes() > 0) {  // one exchange region every rank uses
+        void* hx = nullptr;
+        if (hipHostMalloc(&hx, svc_hx_bytes(n), hipHostMallocUncached | hipHostMallocMapped | hipHostMallocPortable) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            throw std::runtime_error("rdc: cannot allocate the service's host exchange region");
+        }
+        memset(hx, 0, svc_hx_bytes(n));
+        std::shared_ptr<char> mem(static_cast<char*>(hx), [](char* q) { (void)hipHostFree(q); });
+        for (auto& c : cs) c->ch_->svc_hx = mem;
     }
     // Pinned coherent pages of its own, not a registered heap object: a
     // registration covers whole pages, and a heap object shares its first and
@@ -1580,7 +1610,8 @@ bool Communicator::SmallHostAllreduce(void* host, size_t count, int dtype, int o
         std::lock_guard<std::mutex> lk(ch_->mu);
         if (!ch_->svc)
             ch_->svc.reset(new SmallService(rank_, n_, device_, ch_->peer_svc_region, err_ + 56,
-                                            tree_len_, tree_dst_, tree_src_, cfg_.timeout_s, wall_khz_));
+                                            tree_len_, tree_dst_, tree_src_, cfg_.timeout_s, wall_khz_,
+                                            ch_->svc_hx.get()));
         svc = ch_->svc.get();
     }
     // every rank allocates the same way on one machine image; a rank without

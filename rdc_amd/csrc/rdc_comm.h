@@ -84,11 +84,13 @@ struct Channel {
     char* peer_scratch[RDC_MAX_RANKS] = {};
     char* peer_ag[RDC_MAX_RANKS] = {};
     uint64_t* peer_flags[RDC_MAX_RANKS] = {};
-    // small-allreduce service (rdc_service.h): its own uncached slots
     // small-allreduce service slots (rdc_service.h): [2 halves][n] x
     // RDC_SVC_SLOT_BYTES of LL words per rank, IPC-mapped
     char* svc_region = nullptr;
     char* peer_svc_region[RDC_MAX_RANKS] = {};
+    // the service's host exchange: [2 halves][n] x RDC_SVC_HX_RANK_BYTES of
+    // shared host memory every rank maps (null: RDC_HOST_SERVICE_HX_BYTES=0)
+    std::shared_ptr<char> svc_hx;
     std::unique_ptr<SmallService> svc;  // started on first use
     bool svc_enabled = false;          // agreed at creation: the service may run on this channel
     bool svc_counted = false;          // counted in the process's per-device service registry

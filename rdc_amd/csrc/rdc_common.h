@@ -127,10 +127,15 @@ struct CollArgs {
 #define RDC_SVC_MAX_BYTES (64u << 10)  // largest buffer it serves
 #define RDC_SVC_SLOT_BYTES (2u * RDC_SVC_MAX_BYTES)  // one rank's LL words: two planes of RDC_SVC_MAX_BYTES
 #define RDC_SVC_LL_MAX (16u << 10)  // largest input sent over PCIe as LL words
+// host exchange (rdc_service.h): every rank's LL input in one POSIX shared
+// host region, [2 halves][n ranks][RDC_SVC_HX_RANK_BYTES], read by every
+// rank's service block over PCIe (no xGMI hand-off)
+#define RDC_SVC_HX_RANK_BYTES (2u * RDC_SVC_LL_MAX)
 enum { RDC_SVC_NEVER = 0, RDC_SVC_RUNNING = 1, RDC_SVC_EXITING = 2, RDC_SVC_EXITED = 3 };
 
 struct SvcBox {  // pinned host memory, hipHostMallocUncached; one per rank
-    // request header, itself an LL word: (seq << 32) | tree << 31 | LL input << 30 | LL result << 29 | bytes
+    // request header, itself an LL word:
+    //   (seq << 32) | tree << 31 | LL input << 30 | LL result << 29 | host exchange << 28 | bytes
     alignas(64) uint64_t hdr;
     alignas(64) uint32_t done;    // device: last completed request
     alignas(64) uint32_t state;   // device: RDC_SVC_*
@@ -151,6 +156,9 @@ struct SvcArgs {
     int strict;                     // RDC_STRICT_FENCES: system fence before `done`
     int trace;                      // RDC_SVC_TRACE: stamp SvcBox::trace per request
     int eager;                      // threads that read their LL input vector while polling the header
+    char* hx;                       // device address of the host exchange region, or null
+    int hx_eager;                   // threads that poll every rank's exchange words of their vector
+                                    //   while polling the header
     uint64_t idle_ticks;            // wall_clock64 ticks without a request before exiting
     uint64_t timeout_ticks;         // waiting for a peer's contribution
     int tree_len;

@@ -1079,13 +1079,20 @@ __device__ __forceinline__ bool ll_match(const v4u& lo, const v4u& hi, uint32_t 
     return lo.y == seq && lo.w == seq && hi.y == seq && hi.w == seq;
 }
 
-// Header bits: 31 tree order, 30 LL input, 29 LL result, 0-28 bytes.
+// Header bits: 31 tree order, 30 LL input, 29 LL result, 28 host exchange,
+// 0-27 bytes.
 //   LL input (<= RDC_HOST_SERVICE_LL_BYTES): the host writes its input as LL
 //     words, so the poll that finds the header can already hold the data (the
 //     first `eager` threads read their vector every round): one PCIe round
 //     trip fewer; otherwise the input as is, read after the header is seen.
 //   LL result: the result as LL words the host polls (no drain, no `done`
 //     wait on the host); otherwise as is, drained, then `done`.
+//   Host exchange (a.hx, small n * bytes): every rank's host writes its LL
+//     input into its slot of ONE shared host region, and every rank's block
+//     reads all n inputs from there over PCIe — no send to the peers' slots,
+//     no xGMI hand-off; the first `hx_eager` threads poll every rank's words
+//     of their vector with the header.  The halves alternate with seq like the
+//     slots (a rank is at most one request ahead of any peer's reads).
 // LL words are PLANAR: vector i's {w0, seq, w1, seq} at plane 0 + 16 i and
 // {w2, seq, w3, seq} at plane 1 + 16 i, so the 64 lanes of one instruction
 // touch 1 KiB of contiguous memory (an interleaved 32-byte pair per lane made
@@ -1100,6 +1107,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
     const int n = a.n, r = a.rank;
     const unsigned tid = threadIdx.x;
     SvcBox* box = a.box;
+    const bool hxm = a.hx != nullptr;
+    const uint32_t all = (n >= 32 ? ~0u : (1u << n) - 1u);
     __shared__ v4u s_in[RDC_SVC_MAX_BYTES / 16];  // this rank's input, read once over PCIe
     __shared__ v4u s_pv[NMAX * BS];               // [q][thread]: rank q's vector being folded
     __shared__ uint32_t s_next;
@@ -1115,13 +1124,32 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
         // ---- wait for a request (rounds: every thread's loads, one barrier)
         const uint32_t seq = s_next;
         const uint64_t t0 = wall_clock64();
-        const bool eager = tid < (unsigned)a.eager;
+        const bool eager = !hxm && tid < (unsigned)a.eager;
+        const bool heager = hxm && tid < (unsigned)a.hx_eager;
+        const char* hxh = hxm ? a.hx + (uint64_t)(seq & 1u) * (uint64_t)n * RDC_SVC_HX_RANK_BYTES : nullptr;
+        uint32_t hpend = all;  // heager: ranks whose words of vector tid are not in s_pv yet
         v4u elo = {0, 0, 0, 0}, ehi = {0, 0, 0, 0};
         int go;
         for (;;) {
             if (eager) {
                 elo = ld16_nt(box->data + 16 * tid);
                 ehi = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * tid);
+            }
+            if (heager && hpend) {  // all pending ranks' loads in flight, then the matches
+                v4u hl[NMAX], hh[NMAX];
+#pragma unroll
+                for (int q = 0; q < NMAX; ++q)
+                    if ((hpend >> q) & 1u) {
+                        const char* p = hxh + (uint64_t)q * RDC_SVC_HX_RANK_BYTES + 16 * tid;
+                        hl[q] = ld16_nt(p);
+                        hh[q] = ld16_nt(p + RDC_SVC_LL_MAX);
+                    }
+#pragma unroll
+                for (int q = 0; q < NMAX; ++q)
+                    if (((hpend >> q) & 1u) && ll_match(hl[q], hh[q], seq)) {
+                        s_pv[q * BS + tid] = v4u{hl[q].x, hl[q].z, hh[q].x, hh[q].z};
+                        hpend &= ~(1u << q);
+                    }
             }
             if (tid == 0) {
                 uint64_t q = box_load64(&box->hdr);
@@ -1156,8 +1184,9 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
         uint64_t ts[4];
         if (a.trace) ts[0] = wall_clock64();
         const uint64_t req = s_req;
-        const uint64_t bytes = req & 0x1fffffffu;
+        const uint64_t bytes = req & 0x0fffffffu;
         const bool tree = (req >> 31) & 1u, ll = (req >> 30) & 1u, ll_out = (req >> 29) & 1u;
+        const bool hx = hxm && ((req >> 28) & 1u);
         const uint64_t nvec = (bytes + 15) >> 4;  // rounded up: the mailbox and slots have room
         const uint64_t half = (uint64_t)(seq & 1u) * (uint64_t)n * RDC_SVC_SLOT_BYTES;
         const uint64_t deadline = wall_clock64() + a.timeout_ticks;
@@ -1173,7 +1202,9 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                 st16_wt(rs, (uint32_t)(16 * i + RDC_SVC_MAX_BYTES), v4u{x.z, seq, x.w, seq});
             }
         };
-        if (ll) {
+        if (hx) {
+            // nothing to send: the peers read this rank's input where its host wrote it
+        } else if (ll) {
             const bool have0 = eager && ll_match(elo, ehi, seq);
             for (uint64_t i0 = tid; i0 < nvec && ok; i0 += (uint64_t)U * BS) {
                 v4u lo[U], hi[U];
@@ -1219,21 +1250,25 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
         if (a.trace) ts[1] = wall_clock64();
         // 2) per vector: every peer's words (polled together), folded in the
         //    reference's order in registers, written straight to the mailbox
-        const char* mine = a.region[r] + half;
+        //    (host exchange: every rank's words, this rank's included, from
+        //    the shared host region)
+        const char* src = hx ? hxh : a.region[r] + half;
+        const uint64_t stride = hx ? RDC_SVC_HX_RANK_BYTES : RDC_SVC_SLOT_BYTES;
+        const uint64_t plane = hx ? RDC_SVC_LL_MAX : RDC_SVC_MAX_BYTES;
+        const uint32_t pending0 = hx ? all : all & ~(1u << r);
         const uint64_t count = bytes / sizeof(T), ck = count / (uint64_t)n, cm = count % (uint64_t)n;
 #pragma unroll 1
         for (uint64_t i = tid; i < nvec && ok; i += BS) {
             v4u* pv = s_pv + tid;  // pv[q * BS]
-            const v4u own = s_in[i];
-            uint32_t pending = ((1u << n) - 1u) & ~(1u << r);
+            uint32_t pending = (hx && heager && i == tid) ? hpend : pending0;
             uint32_t spins = 0;
             while (pending) {
                 asm volatile("" ::: "memory");  // a fresh load of every pending word per pass
 #pragma unroll
                 for (int q = 0; q < NMAX; ++q)
                     if ((pending >> q) & 1u) {
-                        const char* p = mine + (uint64_t)q * RDC_SVC_SLOT_BYTES + 16 * i;
-                        const v4u lo = ld16_nt(p), hi = ld16_nt(p + RDC_SVC_MAX_BYTES);
+                        const char* p = src + (uint64_t)q * stride + 16 * i;
+                        const v4u lo = ld16_nt(p), hi = ld16_nt(p + plane);
                         if (ll_match(lo, hi, seq)) {
                             pv[q * BS] = v4u{lo.x, lo.z, hi.x, hi.z};
                             pending &= ~(1u << q);
@@ -1246,7 +1281,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
             }
             if (!ok) break;
             if (a.trace && i == tid) ts[2] = wall_clock64();
-            pv[r * BS] = own;
+            const v4u own = hx ? pv[r * BS] : s_in[i];
+            if (!hx) pv[r * BS] = own;
             v4u res;
             if (tree) {  // acc[d] = OP(acc[d], acc[s]) over the host-planned program; result acc[0]
                 for (int j = 0; j < a.tree_len; ++j) {

@@ -32,9 +32,15 @@ bool SmallService::Enabled() {
     return on;
 }
 
+uint64_t SmallService::HxBytes() {
+    static const uint64_t v = (uint64_t)std::max(0.0, env_double("RDC_HOST_SERVICE_HX_BYTES", 32768));
+    return v;
+}
+
 SmallService::SmallService(int rank, int n, int device, char* const* region, uint32_t* derr,
-                           int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz)
-    : rank_(rank), device_(device), timeout_s_(timeout_s) {
+                           int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz,
+                           char* hx)
+    : rank_(rank), device_(device), timeout_s_(timeout_s), n_(n) {
     memset(&args_, 0, sizeof(args_));
     for (int p = 0; p < n; ++p) args_.region[p] = region[p];
     args_.derr = derr;
@@ -50,6 +56,8 @@ SmallService::SmallService(int rank, int n, int device, char* const* region, uin
     ll_out_bytes_ = (uint64_t)std::min(env_double("RDC_HOST_SERVICE_LL_OUT_BYTES", 256), (double)RDC_SVC_LL_MAX);
     const int block = n <= 8 ? 512 : 256;  // Kernels::svc's block size
     args_.eager = std::max(0, std::min(block, (int)(env_double("RDC_HOST_SERVICE_EAGER_BYTES", 4096) / 16)));
+    args_.hx_eager =
+        std::max(0, std::min(block, (int)(env_double("RDC_HOST_SERVICE_HX_EAGER_BYTES", 8192) / (16.0 * n))));
     wall_khz_ = wall_khz;
     args_.idle_ticks = (uint64_t)(env_double("RDC_HOST_SERVICE_IDLE_US", 1000.0) * (double)wall_khz / 1000.0);
     args_.timeout_ticks = (uint64_t)(timeout_s * (double)wall_khz * 1000.0);
@@ -71,6 +79,12 @@ SmallService::SmallService(int rank, int n, int device, char* const* region, uin
     void* d = nullptr;
     hip_check(hipHostGetDevicePointer(&d, box_, 0), "mailbox device address");
     args_.box = static_cast<SvcBox*>(d);
+    if (hx && HxBytes() > 0) {
+        void* hd = nullptr;
+        hip_check(hipHostGetDevicePointer(&hd, hx, 0), "host exchange device address");
+        hx_ = hx;
+        args_.hx = static_cast<char*>(hd);
+    }
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "service stream");
 }
 
@@ -139,6 +153,8 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
     if (launched_ && kind != kind_) Stop();  // another (dtype, op) needs another kernel
     const uint32_t r = ++req_;
     const bool ll = bytes <= ll_bytes_;
+    // host exchange: the same choice on every rank (n, bytes and the budget agree)
+    const bool hx = hx_ != nullptr && ll && bytes * (uint64_t)n_ <= HxBytes();
     const uint64_t nwords = ((bytes + 15) / 16) * 4;  // whole 16-byte vectors of 4-byte LL payloads
     const auto t0 = std::chrono::steady_clock::now();
     if (ll) {
@@ -163,8 +179,10 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
         // whose r landed before its payload would be taken with stale data.
         // memcpy gives no such guarantee (rep movsb, overlapping vector
         // stores); aligned 8-byte atomic stores do.
-        uint64_t* p0 = reinterpret_cast<uint64_t*>(box_->data);
-        uint64_t* p1 = reinterpret_cast<uint64_t*>(box_->data + RDC_SVC_LL_MAX);
+        char* dst = hx ? hx_ + ((uint64_t)(r & 1u) * (uint64_t)n_ + (uint64_t)rank_) * RDC_SVC_HX_RANK_BYTES
+                       : box_->data;
+        uint64_t* p0 = reinterpret_cast<uint64_t*>(dst);
+        uint64_t* p1 = reinterpret_cast<uint64_t*>(dst + RDC_SVC_LL_MAX);
         const uint64_t* s0 = stage_.data();
         const uint64_t* s1 = stage_.data() + RDC_SVC_LL_MAX / 8;
         for (uint64_t j = 0; j < plane_words; ++j) {
@@ -179,7 +197,7 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
     const bool ll_out = bytes <= ll_out_bytes_;
     __atomic_store_n(&box_->hdr,
                      ((uint64_t)r << 32) | (tree ? 1ull << 31 : 0ull) | (ll ? 1ull << 30 : 0ull) |
-                         (ll_out ? 1ull << 29 : 0ull) | bytes,
+                         (ll_out ? 1ull << 29 : 0ull) | (hx ? 1ull << 28 : 0ull) | bytes,
                      __ATOMIC_SEQ_CST);
     EnsureRunning(ks, kind);
     const double limit = timeout_s_ * 2 + 10;

@@ -26,6 +26,17 @@
 // leaves: host store header / load state, device store state / fence / load
 // header).  Its slots are its own, not the channel's scratch, so it never
 // races the channel's stream-ordered launches.
+//
+// Host exchange (round 4): when n * bytes <= RDC_HOST_SERVICE_HX_BYTES
+// (default 32 KiB) and the input goes as LL words, every rank's host writes
+// them into its slot of ONE region of POSIX shared host memory that every
+// rank maps and registers (uncached on the GPU side), and every rank's block
+// reads all n inputs from it — the xGMI send and the peers' polls leave the
+// critical path (request seen -> input sent -> peers in was 1.9-2.3 us of a
+// 7.9 us call, profiles/r04/host_registered_events/svc4k_trace.txt).  Each GPU
+// then reads n * bytes of LL words over its own PCIe link, so it is for small
+// n * bytes only.  The first RDC_HOST_SERVICE_HX_EAGER_BYTES of the ranks'
+// inputs together (default 8 KiB) are polled with the header.
 // RDC_HOST_SERVICE=0 disables it; with more than RDC_HOST_SERVICE_SHARE_MAX
 // (default 4) ranks on one GPU it is not used (their persistent blocks'
 // queues get time-sliced by the hardware scheduler).
@@ -44,8 +55,14 @@ class SmallService {
 public:
     // region: every rank's service slots (peers' IPC-mapped or direct); derr:
     // a device word for the kernel's errors
+    // hx: this process's mapping of the channel's host exchange region
+    // ([2][n] x RDC_SVC_HX_RANK_BYTES, registered for the device), or null
     SmallService(int rank, int n, int device, char* const* region, uint32_t* derr,
-                 int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz);
+                 int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz,
+                 char* hx = nullptr);
+    // n * bytes budget of the host exchange (RDC_HOST_SERVICE_HX_BYTES, default
+    // 32 KiB; 0 = off): a plan key, every rank must agree
+    static uint64_t HxBytes();
     ~SmallService();
     static bool Enabled();
     // most ranks per GPU it runs with (RDC_HOST_SERVICE_SHARE_MAX, default 4)
@@ -70,6 +87,8 @@ private:
     bool launched_ = false;
     bool broken_ = false;
     uint32_t req_ = 0;
+    int n_ = 1;
+    char* hx_ = nullptr;  // host address of the exchange region, or null
     int wall_khz_ = 100000;
     uint64_t ll_bytes_ = RDC_SVC_LL_MAX;  // LL input up to this many bytes
     uint64_t ll_out_bytes_ = 0;           // LL result up to this many bytes (set from the env in the ctor)

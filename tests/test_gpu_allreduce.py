@@ -503,7 +503,12 @@ def expected_host_mix(world, mincount=1):
                                        (8, {"RDC_HOST_SERVICE_SHARE_MAX": "8"}),
                                        (5, {"RDC_HOST_SERVICE_SHARE_MAX": "8"}),
                                        (7, {"RDC_HOST_SERVICE_SHARE_MAX": "8",
-                                            "rdc_reduce_ring_mincount": "2K"})])
+                                            "rdc_reduce_ring_mincount": "2K"}),
+                                       (2, {"RDC_HOST_SERVICE_HX_BYTES": "0"}),
+                                       (3, {"RDC_HOST_SERVICE_HX_BYTES": "1048576", "RDC_HOST_SERVICE_HX_EAGER_BYTES": "0",
+                                            "rdc_reduce_ring_mincount": "8K"}),
+                                       (4, {"RDC_HOST_SERVICE_HX_BYTES": "1048576",
+                                            "RDC_HOST_SERVICE_HX_EAGER_BYTES": "65536"})])
 def test_mp_host_small_service(world, env):
     """Small synchronous HOST allreduces (cfg1's path) through the resident
     service block (rdc_service.h): 12 calls of 1 B - 64 KiB over 8 (dtype, op)
@@ -511,9 +516,11 @@ def test_mp_host_small_service(world, env):
     idle time (it exits and is relaunched), device collectives in between,
     the tree order below rdc_reduce_ring_mincount; LL and plain input modes
     (RDC_HOST_SERVICE_LL_BYTES=0), no eager polling, 8 ranks (the 8-wide
-    kernel; RDC_HOST_SERVICE_SHARE_MAX lifts the one-GPU cap); and the
-    launch path with RDC_HOST_SERVICE=0.  Every result bit-exact against the
-    oracle."""
+    kernel; RDC_HOST_SERVICE_SHARE_MAX lifts the one-GPU cap); the host
+    exchange (every rank's input from one shared host region) at its default
+    budget, up to the 16 KiB LL limit, with no and with whole-block eager
+    polling, and switched off; and the launch path with RDC_HOST_SERVICE=0.
+    Every result bit-exact against the oracle."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cases = [{"count": 0, "dtype": 6, "op": 2, "kind": "host_mix", "ops": HOST_MIX}]
@@ -1249,7 +1256,7 @@ except Exception as e:  # the expected path
 
 @pytest.mark.parametrize("key,value", [("RDC_TILE_BYTES", "1M"), ("RDC_HOST_SERVICE", "0"),
                                        ("RDC_HOST_SERVICE_SHARE_MAX", "2"), ("RDC_HOST_PIECE_BYTES", "4194304"),
-                                       ("RDC_HOST_BALANCE", "1")])
+                                       ("RDC_HOST_BALANCE", "1"), ("RDC_HOST_SERVICE_HX_BYTES", "0")])
 def test_mp_plan_disagreement_is_refused(key, value):
     """Ranks whose launch-plan parameters differ (one rank's env) are refused
     at communicator creation with the parameter named, on every rank: a

@@ -18,6 +18,8 @@
 #                           VAR=value pairs; '-' = none), e.g. ab:tile:RDC_TILE_BYTES=256K:-
 #     hostab:<name>:<envA>:<envB>:<bytes>:<calls>
 #                           tools/host_path.py (host-buffer RdcAllreduce, n = 2) alternated A B A B
+#     py:<name>:<env>:<script>:<args>
+#                           one python process (a script that starts its own ranks), stdout to <name>.txt
 #     run:<name>:<env>:<n>:<script>:<args>
 #                           any script as n torch.distributed ranks with env (',' separates), stdout
 #                           to <name>.txt, stderr to <name>.err
@@ -103,6 +105,10 @@ for step in "$@"; do
                 > $OUT/hostab_${a1}_$v.$port.txt 2>&1 || { tail -20 $OUT/hostab_${a1}_$v.$port.txt; exit 1; }
             echo "$v $(grep -o '"ms_per_call": [0-9.]*' $OUT/hostab_${a1}_$v.$port.txt | head -1)"
         done ;;
+    py)
+        env $(envset "$a2") timeout -k 10 300 python3 $a3 $(echo "$a4" | tr ',' ' ') \
+            > $OUT/$a1.txt 2> $OUT/$a1.err || { tail -20 $OUT/$a1.err; exit 1; }
+        tail -c 600 $OUT/$a1.txt; echo ;;
     run)
         port=$((port + 11))
         env $(envset "$a2") timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $a3 \

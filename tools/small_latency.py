@@ -88,11 +88,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--iters", type=int, default=2000)
-    ap.add_argument("--bytes", default="4096,65536")
+    ap.add_argument("--bytes", nargs="+", default=["4096,65536"])
     ap.add_argument("--rank", type=int, default=-1)
     ap.add_argument("--port", type=int, default=0)
     a = ap.parse_args()
-    sizes = [int(x) for x in a.bytes.split(",")]
+    sizes = [int(x) for b in a.bytes for x in b.split(",")]
     if a.rank >= 0:
         worker(a.rank, a.world, a.port, a.iters, sizes)
         return
@@ -101,7 +101,7 @@ def main():
     port = s.getsockname()[1]
     s.close()
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--world", str(a.world), "--iters",
-                               str(a.iters), "--bytes", a.bytes, "--rank", str(r), "--port", str(port)])
+                               str(a.iters), "--bytes", ",".join(map(str, sizes)), "--rank", str(r), "--port", str(port)])
              for r in range(a.world)]
     rc = 0
     for p in procs:
