@@ -33,7 +33,9 @@ bool SmallService::Enabled() {
 }
 
 uint64_t SmallService::HxBytes() {
-    static const uint64_t v = (uint64_t)std::max(0.0, env_double("RDC_HOST_SERVICE_HX_BYTES", 32768));
+    // off by default: on one shared GPU it measured no faster at n = 2 and
+    // slower at n = 4; opt in per node
+    static const uint64_t v = (uint64_t)std::max(0.0, env_double("RDC_HOST_SERVICE_HX_BYTES", 0));
     return v;
 }
 

@@ -27,8 +27,8 @@
 // header).  Its slots are its own, not the channel's scratch, so it never
 // races the channel's stream-ordered launches.
 //
-// Host exchange (round 4): when n * bytes <= RDC_HOST_SERVICE_HX_BYTES
-// (default 32 KiB) and the input goes as LL words, every rank's host writes
+// Host exchange (round 4, opt-in): when n * bytes <= RDC_HOST_SERVICE_HX_BYTES
+// (default 0 = off; e.g. 32768) and the input goes as LL words, every rank's host writes
 // them into its slot of ONE region of POSIX shared host memory that every
 // rank maps and registers (uncached on the GPU side), and every rank's block
 // reads all n inputs from it — the xGMI send and the peers' polls leave the
@@ -61,7 +61,7 @@ public:
                  int tree_len, const int* tree_dst, const int* tree_src, double timeout_s, int wall_khz,
                  char* hx = nullptr);
     // n * bytes budget of the host exchange (RDC_HOST_SERVICE_HX_BYTES, default
-    // 32 KiB; 0 = off): a plan key, every rank must agree
+    // 0 = off): a plan key, every rank must agree
     static uint64_t HxBytes();
     ~SmallService();
     static bool Enabled();

@@ -504,7 +504,7 @@ def expected_host_mix(world, mincount=1):
                                        (5, {"RDC_HOST_SERVICE_SHARE_MAX": "8"}),
                                        (7, {"RDC_HOST_SERVICE_SHARE_MAX": "8",
                                             "rdc_reduce_ring_mincount": "2K"}),
-                                       (2, {"RDC_HOST_SERVICE_HX_BYTES": "0"}),
+                                       (2, {"RDC_HOST_SERVICE_HX_BYTES": "32768"}),
                                        (3, {"RDC_HOST_SERVICE_HX_BYTES": "1048576", "RDC_HOST_SERVICE_HX_EAGER_BYTES": "0",
                                             "rdc_reduce_ring_mincount": "8K"}),
                                        (4, {"RDC_HOST_SERVICE_HX_BYTES": "1048576",
@@ -517,9 +517,9 @@ def test_mp_host_small_service(world, env):
     the tree order below rdc_reduce_ring_mincount; LL and plain input modes
     (RDC_HOST_SERVICE_LL_BYTES=0), no eager polling, 8 ranks (the 8-wide
     kernel; RDC_HOST_SERVICE_SHARE_MAX lifts the one-GPU cap); the host
-    exchange (every rank's input from one shared host region) at its default
-    budget, up to the 16 KiB LL limit, with no and with whole-block eager
-    polling, and switched off; and the launch path with RDC_HOST_SERVICE=0.
+    exchange (RDC_HOST_SERVICE_HX_BYTES: every rank's input from one shared
+    host region) at a 32 KiB budget and up to the 16 KiB LL limit, with no and
+    with whole-block eager polling; and the launch path with RDC_HOST_SERVICE=0.
     Every result bit-exact against the oracle."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -1256,7 +1256,7 @@ except Exception as e:  # the expected path
 
 @pytest.mark.parametrize("key,value", [("RDC_TILE_BYTES", "1M"), ("RDC_HOST_SERVICE", "0"),
                                        ("RDC_HOST_SERVICE_SHARE_MAX", "2"), ("RDC_HOST_PIECE_BYTES", "4194304"),
-                                       ("RDC_HOST_BALANCE", "1"), ("RDC_HOST_SERVICE_HX_BYTES", "0")])
+                                       ("RDC_HOST_BALANCE", "1"), ("RDC_HOST_SERVICE_HX_BYTES", "32768")])
 def test_mp_plan_disagreement_is_refused(key, value):
     """Ranks whose launch-plan parameters differ (one rank's env) are refused
     at communicator creation with the parameter named, on every rank: a
