@@ -1,5 +1,6 @@
 // Pipelined host-resident allreduce (see rdc_host.h).
 #include "rdc_host.h"
+#include "rdc_kernels.h"
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -27,9 +28,11 @@ int env_int(const char* name, int dflt) {
 }
 // Buffers up to HostInlineBytes() go as ONE piece on the caller's thread;
 // larger ones through the pipeline in pieces of piece_target() bytes
-// (RDC_HOST_PIECE_BYTES, default 8 MiB: n = 2 on one GPU, 64 MiB 4.7-4.9 ms
-// vs 6.3-7.6 ms with 16 MiB pieces, 256 MiB 15-20 vs 19-23 ms;
-// profiles/r02/host_pieces/)
+// (RDC_HOST_PIECE_BYTES, default 16 MiB since round 4: with contiguous pieces
+// and the ramp, n = 2 on one GPU, staged 64 MiB 5.16-5.21 vs 5.64 ms with
+// 8 MiB pieces and 256 MiB 20.8-20.9 vs 21.6-21.7 ms, registered 13.4 vs
+// 15.9 ms; 32 MiB within noise of 16; profiles/r04/host_gap/.  Round 2's
+// pipeline, before contiguous pieces, measured 8 MiB faster.)
 size_t piece_target() { return HostPieceBytes(); }
 constexpr size_t kParallelMin = (size_t)512 << 10;  // below this a copy runs on the caller alone (waking the pool costs more)
 // RDC_HOST_TRACE=1: per-piece timeline on stderr (diagnostics)
@@ -76,7 +79,7 @@ int HostBalanceSetting() {
 size_t HostPieceBytes() {
     static const size_t v = [] {
         const size_t x = env_bytes("RDC_HOST_PIECE_BYTES");
-        return x >= ((size_t)1 << 20) ? x : (size_t)8 << 20;
+        return x >= ((size_t)1 << 20) ? x : (size_t)16 << 20;
     }();
     return v;
 }
@@ -384,6 +387,17 @@ void host_piece_ranges(const Communicator* c, uint64_t lo, uint64_t hi, const in
 }
 }  // namespace
 
+namespace {
+// the device address of registered host bytes [h, h + bytes)
+char* registered_device_address(char* h, uint64_t bytes) {
+    const void* base = nullptr;
+    if (!HostRegistryCovers(h, bytes, &base)) throw std::logic_error("rdc: device address of an unregistered range");
+    void* dbase = nullptr;
+    hip_check(hipHostGetDevicePointer(&dbase, const_cast<void*>(base), 0), "hipHostGetDevicePointer");
+    return static_cast<char*>(dbase) + (h - static_cast<const char*>(base));
+}
+}  // namespace
+
 // A registered buffer is DMA-able in place (57 GB/s either way on the box,
 // the rate of hipHostMalloc memory): no pinned slots, no copy pool, no drain
 // thread.  Every piece's H2D, allreduce and D2H is queued up front on the
@@ -409,8 +423,18 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
         AllreduceRegisteredZeroCopy(c, h, count, dtype, op, comm_stream, bounds, cb, ce);
         return;
     }
+    // the copies: DMA, or kernels on the caller's pages' device mapping
+    char* const hd = RegisteredKernelCopy() ? registered_device_address(h, S) : nullptr;
+    auto h2d = [&](uint64_t lo, uint64_t len, hipStream_t s) {
+        if (hd) hip_check(launch_copy(dev_ + lo, hd + lo, len, s), "H2D kernel");
+        else hip_check(hipMemcpyAsync(dev_ + lo, h + lo, len, hipMemcpyHostToDevice, s), "H2D");
+    };
+    auto d2h = [&](uint64_t lo, uint64_t len, hipStream_t s) {
+        if (hd) hip_check(launch_copy(hd + lo, dev_ + lo, len, s), "D2H kernel");
+        else hip_check(hipMemcpyAsync(h + lo, dev_ + lo, len, hipMemcpyDeviceToHost, s), "D2H");
+    };
     if (K == 1) {  // the inline piece's collective: the whole buffer
-        hip_check(hipMemcpyAsync(dev_, h, S, hipMemcpyHostToDevice, comm_stream), "H2D");
+        h2d(0, S, comm_stream);
         hip_check(hipEventRecord(h2d_done_[0], comm_stream), "record");
         try {
             c->Allreduce(dev_, count, dtype, op, comm_stream);
@@ -419,7 +443,7 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
             throw;
         }
         try {
-            hip_check(hipMemcpyAsync(h, dev_, S, hipMemcpyDeviceToHost, comm_stream), "D2H");
+            d2h(0, S, comm_stream);
             hip_check(hipEventRecord(in_done_[0], comm_stream), "record");
             SpinEvent(in_done_[0], "host allreduce");
         } catch (...) {
@@ -452,7 +476,7 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
             if (ahead > 0 && k >= ahead)
                 hip_check(hipStreamWaitEvent(h2d_, ar_done_[(size_t)(k - ahead)], 0), "wait");
             mark(k, 0, h2d_);
-            hip_check(hipMemcpyAsync(dev_ + lo, h + lo, hi - lo, hipMemcpyHostToDevice, h2d_), "H2D");
+            h2d(lo, hi - lo, h2d_);
             hip_check(hipEventRecord(h2d_done_[(size_t)k], h2d_), "record");
             mark(k, 1, h2d_);
             hip_check(hipStreamWaitEvent(comm_stream, h2d_done_[(size_t)k], 0), "wait");
@@ -462,7 +486,7 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
             mark(k, 3, comm_stream);
             hip_check(hipStreamWaitEvent(d2h_, ar_done_[(size_t)k], 0), "wait");
             mark(k, 4, d2h_);
-            hip_check(hipMemcpyAsync(h + lo, dev_ + lo, hi - lo, hipMemcpyDeviceToHost, d2h_), "D2H");
+            d2h(lo, hi - lo, d2h_);
             mark(k, 5, d2h_);
         }
         hip_check(hipEventRecord(in_done_[0], d2h_), "record");
@@ -484,11 +508,27 @@ void HostPath::AllreduceRegistered(Communicator* c, char* h, size_t count, int d
 // their results to host memory over PCIe): no device image, no H2D / D2H
 // DMA.  The pieces and their collectives are the staged path's (the same
 // AllreduceRanges calls), so zero-copy, registered-DMA and staged ranks still
-// meet in one call.  A plan key (rdc_comm.cpp kPlanKeys), agreed at creation.
+// meet in one call; each rank may choose for itself.
 bool RegisteredZeroCopy() {
     static const bool on = env_int("RDC_HOST_REG_ZC", 0) != 0;
     return on;
 }
+
+// RDC_HOST_REG_KCOPY (default 1): the registered path's H2D / D2H copies are
+// kernels (launch_copy: up to 128 blocks loading from / storing to the
+// caller's pages through their device mapping, 53-57 GB/s either way,
+// tools/zc_bw.hip) instead of the DMA engines.  DMA copies from and into
+// registered pages are faster back to back (64 MiB 3.8 vs 4.8 ms, n = 2 on one
+// GPU) but stall on the first calls (14-17 ms) and slow down whenever the
+// host idled before the call (20 ms idle: 5.0-7.1 ms per 64 MiB call, kernel
+// copies 4.6-5.2; profiles/r04/host_gap/) — as it does between the
+// allreduces of a training step.  The same pieces and collectives either
+// way; a rank's own choice (0 = DMA).
+bool RegisteredKernelCopy() {
+    static const bool on = env_int("RDC_HOST_REG_KCOPY", 1) != 0;
+    return on;
+}
+
 
 void HostPath::AllreduceRegisteredZeroCopy(Communicator* c, char* h, size_t count, int dtype, int op,
                                            hipStream_t comm_stream, const std::vector<uint64_t>& bounds,
@@ -496,11 +536,7 @@ void HostPath::AllreduceRegisteredZeroCopy(Communicator* c, char* h, size_t coun
     const size_t esz = rdc_dtype_size(dtype);
     const int K = (int)bounds.size() - 1;
     // the device address of the caller's pages: the registration's, plus the offset
-    const void* base = nullptr;
-    if (!HostRegistryCovers(h, count * esz, &base)) throw std::logic_error("rdc: zero-copy of an unregistered range");
-    void* dbase = nullptr;
-    hip_check(hipHostGetDevicePointer(&dbase, const_cast<void*>(base), 0), "hipHostGetDevicePointer");
-    char* hd = static_cast<char*>(dbase) + (h - static_cast<const char*>(base));
+    char* hd = registered_device_address(h, count * esz);
     uint32_t token = 0;
     try {
         for (int k = 0; k < K; ++k) {

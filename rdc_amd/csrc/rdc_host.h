@@ -30,7 +30,7 @@
 
 namespace rdc_amd {
 
-// RDC_HOST_PIECE_BYTES (default 8 MiB): every rank cuts a pipelined host
+// RDC_HOST_PIECE_BYTES (default 16 MiB): every rank cuts a pipelined host
 // buffer into the same pieces, so it is one of the plan keys agreed at
 // communicator creation (rdc_comm.cpp PlanKey)
 size_t HostPieceBytes();
@@ -56,6 +56,8 @@ int HostBalanceSetting();
 bool HostRegistryCovers(const void* p, size_t bytes, const void** base = nullptr);
 // RDC_HOST_REG_ZC=1: registered host buffers are reduced in place over PCIe (no DMA)
 bool RegisteredZeroCopy();
+// RDC_HOST_REG_KCOPY (default 1): the registered path copies with kernels, not DMA
+bool RegisteredKernelCopy();
 // host allreduces of this process that took the registered path
 uint64_t HostRegisteredCalls();
 

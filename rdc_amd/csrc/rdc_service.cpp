@@ -222,6 +222,16 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
     if (ll_out) {  // every result word as it lands, decoded in place
         const uint64_t* o = reinterpret_cast<const uint64_t*>(box_->out);
         const uint64_t used = (bytes + 3) / 4;
+        // the last word first: spinning on word 0 while the device's 16-byte
+        // stores land line by line pulls every line into this core's cache and
+        // loses it again to the next store into it (each re-read a memory
+        // round trip); once the last word is in, most lines are complete
+        if (used > 64) {
+            while ((uint32_t)(__atomic_load_n(o + ll_index(used - 1), __ATOMIC_ACQUIRE) >> 32) != r) {
+                __builtin_ia32_pause();
+                check(++spins);
+            }
+        }
         for (uint64_t j = 0; j < used; ++j) {
             uint64_t v;
             while ((uint32_t)((v = __atomic_load_n(o + ll_index(j), __ATOMIC_ACQUIRE)) >> 32) != r) {

@@ -609,8 +609,9 @@ HOST_SWEEP_BYTES = [
     524287, 524289, 786435,            # the copy pool's 512 KiB threshold, 2-3 parts with a remainder
     1048575, 1048577, 1048579,         # zero-copy / staged small path (1 MiB) vs one inline piece
     (3 << 20) + 7, 16777215, 16777217,  # one inline piece up to 16 MiB, the pipeline above
-    (33 << 20) + 4097,                 # pipeline without the ramp (< 8 pieces)
-    (64 << 20) + 4095,                 # pipeline with the ramp (>= 8 pieces), ragged last piece
+    (33 << 20) + 4097,                 # pipeline without the ramp (< 8 pieces of 16 MiB)
+    (64 << 20) + 4095,                 # 4 pieces, ragged last piece
+    (128 << 20) + 4095,                # pipeline with the ramp (>= 8 pieces), ragged last piece
 ]
 
 
@@ -641,12 +642,15 @@ def test_mp_host_size_sweep(world, balance):
             assert bad.size == 0, "%r rank %d: %d bytes differ, first at byte %d" % (c, r, bad.size, bad[0])
 
 
-REGISTERED_BYTES = [(1 << 20) + 4, (3 << 20) + 7, 16777217, (33 << 20) + 4097, (64 << 20) + 4095]
+REGISTERED_BYTES = [(1 << 20) + 4, (3 << 20) + 7, 16777217, (33 << 20) + 4097, (128 << 20) + 4095]
 
 
-@pytest.mark.parametrize("world,pinned,balance,zc", [(2, True, "0", "0"), (3, True, "0", "0"), (3, "even", "0", "0"),
-                                                     (4, True, "1", "0"), (2, True, "0", "1"), (3, "even", "1", "1")])
-def test_mp_host_registered(world, pinned, balance, zc):
+@pytest.mark.parametrize("world,pinned,balance,mode", [(2, True, "0", "dma"), (3, True, "0", "dma"),
+                                                       (3, "even", "0", "dma"), (4, True, "1", "dma"),
+                                                       (2, True, "0", "zc"), (3, "even", "1", "zc"),
+                                                       (2, True, "0", "kcopy"), (3, "even", "1", "kcopy")])
+# dma: RDC_HOST_REG_KCOPY=0 (the DMA engines); kcopy: the default kernel copies
+def test_mp_host_registered(world, pinned, balance, mode):
     """Host buffers inside a registered RdcNewBuffer(pinned=1) range
     (rdc/buffer.py:34-38) DMA in place (HostPath::AllreduceRegistered): the
     inline piece, the pipeline with and without the ramp, ragged last pieces,
@@ -661,9 +665,12 @@ def test_mp_host_registered(world, pinned, balance, zc):
                       "seed": 0x5EEDC000 + k})
         cases.append({"count": nb // 4 + 1, "dtype": 6, "op": 2, "kind": "host_allreduce", "pinned": pinned,
                       "host_offset": 4 * (k % 2), "seed": 0x5EEDD000 + k})
-    # zc: RDC_HOST_REG_ZC=1, the registered ranks' pieces reduced in place over PCIe ("even": beside
-    # staged ranks in one call, pieces and collectives identical)
-    tmp = run_mp(world, cases, timeout=400, env_extra={"RDC_HOST_BALANCE": balance, "RDC_HOST_REG_ZC": zc})
+    # zc: RDC_HOST_REG_ZC=1, the registered ranks' pieces reduced in place over PCIe; kcopy:
+    # RDC_HOST_REG_KCOPY=1, their H2D / D2H copies done by kernels ("even": beside staged ranks in one
+    # call, pieces and collectives identical)
+    tmp = run_mp(world, cases, timeout=400, env_extra={"RDC_HOST_BALANCE": balance,
+                                                       "RDC_HOST_REG_ZC": "1" if mode == "zc" else "0",
+                                                       "RDC_HOST_REG_KCOPY": "0" if mode == "dma" else "1"})
     for i, c in enumerate(cases):
         want = expected_for(c, world)
         for r in range(world):

@@ -264,14 +264,14 @@ def host_pieces(sizes, env):
     return {int(k): v for k, v in json.loads(p.stdout).items()}
 
 
-@pytest.mark.parametrize("piece,ramp", [("8M", "1"), ("8M", "0"), ("4M", "1"), ("1M", "1")])
+@pytest.mark.parametrize("piece,ramp", [("16M", "1"), ("8M", "1"), ("8M", "0"), ("4M", "1"), ("1M", "1")])
 def test_host_pipeline_pieces(piece, ramp):
     """The host pipeline's contiguous pieces (rdc_host.cpp HostPieceBounds):
     they tile [0, S) in order, interior bounds on 4 KiB (hence element)
     boundaries, one piece up to 16 MiB, pieces of about RDC_HOST_PIECE_BYTES
     P, and with the ramp the first and last three P/8, P/4, P/2 (mirrored)
     for buffers of at least 8 P."""
-    P = {"8M": 8 << 20, "4M": 4 << 20, "1M": 1 << 20}[piece]
+    P = {"16M": 16 << 20, "8M": 8 << 20, "4M": 4 << 20, "1M": 1 << 20}[piece]
     sizes = [16 << 20, (16 << 20) + 4, 64 << 20, (64 << 20) + 12, 100000012, 256 << 20, 3 * P + 4096 * 7 + 8]
     got = host_pieces(sizes, {"RDC_HOST_PIECE_BYTES": str(P), "RDC_HOST_PIECE_RAMP": ramp})
     for S in sizes:
@@ -404,3 +404,16 @@ def test_host_piece_ranges_keep_every_element_in_its_chunk_order(n):
     # chunk 3 of an 8-rank buffer of 8 Mi fp32 (4 MiB) as one piece: 8 equal parts in its order
     rs = piece_ranges(8, 8 << 20, 6, 4 * (3 << 20), 4 * (4 << 20), 1)
     assert [l for _, l, _ in rs] == [512 << 10] * 8 and {f for _, _, f in rs} == {3}
+
+
+def test_host_pipeline_default_piece_is_16MiB(monkeypatch):
+    """With RDC_HOST_PIECE_BYTES unset, pieces are 16 MiB (round 4's measured
+    default, rdc_host.cpp HostPieceBytes): 256 MiB = the ramp (2, 4, 8 MiB),
+    pieces of about 16 MiB, the mirrored ramp."""
+    monkeypatch.delenv("RDC_HOST_PIECE_BYTES", raising=False)
+    monkeypatch.delenv("RDC_HOST_PIECE_RAMP", raising=False)
+    b = host_pieces([256 << 20], {})[256 << 20]
+    lens = [y - x for x, y in zip(b, b[1:])]
+    P = 16 << 20
+    assert lens[:3] == [P // 8, P // 4, P // 2] and max(lens) <= P + 4096, lens
+    assert sum(lens) == 256 << 20

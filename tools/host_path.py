@@ -7,6 +7,8 @@ allreduce, D2H copy, synchronise (RdcAllreduce on a numpy buffer).
     RDC_BENCH_PINNED=1 ...: the buffer is a registered RdcNewBuffer(pinned=1)
     range (page-aligned mmap), so the library DMAs it in place
     (RDC_BENCH_THP=1: madvise(MADV_HUGEPAGE) on that mmap first)
+    RDC_BENCH_GAP_MS=G: the host idles G ms before every call (untimed), as a
+    training step's compute would between allreduces
 
 Prints one JSON line (rank 0) with GB/s = S / t per call (max over ranks).
 """
@@ -68,13 +70,18 @@ def main():
     if world > 1:
         dist.barrier()
     per = []
+    gap = float(os.environ.get("RDC_BENCH_GAP_MS", "0")) / 1e3  # idle host time before every call (not timed)
+    idle = 0.0
     t0 = time.perf_counter()
     for _ in range(iters):
+        if gap > 0:
+            time.sleep(gap)
+            idle += gap
         t1 = time.perf_counter()
         call()
         per.append(time.perf_counter() - t1)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / iters
+    dt = (time.perf_counter() - t0 - idle) / iters
     per_call_ms = [round(x * 1e3, 3) for x in per]
     per.sort()
     med_us, max_us = per[len(per) // 2] * 1e6, per[-1] * 1e6
