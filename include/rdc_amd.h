@@ -309,6 +309,15 @@ int RdcFill(void* dev_buf, size_t count, int dtype, uint64_t seed, int rank, voi
  * the communicator on one physical GPU, cus the fewest CUs of any rank's GPU.
  * Returns the grid (not a status). */
 int RdcPlanResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu);
+/* The clamp communicators apply (round 4): a dispatch sends workgroup i to
+ * XCD i % xcds, so the grid is min(want, xcds x floor((blocks_per_cu x
+ * cus / xcds - blocks_per_cu x reserve_cus) / ranks_per_gpu)) — every XCD
+ * holds every rank's share even when the reserve_cus CUs kept for resident
+ * service blocks all sit on one XCD (xcds = 1 when it does not divide cus).
+ * With xcds = 1 and reserve_cus = 0 it is RdcPlanResidentGrid.  Communicators
+ * pass hipDeviceAttributeNumberOfXccs (the most of any rank) and reserve one
+ * CU per rank on the GPU. */
+int RdcPlanResidentGridXcd(int want, int blocks_per_cu, int cus, int ranks_per_gpu, int xcds, int reserve_cus);
 /* The tree allreduce's fold for n ranks (rdc_reduce_ring_mincount path): the
  * post-order program acc[dst[i]] = OP(acc[dst[i]], acc[src[i]]), i < n-1,
  * over the n ranks' inputs (acc[q] = rank q's value); the result is acc[0].

@@ -55,6 +55,7 @@ def _load():
         "RdcCommGetParam": (i, [vp, ctypes.c_char_p, ctypes.POINTER(u64)]),
         "RdcPlanTree": (i, [i, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
         "RdcPlanResidentGrid": (i, [i, i, i, i]),
+        "RdcPlanResidentGridXcd": (i, [i, i, i, i, i, i]),
         "RdcCommAllreduce": (i, [vp, vp, sz, i, i, vp]),
         "RdcCommAllreduceEx": (i, [vp, vp, sz, i, i, i, vp]),
         "RdcCommBroadcast": (i, [vp, vp, sz, i, vp]),

@@ -710,6 +710,10 @@ int RdcPlanResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu)
     return ResidentGrid(want, blocks_per_cu, cus, ranks_per_gpu);
 }
 
+int RdcPlanResidentGridXcd(int want, int blocks_per_cu, int cus, int ranks_per_gpu, int xcds, int reserve_cus) {
+    return ResidentGrid(want, blocks_per_cu, cus, ranks_per_gpu, xcds, reserve_cus);
+}
+
 int RdcPlanLayout(int n, size_t scratch_bytes, uint64_t* out4) {
     return guard([&] {
         if (n < 1 || n > RDC_MAX_RANKS || !out4) throw std::invalid_argument("rdc: bad argument");

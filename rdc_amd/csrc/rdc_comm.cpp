@@ -79,7 +79,7 @@ struct PeerInfo {
     uint64_t max_tiles;
     uint64_t p2p_slot_bytes;
     int32_t num_cus;
-    int32_t pad2;
+    int32_t num_xcds;  // hipDeviceAttributeNumberOfXccs (dispatch round-robins workgroups over them)
     uint64_t plan[kPlanKeys];  // PlanKey: the parameters that shape a launch plan (must agree)
     char host[64];
     char pci[32];  // physical GPU (ranks may share one: tests, emulation)
@@ -269,6 +269,34 @@ bool strict_fences() {
     return on;
 }
 
+// RDC_LAUNCH_LOG=<prefix>: every collective launch appended to <prefix>.<pid>
+// (communicator, launch number, kind, bytes, grid, tile) — diagnostics for
+// ranks whose launch sequences diverge
+void log_launch(const Communicator* c, uint32_t seq, int kind, uint64_t bytes, int grid, uint64_t tile) {
+    static const char* prefix = getenv("RDC_LAUNCH_LOG");
+    if (!prefix || !*prefix) return;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    static FILE* f = [] {
+        char path[512];
+        snprintf(path, sizeof(path), "%s.%d", getenv("RDC_LAUNCH_LOG"), (int)getpid());
+        return fopen(path, "a");
+    }();
+    if (!f) return;
+    // the device's block-arrival and completed-launch counters before this
+    // launch (a synchronous read: waits for this rank's earlier launches)
+    uint32_t w[16] = {0};
+    uint64_t ctr = 0;
+    if (c->err_words()) {
+        (void)hipMemcpy(w, c->err_words() + 16, sizeof(uint32_t), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(&ctr, c->err_words() + 32, sizeof(ctr), hipMemcpyDeviceToHost);
+    }
+    fprintf(f, "%s rank %d launch %u kind %d bytes %llu grid %d tile %llu | arrivals %u completed %llu\n",
+            c->name().c_str(), c->rank(), seq, kind, (unsigned long long)bytes, grid, (unsigned long long)tile, w[0],
+            (unsigned long long)ctr);
+    fflush(f);
+}
+
 bool share_enabled() {
     const char* v = getenv("RDC_SHARE_SCRATCH");
     return !(v && *v && atoi(v) == 0);
@@ -366,8 +394,19 @@ void Communicator::AllocChannel() {
     ch->svc_region = static_cast<char*>(alloc_shared(svc_bytes, &k5));
     hip_check(hipMemset(ch->svc_region, 0, svc_bytes), "memset service slots");
     ch->alloc_kind = std::max(std::max(std::max(k1, k2), k3), k5);
-    // [0] error word, [16] block arrival counter, [32] completed-launch counter, [48] last kind
-    hip_check(hipMalloc(&ch->err, 256), "hipMalloc err");
+    // [0] error word, [16] block arrival counter, [32] completed-launch counter, [48] last kind.
+    // [64..] the first timed-out wait (rdc_device.h block_wait: seq, flag value,
+    // flag address).  Uncached like the flags: every block of a launch reads
+    // the launch counter and the error word and adds to the arrival counter
+    // from whichever XCD it runs on, and the launch's last block rewrites them,
+    // so no XCD's L2 may keep a line of them.
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ch->err), 256, hipDeviceMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ch->err), 256, hipDeviceMallocFinegrained) != hipSuccess) {
+            (void)hipGetLastError();
+            hip_check(hipMalloc(&ch->err, 256), "hipMalloc err");
+        }
+    }
     hip_check(hipMemset(ch->flags, 0, ch->L.flag_bytes), "memset flags");
     hip_check(hipMemset(ch->err, 0, 256), "memset err");
     hip_check(hipHostMalloc(reinterpret_cast<void**>(&ch->err_host), 64, hipHostMallocCoherent), "hipHostMalloc err");
@@ -429,6 +468,17 @@ void Communicator::Alias() {
     }
 }
 
+namespace {
+int device_xcds(int device) {
+    int x = 0;
+    if (hipDeviceGetAttribute(&x, hipDeviceAttributeNumberOfXccs, device) != hipSuccess || x < 1) {
+        (void)hipGetLastError();
+        x = 1;
+    }
+    return x;
+}
+}  // namespace
+
 void Communicator::AllocLocal() {
     hip_check(hipSetDevice(device_), "hipSetDevice");
     AllocChannel();
@@ -436,6 +486,7 @@ void Communicator::AllocLocal() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_) == hipSuccess && cus > 0)
         num_cus_ = cus;
+    num_xcds_ = device_xcds(device_);
     int wclk = 0;  // kHz
     if (hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, device_) != hipSuccess || wclk <= 0)
         wclk = 100000;
@@ -459,6 +510,8 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         c->num_cus_ = cus;
+    c->num_xcds_ = device_xcds(device);
+    c->xcds_max_ = c->num_xcds_;
     int wclk = 0;  // kHz
     if (hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, device) != hipSuccess || wclk <= 0) wclk = 100000;
     c->wall_khz_ = wclk;
@@ -475,6 +528,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     mine.slot_bytes = L.slot_bytes;
     mine.max_tiles = L.max_tiles;
     mine.num_cus = c->num_cus_;
+    mine.num_xcds = c->num_xcds_;
     PlanKey(cfg, tune_file().empty() ? 0 : 1, mine.plan);
     std::shared_ptr<Channel> cand;
     if (share_enabled()) {
@@ -551,6 +605,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     c->share_max_ = 1;
     for (int p = 0; p < c->n_; ++p) {
         c->cus_min_ = std::min(c->cus_min_, std::max(1, (int)all[(size_t)p].num_cus));
+        c->xcds_max_ = std::max(c->xcds_max_, std::max(1, (int)all[(size_t)p].num_xcds));
         int same = 0;
         for (int q = 0; q < c->n_; ++q) same += strncmp(all[(size_t)p].pci, all[(size_t)q].pci, sizeof(mine.pci)) == 0;
         c->share_max_ = std::max(c->share_max_, same);
@@ -687,16 +742,18 @@ void Communicator::CreateGroup(const std::string& name, int n, const int* device
         c->ch_->svc_enabled = SmallService::Enabled();  // one process drives every rank: all or none
         cs.push_back(std::move(c));
     }
-    int share = 1, cus = cs[0]->num_cus_;
+    int share = 1, cus = cs[0]->num_cus_, xcds = 1;
     for (int i = 0; i < n; ++i) {
         int same = 0;
         for (int j = 0; j < n; ++j) same += devices[i] == devices[j];
         share = std::max(share, same);
         cus = std::min(cus, cs[(size_t)i]->num_cus_);
+        xcds = std::max(xcds, cs[(size_t)i]->num_xcds_);
     }
     for (auto& c : cs) {
         c->share_max_ = share;
         c->cus_min_ = cus;
+        c->xcds_max_ = xcds;
     }
     if (SmallService::Enabled() && SmallService::HxBytes() > 0) {  // one exchange region every rank uses
         void* hx = nullptr;
@@ -882,7 +939,8 @@ int Communicator::mesh_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_bl
 // be co-resident while the service runs (RDC_NBLOCKS / Tune / Autotune can
 // ask for 4 blocks per CU) and its waits would time out.
 int Communicator::LaunchGrid(int want, int blocks_per_cu) const {
-    return ResidentGrid(want, blocks_per_cu, std::max(1, cus_min_ - share_max_), share_max_);
+    // one CU per rank on the GPU kept for its resident service block (LDS-heavy)
+    return ResidentGrid(want, blocks_per_cu, cus_min_, share_max_, xcds_max_, share_max_);
 }
 
 void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStream_t stream, int algo) {
@@ -984,6 +1042,7 @@ void Communicator::LaunchTree(const KernelSet& ks, char* buf, uint64_t total, hi
         last_launch_[4] = p.tile_bytes;
         last_launch_[5] = RDC_ALGO_TREE;
         ++seq_;
+        log_launch(this, seq_, RDC_ALGO_TREE, len, p.nb_scatter, p.tile_bytes);
         hip_check(ks.tree(a, p.nb_scatter, stream), "launch tree allreduce");
     }
     trace_ = nullptr;
@@ -1022,6 +1081,7 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         last_launch_[4] = p.tile_bytes;
         last_launch_[5] = RDC_ALGO_ONESHOT;
         ++seq_;
+        log_launch(this, seq_, RDC_ALGO_ONESHOT, total, p.nb_scatter, p.tile_bytes);
         hip_check(ks.oneshot(a, p.nb_scatter, stream), "launch one-shot allreduce");
         return;
     }
@@ -1056,6 +1116,7 @@ void Communicator::LaunchRanges(const KernelSet& ks, char* buf, const uint64_t* 
         last_launch_[3] = (uint64_t)(algo == RDC_ALGO_RING ? 0 : p.nb_gather);
         last_launch_[4] = p.tile_bytes;
         last_launch_[5] = (uint64_t)algo;
+        log_launch(this, seq_, algo, total, grid, p.tile_bytes);
         a.units = units;
         a.nunits = nunits;
         if (algo == RDC_ALGO_RING) {
@@ -1306,6 +1367,7 @@ void Communicator::Broadcast(void* buf, size_t bytes, int root, hipStream_t stre
         // large pieces: root -> one forwarder per tile -> the other ranks (k_bcast)
         a.bcast_split = (n_ >= 3 && p.len[0] >= cfg_.bcast_split_bytes && p.tiles[0] >= n_ - 1) ? 1 : 0;
         ++seq_;
+        log_launch(this, seq_, 100, p.len[0], p.nb_scatter, p.tile_bytes);
         hip_check(launch_bcast(a, p.nb_scatter, stream), "launch broadcast");
     }
 }
@@ -1587,6 +1649,7 @@ void Communicator::Allgather(void* const* bufs, const uint64_t* sizes, hipStream
         a.nb_gather = p.nb_gather;
         a.kind = RDC_KIND_ALLGATHER;
         ++seq_;
+        log_launch(this, seq_, 101, 0, p.nb_scatter + p.nb_gather, p.tile_bytes);
         hip_check(launch_allgather(a, p.nb_scatter + p.nb_gather, stream), "launch allgather");
     }
 }
@@ -1680,9 +1743,14 @@ void Communicator::RaiseIfError(uint32_t e) const {
                                      " (communicators sharing a scratch channel were used in different orders "
                                      "on different ranks; issue them in one order everywhere or set "
                                      "RDC_SHARE_SCRATCH=0; communicator is now unusable)");
+        static const char* algos[] = {"auto", "ring", "mesh", "one-shot", "tree", "pull mesh"};
+        const uint64_t al = last_launch_[5];
         throw std::runtime_error(std::string("rdc: device collective failed on rank ") + std::to_string(rank_) +
                                  ": " + (e < 7 ? names[e] : "unknown") +
-                                 " (a peer did not join the collective; communicator is now unusable)");
+                                 " (a peer did not join the collective; communicator is now unusable; this "
+                                 "rank's last launch: " + (al < 6 ? algos[al] : "?") + ", grid " +
+                                 std::to_string(last_launch_[0]) + ", tile " + std::to_string(last_launch_[4]) +
+                                 " B, launches issued " + std::to_string(seq_) + ")");
     }
 }
 

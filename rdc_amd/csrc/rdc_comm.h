@@ -221,6 +221,7 @@ public:
     void SetLaunchCounter(uint64_t value);
 
     int rank() const { return rank_; }
+    uint32_t* err_words() const { return err_; }  // device: [0] error, [16] arrivals, [32] launches (diagnostics)
     int size() const { return n_; }
     Bootstrap* bootstrap() const { return bs_; }
     int device() const { return device_; }
@@ -314,6 +315,8 @@ private:
     int alloc_kind_ = 0;
     int num_cus_ = 256;             // this GPU
     int cus_min_ = 256;             // fewest CUs of any rank's GPU (grids are planned identically on all ranks)
+    int num_xcds_ = 1;              // this GPU's XCDs
+    int xcds_max_ = 1;              // most XCDs of any rank's GPU (ResidentGrid's per-XCD clamp)
     int share_max_ = 1;             // most ranks of this communicator on one physical GPU
     int wall_khz_ = 100000;         // wall_clock64() rate
     char* peer_scratch_[RDC_MAX_RANKS] = {};

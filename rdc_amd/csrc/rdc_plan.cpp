@@ -37,8 +37,15 @@ void SplitRanges(int64_t count, int n, int64_t* b, int64_t* e) {
     }
 }
 
-int ResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu) {
-    const long cap = std::max(1L, (long)std::max(1, blocks_per_cu) * std::max(1, cus) / std::max(1, ranks_per_gpu));
+int ResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu, int xcds, int reserve_cus) {
+    const long bpc = std::max(1, blocks_per_cu), ranks = std::max(1, ranks_per_gpu);
+    cus = std::max(1, cus);
+    if (xcds < 1 || cus % xcds != 0) xcds = 1;
+    // a dispatch sends workgroup i to XCD i % xcds, so each XCD must hold
+    // every rank's share of it; reserved CUs (resident service blocks) may
+    // all sit on one XCD, so every XCD gives them up
+    const long per_xcd = bpc * (cus / xcds) - bpc * std::max(0, reserve_cus);
+    const long cap = std::max(1L, per_xcd / ranks * xcds);
     return (int)std::max(1L, std::min<long>(want, cap));
 }
 

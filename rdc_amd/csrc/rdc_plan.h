@@ -57,7 +57,7 @@ struct MeshSplit {
 // the kernel) x cus / ranks_per_gpu (the most ranks sharing one physical GPU).
 // Every rank computes it from the same exchanged values, so the grid — and
 // the tile plan derived from it — is identical on all ranks.
-int ResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu);
+int ResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu, int xcds = 1, int reserve_cus = 0);
 
 // tile size and grid for a piece whose largest chunk is chunk_bytes
 void PlanTiles(size_t chunk_bytes, int n, int algo, size_t cfg_tile, int max_blocks, Piece* p,

@@ -338,8 +338,9 @@ def run_mp(world, cases, timeout=240, env_extra=None):
                 q.kill()
             raise
         outs.append(out.decode(errors="replace"))
-    for r, p in enumerate(procs):
-        assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r][-3000:])
+    failed = [r for r, p in enumerate(procs) if p.returncode != 0]
+    assert not failed, "\n".join("rank %d failed (rc %d):\n%s" % (r, procs[r].returncode, outs[r][-1500:])
+                                  for r in failed)
     return tmp
 
 
@@ -615,7 +616,7 @@ HOST_SWEEP_BYTES = [
 ]
 
 
-@pytest.mark.parametrize("world,balance", [(2, "0"), (3, "0"), (3, "1"), (5, "1")])
+@pytest.mark.parametrize("world,balance", [(2, "0"), (3, "0"), (3, "1"), (4, "1"), (5, "0"), (5, "1")])
 def test_mp_host_size_sweep(world, balance):
     """Host buffers at every boundary of the host path (rdc_host.cpp: service,
     copy-pool parts, zero-copy / staged small path, inline piece, pipeline

@@ -417,3 +417,44 @@ def test_host_pipeline_default_piece_is_16MiB(monkeypatch):
     P = 16 << 20
     assert lens[:3] == [P // 8, P // 4, P // 2] and max(lens) <= P + 4096, lens
     assert sum(lens) == 256 << 20
+
+
+def _xcd_loads(grid, xcds):
+    """Workgroups per XCD of one dispatch (workgroup i -> XCD i % xcds)."""
+    return [len(range(x, grid, xcds)) for x in range(xcds)]
+
+
+@pytest.mark.parametrize("per_cu,ranks,reserve,expect", [
+    (2, 1, 1, 496),   # one rank per GPU, its service block's CU kept: 8 x (64 - 2)
+    (2, 4, 4, 112),   # 4 ranks on one GPU with services: 8 x floor((64 - 8) / 4)
+    (2, 5, 5, 80),    # 5 ranks: the old clamp gave 100, i.e. 13 per XCD x 5 = 65 > 64 on XCDs 0-3
+    (2, 8, 8, 48),
+    (1, 3, 0, 80),
+])
+def test_resident_grid_per_xcd(per_cu, ranks, reserve, expect):
+    """rdc_plan.cpp ResidentGrid with XCDs (RdcPlanResidentGridXcd): on 256 CUs
+    in 8 XCDs every XCD holds every rank's workgroups of one dispatch, even
+    with every reserved CU on that XCD.  The old whole-GPU clamp let 5 ranks'
+    mesh grids of 100 put 65 workgroups on XCD 0's 64 slots, and a spinning
+    collective whose workgroup never starts waits out RDC_TIMEOUT (the 5-rank
+    host sweep on one GPU)."""
+    from rdc_amd._lib import _LIB
+    g = _LIB.RdcPlanResidentGridXcd(4096, per_cu, 256, ranks, 8, reserve)
+    assert g == expect
+    assert max(_xcd_loads(g, 8)) * ranks <= per_cu * 32 - per_cu * reserve
+    assert _LIB.RdcPlanResidentGridXcd(4096, per_cu, 256, ranks, 1, 0) == _LIB.RdcPlanResidentGrid(4096, per_cu, 256,
+                                                                                                     ranks)
+
+
+def test_resident_grid_per_xcd_never_oversubscribes_an_xcd():
+    from rdc_amd._lib import _LIB
+    rng = np.random.default_rng(5)
+    for _ in range(3000):
+        xcds = int(rng.choice([1, 2, 4, 8]))
+        cus = xcds * int(rng.integers(1, 40))
+        want, per_cu, ranks = int(rng.integers(1, 8192)), int(rng.integers(1, 9)), int(rng.integers(1, 17))
+        reserve = int(rng.integers(0, 3)) * ranks // 2
+        g = _LIB.RdcPlanResidentGridXcd(want, per_cu, cus, ranks, xcds, reserve)
+        assert 1 <= g <= max(1, want)
+        room = per_cu * (cus // xcds) - per_cu * reserve
+        assert g == 1 or max(_xcd_loads(g, xcds)) * ranks <= room, (want, per_cu, cus, ranks, xcds, reserve, g)
