@@ -400,15 +400,15 @@ void Communicator::AllocChannel() {
     // the launch counter and the error word and adds to the arrival counter
     // from whichever XCD it runs on, and the launch's last block rewrites them,
     // so no XCD's L2 may keep a line of them.
-    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ch->err), 256, hipDeviceMallocUncached) != hipSuccess) {
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ch->err), 512, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
-        if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ch->err), 256, hipDeviceMallocFinegrained) != hipSuccess) {
+        if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ch->err), 512, hipDeviceMallocFinegrained) != hipSuccess) {
             (void)hipGetLastError();
-            hip_check(hipMalloc(&ch->err, 256), "hipMalloc err");
+            hip_check(hipMalloc(&ch->err, 512), "hipMalloc err");
         }
     }
     hip_check(hipMemset(ch->flags, 0, ch->L.flag_bytes), "memset flags");
-    hip_check(hipMemset(ch->err, 0, 256), "memset err");
+    hip_check(hipMemset(ch->err, 0, 512), "memset err");
     hip_check(hipHostMalloc(reinterpret_cast<void**>(&ch->err_host), 64, hipHostMallocCoherent), "hipHostMalloc err");
     memset(ch->err_host, 0, 64);
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ch->err_host_dev), ch->err_host, 0),
@@ -616,13 +616,15 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         const char* q = getenv("GPU_MAX_HW_QUEUES");
         const int per = q && *q ? atoi(q) : 4;
         static bool warned = false;
-        if (c->rank_ == 0 && !warned && c->share_max_ * per > 16) {
+        // (and 5 x 3 queues: time-sliced, hand-offs lost; rdc_amd/launcher.py hw_queues_per_process)
+        const int want = std::max(1, 16 / c->share_max_) == 3 ? 2 : std::max(1, 16 / c->share_max_);
+        if (c->rank_ == 0 && !warned && c->share_max_ > 1 && (c->share_max_ * per > 16 || (per == 3 && c->share_max_ > 4))) {
             warned = true;
             fprintf(stderr,
                     "rdc: %d ranks share one GPU with GPU_MAX_HW_QUEUES=%d each; the GPU time-slices that many "
                     "queues and collectives wait ~10 ms per slice. Set GPU_MAX_HW_QUEUES=%d (rdc_amd.launcher "
                     "does)\n",
-                    c->share_max_, per, std::max(1, 16 / c->share_max_));
+                    c->share_max_, per, want);
         }
     }
     // schedules and shapes an earlier Autotune of this node measured for this
@@ -897,6 +899,8 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     a->half_bytes = OneshotHalfBytes(layout());
     a->timeout_ticks = (uint64_t)(cfg_.timeout_s * (double)wall_khz_ * 1000.0);
     a->uc = (alloc_kind_ == 0 && !strict_fences()) ? 1 : 0;
+    static const bool seq_check = getenv("RDC_SEQ_CHECK") && atoi(getenv("RDC_SEQ_CHECK")) != 0;
+    a->expect = seq_check ? (uint64_t)seq_ + 1 : 0;  // the launch about to be issued (one communicator per channel)
 }
 
 Layout Communicator::layout() const {
@@ -1745,12 +1749,41 @@ void Communicator::RaiseIfError(uint32_t e) const {
                                      "RDC_SHARE_SCRATCH=0; communicator is now unusable)");
         static const char* algos[] = {"auto", "ring", "mesh", "one-shot", "tree", "pull mesh"};
         const uint64_t al = last_launch_[5];
+        // the first timed-out wait (rdc_device.h block_wait): which flag, the
+        // launch number it waited for and the value it last saw
+        std::string waited;
+        uint32_t diag[8] = {0};
+        if (err_ && hipMemcpy(diag, err_ + 64, sizeof(diag), hipMemcpyDeviceToHost) == hipSuccess && diag[0] == 1) {
+            uint64_t d[3];
+            memcpy(d, diag + 2, sizeof(d));
+            const uint64_t at = (d[2] - (uint64_t)(uintptr_t)flags_) / sizeof(uint64_t);
+            const uint64_t mt = max_tiles_ ? max_tiles_ : 1;
+            char buf[200];
+            snprintf(buf, sizeof(buf), "; waited for launch %llu (tag %llu) at flag row %llu tile %llu, saw launch %llu "
+                     "(tag %llu)", (unsigned long long)(d[0] >> 8), (unsigned long long)(d[0] & 255),
+                     (unsigned long long)(at / mt), (unsigned long long)(at % mt), (unsigned long long)(d[1] >> 8),
+                     (unsigned long long)(d[1] & 255));
+            waited = buf;
+        } else {
+            (void)hipGetLastError();
+        }
+        if (err_ && hipMemcpy(diag, err_ + 72, sizeof(diag), hipMemcpyDeviceToHost) == hipSuccess && diag[0] == 1) {
+            uint64_t d[3];
+            memcpy(d, diag + 2, sizeof(d));
+            char buf[160];
+            snprintf(buf, sizeof(buf), "; a block of launch %llu read launch number %llu (block %llu of %llu)",
+                     (unsigned long long)d[1], (unsigned long long)d[0], (unsigned long long)(d[2] & 0xffffffffu),
+                     (unsigned long long)(d[2] >> 32));
+            waited += buf;
+        } else {
+            (void)hipGetLastError();
+        }
         throw std::runtime_error(std::string("rdc: device collective failed on rank ") + std::to_string(rank_) +
                                  ": " + (e < 7 ? names[e] : "unknown") +
                                  " (a peer did not join the collective; communicator is now unusable; this "
                                  "rank's last launch: " + (al < 6 ? algos[al] : "?") + ", grid " +
                                  std::to_string(last_launch_[0]) + ", tile " + std::to_string(last_launch_[4]) +
-                                 " B, launches issued " + std::to_string(seq_) + ")");
+                                 " B, launches issued " + std::to_string(seq_) + waited + ")");
     }
 }
 

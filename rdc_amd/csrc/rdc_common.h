@@ -118,6 +118,8 @@ struct CollArgs {
     int uc;                              // 1: every scratch region is uncached (hand-offs need no L2
                                          //   write-back, rdc_device.h block_publish)
     uint64_t* trace;                     // optional (mesh/ring): per block {start, end} wall_clock64 ticks
+    uint64_t expect;                     // RDC_SEQ_CHECK: the launch number the host issued (diagnostics;
+                                         //   a block that reads another one records it, err words 72..)
 };
 
 // ------------------------------------------------ small-allreduce service --

@@ -274,9 +274,11 @@ __device__ __forceinline__ bool block_wait(uint64_t* const* flags, int nflags, u
         bool ok = true;
         bool wrong = false;  // this lane's flag reached the counter with another tag
         uint32_t spins = 0;
+        uint64_t seen = 0;   // this lane's last flag value
         while (true) {
             if (!mine) {
                 const uint64_t v = flag_load(flags[lane]);
+                seen = v;
                 if (seq_reached(v, seq)) {
                     if (!tagged || same_tag(v, seq)) mine = true;
                     else wrong = true;
@@ -294,6 +296,23 @@ __device__ __forceinline__ bool block_wait(uint64_t* const* flags, int nflags, u
                 if (__any(dead)) { ok = false; break; }
             }
             __builtin_amdgcn_s_sleep(1);
+        }
+        if (!ok) {
+            // the first wait to give up records what it waited for (err words
+            // 64..71: claim, -, seq, flag value, flag address), before the
+            // error word tells the other blocks to give up
+            const uint64_t open = __ballot(!mine);
+            if (open != 0 && lane == (int)__builtin_ctzll(open)) {
+                uint32_t expected = 0;
+                if (__hip_atomic_compare_exchange_strong(ab.err + 64, &expected, 1u, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    uint64_t* d = reinterpret_cast<uint64_t*>(ab.err + 66);
+                    __hip_atomic_store(d, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(d + 1, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(d + 2, (uint64_t)(uintptr_t)flags[lane], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
         }
         if (lane == 0) {
             if (ok && !uc) {

@@ -44,6 +44,17 @@ __device__ __forceinline__ uint64_t* done_word(const CollArgs& a, int owner, int
 // (rdc_device.h).
 __device__ __forceinline__ uint64_t launch_seq(const CollArgs& a) {
     const uint64_t done = __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.expect != 0 && done + 1ull != a.expect && threadIdx.x == 0) {  // RDC_SEQ_CHECK diagnostics
+        uint32_t expected = 0;
+        if (__hip_atomic_compare_exchange_strong(a.err + 72, &expected, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+            uint64_t* d = reinterpret_cast<uint64_t*>(a.err + 74);
+            __hip_atomic_store(d, done + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(d + 1, a.expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(d + 2, (uint64_t)blockIdx.x | ((uint64_t)gridDim.x << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     return ((done + 1ull) << kTagBits) | ((uint64_t)a.tag & kTagMask);
 }
 // A channel that failed (a peer missed a hand-off, an order violation) is

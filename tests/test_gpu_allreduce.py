@@ -324,7 +324,8 @@ def run_mp(world, cases, timeout=240, env_extra=None):
     # to workers that share a GPU (8 ranks -> 2 queues each)
     from rdc_amd.launcher import hw_queues_per_process, queues_over_budget
     q = hw_queues_per_process(world)
-    if q is not None and env.get("RDC_DEVICE") != "rank" and queues_over_budget(env.get("GPU_MAX_HW_QUEUES"), q):
+    if (q is not None and env.get("RDC_DEVICE") != "rank" and not env.get("RDC_TEST_KEEP_QUEUES")
+            and queues_over_budget(env.get("GPU_MAX_HW_QUEUES"), q)):
         env["GPU_MAX_HW_QUEUES"] = str(q)
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), str(r), str(world),
                                str(port), tmp, cf], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
