@@ -162,7 +162,7 @@ __device__ __forceinline__ void mesh_fold_elem(const CollArgs& a, char* own, con
 // slot0 (rank q's copy at slot0 + q*slot_bytes) in ring order; the result also
 // goes to every peer's allgather region at byte offset soff.
 template <int OP, typename T, int NMAX>
-__device__ void mesh_reduce_range(const CollArgs& a, char* own, const char* slot0, uint64_t soff, uint64_t tlen) {
+__device__ __forceinline__ void mesh_reduce_range(const CollArgs& a, char* own, const char* slot0, uint64_t soff, uint64_t tlen) {
     const int n = a.n, r = a.rank, f = a.fold[r];
     const unsigned tid = threadIdx.x;
     if ((((uintptr_t)own ^ (uintptr_t)slot0) & 15) != 0) {
@@ -285,7 +285,7 @@ __device__ __forceinline__ void for_unit_pieces(const CollArgs& a, uint64_t p0, 
 }
 
 template <int OP, typename T, int NMAX>
-__device__ void mesh_body(const CollArgs& a, uint64_t seq) {
+__device__ __forceinline__ void mesh_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     int b = blockIdx.x;
@@ -390,7 +390,7 @@ __device__ void mesh_body(const CollArgs& a, uint64_t seq) {
 // owner overwrites its AG slot for tile t only after folding the NEXT
 // launch's tile t, which needs every peer's next-launch stage.
 template <int OP, typename T, int NMAX>
-__device__ void pull_fold_range(const CollArgs& a, char* own, const char* const* src, char* res, uint64_t tlen) {
+__device__ __forceinline__ void pull_fold_range(const CollArgs& a, char* own, const char* const* src, char* res, uint64_t tlen) {
     const int n = a.n, r = a.rank, f = a.fold[r];  // the ring order of chunk f
     const unsigned tid = threadIdx.x;
     auto fold_elem = [&](uint64_t e) {
@@ -456,7 +456,7 @@ __device__ void pull_fold_range(const CollArgs& a, char* own, const char* const*
 }
 
 template <int OP, typename T, int NMAX>
-__device__ void mesh_pull_body(const CollArgs& a, uint64_t seq) {
+__device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
     Abort ab{a.err, wall_clock64() + a.timeout_ticks};
     int b = blockIdx.x;
@@ -1108,7 +1108,9 @@ __device__ __forceinline__ bool ll_match(const v4u& lo, const v4u& hi, uint32_t 
 // {w2, seq, w3, seq} at plane 1 + 16 i, so the 64 lanes of one instruction
 // touch 1 KiB of contiguous memory (an interleaved 32-byte pair per lane made
 // every instruction 64 separate 16-byte requests).
-template <int OP, typename T, int NMAX, int BS>
+// HX: compiled with the host exchange (a.hx set); the default variant keeps
+// its polling arrays out of the register budget
+template <int OP, typename T, int NMAX, int BS, bool HX>
 __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
     constexpr int L = 16 / sizeof(T);  // elements per vector
     constexpr int U = 4;               // input vectors in flight per thread
@@ -1118,7 +1120,7 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
     const int n = a.n, r = a.rank;
     const unsigned tid = threadIdx.x;
     SvcBox* box = a.box;
-    const bool hxm = a.hx != nullptr;
+    const bool hxm = HX && a.hx != nullptr;
     const uint32_t all = (n >= 32 ? ~0u : (1u << n) - 1u);
     __shared__ v4u s_in[RDC_SVC_MAX_BYTES / 16];  // this rank's input, read once over PCIe
     __shared__ v4u s_pv[NMAX * BS];               // [q][thread]: rank q's vector being folded
@@ -1389,10 +1391,15 @@ struct Kernels {
         return hipGetLastError();
     }
     static hipError_t svc(const SvcArgs& a, hipStream_t s) {
-        if (a.n <= 8)
-            hipLaunchKernelGGL((k_svc<OP, T, 8, 512>), dim3(1), dim3(512), 0, s, a);
+        const bool hx = a.hx != nullptr;
+        if (a.n <= 8 && hx)
+            hipLaunchKernelGGL((k_svc<OP, T, 8, 512, true>), dim3(1), dim3(512), 0, s, a);
+        else if (a.n <= 8)
+            hipLaunchKernelGGL((k_svc<OP, T, 8, 512, false>), dim3(1), dim3(512), 0, s, a);
+        else if (hx)
+            hipLaunchKernelGGL((k_svc<OP, T, 16, 256, true>), dim3(1), dim3(256), 0, s, a);
         else
-            hipLaunchKernelGGL((k_svc<OP, T, 16, 256>), dim3(1), dim3(256), 0, s, a);
+            hipLaunchKernelGGL((k_svc<OP, T, 16, 256, false>), dim3(1), dim3(256), 0, s, a);
         return hipGetLastError();
     }
     static hipError_t tree(const CollArgs& a, int grid, hipStream_t s) {
