@@ -70,8 +70,10 @@ for step in "$@"; do
         cp $(find $OUT/prof_n1 -name "*kernel_stats.csv" | head -1) $OUT/bench_n1_kernel_stats.csv
         head -3 $OUT/bench_n1_kernel_stats.csv ;;
     benchN)
-        run_bench_n $a1 $OUT/bench_n$a1.txt $(echo "$a2" | tr ',' ' ') || { tail -20 $OUT/bench_n$a1.txt.err; exit 1; }
-        grep '^{' $OUT/bench_n$a1.txt | head -c 400; echo ;;
+        tagged=$OUT/bench_n$a1$(echo "${a2:+_$a2}" | tr ',-' '__').txt   # one file per (n, args)
+        run_bench_n $a1 $tagged $(echo "$a2" | tr ',' ' ') || { tail -20 $tagged.err; exit 1; }
+        cp $tagged $OUT/bench_n$a1.txt
+        grep '^{' $tagged | head -c 400; echo ;;
     pmc1)
         P=$OUT/pmc_n1
         rm -rf $P && mkdir -p $P
