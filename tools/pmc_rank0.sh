@@ -5,7 +5,7 @@
 # beside unprofiled ones counts its own requests exactly, profiles/r02/
 # pmc_uc_ipc/).  One counter group per pass (MI355X_MICROARCH.md: FETCH_SIZE
 # and WRITE_SIZE do not fit one TCC pass), then tools/pmc_traffic.py.
-#   tools/pmc_rank0.sh <ring|mesh|oneshot> <world> <bytes> [out-dir]
+#   tools/pmc_rank0.sh <ring|mesh|mesh_pull|oneshot> <world> <bytes> [out-dir]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -29,5 +29,7 @@ pass() {  # $1 = pass name, $2 = counters
     cp $(find $out/$1 -name "*counter_collection.csv" | head -1) $out/$1_counter_collection.csv
 }
 pass fetch FETCH_SIZE && pass write WRITE_SIZE && pass l2 "TCC_HIT_sum TCC_MISS_sum" || exit 1
-python3 tools/pmc_traffic.py $out/fetch_counter_collection.csv $out/write_counter_collection.csv "k_${algo}<" \
+kern="k_${algo}<"
+[ "$algo" = mesh_pull ] && kern="k_mesh<"   # the pull mesh is k_mesh with a.pull set
+python3 tools/pmc_traffic.py $out/fetch_counter_collection.csv $out/write_counter_collection.csv "$kern" \
     "${algo}_f32_n${world}_${bytes}" $out/traffic.json
