@@ -1142,8 +1142,76 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
         const char* hxh = hxm ? a.hx + (uint64_t)(seq & 1u) * (uint64_t)n * RDC_SVC_HX_RANK_BYTES : nullptr;
         uint32_t hpend = all;  // heager: ranks whose words of vector tid are not in s_pv yet
         v4u elo = {0, 0, 0, 0}, ehi = {0, 0, 0, 0};
-        int go;
-        for (;;) {
+        int go = 0;
+        // tid 0: the round's decision from its header / stop reads (shared
+        // with the host-exchange loop below)
+        auto decide = [&](uint64_t q, uint32_t stop) {
+            int g = 0;  // 0 poll again, 1 request, -1 leave
+            if ((uint32_t)(q >> 32) == seq) {
+                g = 1;
+            } else if (stop) {
+                g = -1;
+            } else if (wall_clock64() - t0 > a.idle_ticks) {
+                // leaving: EXITING, then one more look at the header (the
+                // host posts it and then reads `state`; seq_cst both sides)
+                box_store(&box->state, RDC_SVC_EXITING);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+                g = -1;
+                q = box_load64(&box->hdr);
+                if ((uint32_t)(q >> 32) == seq) {
+                    box_store(&box->state, RDC_SVC_RUNNING);
+                    g = 1;
+                }
+            }
+            s_req = q;
+            s_go = g;
+        };
+        if (!HX) {
+            // Two rounds in flight: round k+1's reads go out before round k
+            // is examined, so a request that lands is seen about 1.25 PCIe
+            // round trips later instead of 1.5 (loads return in order; the
+            // compiler waits only for the older round).  Same reads, twice
+            // as often while idle.
+            v4u loA = {0, 0, 0, 0}, hiA = {0, 0, 0, 0}, loB = {0, 0, 0, 0}, hiB = {0, 0, 0, 0};
+            uint64_t qA = 0, qB = 0;
+            uint32_t sA = 0, sB = 0;
+            // branch-free (every lane reads; lanes past the eager range and
+            // waves other than 0 re-read vector 0 and the header, one request
+            // per wave), so the compiler's wait for a round's reads leaves the
+            // next round's in flight
+            const uint64_t ev = eager ? tid : 0;
+            auto issue = [&](v4u& lo, v4u& hi, uint64_t& q, uint32_t& st) {
+                lo = ld16_nt(box->data + 16 * ev);
+                hi = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * ev);
+                q = box_load64(&box->hdr);
+                st = box_load(&box->stop);
+            };
+            auto round = [&](uint64_t q, uint32_t st) {
+                if (tid == 0) decide(q, st);
+                __syncthreads();
+                const int g = s_go;
+                __syncthreads();  // s_go is rewritten by the next round
+                return g;
+            };
+            issue(loA, hiA, qA, sA);
+            for (;;) {
+                issue(loB, hiB, qB, sB);
+                go = round(qA, sA);
+                if (go != 0) {
+                    elo = loA;
+                    ehi = hiA;
+                    break;
+                }
+                issue(loA, hiA, qA, sA);
+                go = round(qB, sB);
+                if (go != 0) {
+                    elo = loB;
+                    ehi = hiB;
+                    break;
+                }
+            }
+        }
+        for (; HX;) {
             if (eager) {
                 elo = ld16_nt(box->data + 16 * tid);
                 ehi = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * tid);
@@ -1165,27 +1233,9 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                     }
             }
             if (tid == 0) {
-                uint64_t q = box_load64(&box->hdr);
+                const uint64_t q = box_load64(&box->hdr);
                 const uint32_t stop = box_load(&box->stop);  // issued with the header read: one round trip
-                int g = 0;  // 0 poll again, 1 request, -1 leave
-                if ((uint32_t)(q >> 32) == seq) {
-                    g = 1;
-                } else if (stop) {
-                    g = -1;
-                } else if (wall_clock64() - t0 > a.idle_ticks) {
-                    // leaving: EXITING, then one more look at the header (the
-                    // host posts it and then reads `state`; seq_cst both sides)
-                    box_store(&box->state, RDC_SVC_EXITING);
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-                    g = -1;
-                    q = box_load64(&box->hdr);
-                    if ((uint32_t)(q >> 32) == seq) {
-                        box_store(&box->state, RDC_SVC_RUNNING);
-                        g = 1;
-                    }
-                }
-                s_req = q;
-                s_go = g;
+                decide(q, stop);
             }
             __syncthreads();
             go = s_go;
