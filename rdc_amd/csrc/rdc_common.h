@@ -161,6 +161,7 @@ struct SvcArgs {
     char* hx;                       // device address of the host exchange region, or null
     int hx_eager;                   // threads that poll every rank's exchange words of their vector
                                     //   while polling the header
+    int pipe;                       // RDC_HOST_SERVICE_PIPELINE: two poll rounds in flight
     uint64_t idle_ticks;            // wall_clock64 ticks without a request before exiting
     uint64_t timeout_ticks;         // waiting for a peer's contribution
     int tree_len;

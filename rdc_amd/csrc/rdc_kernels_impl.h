@@ -1166,12 +1166,14 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
             s_req = q;
             s_go = g;
         };
-        if (!HX) {
-            // Two rounds in flight: round k+1's reads go out before round k
-            // is examined, so a request that lands is seen about 1.25 PCIe
-            // round trips later instead of 1.5 (loads return in order; the
-            // compiler waits only for the older round).  Same reads, twice
-            // as often while idle.
+        if (!HX && a.pipe) {
+            // RDC_HOST_SERVICE_PIPELINE=1: two rounds in flight — round k+1's
+            // reads go out before round k is examined, so a request that lands
+            // is seen about 1.25 PCIe round trips later instead of 1.5 (loads
+            // return in order; the compiler waits only for the older round).
+            // Twice the reads while idle: on one shared link the trace's
+            // poll + done fell 4.9 -> 4.1 us but small_latency's 4 B call rose
+            // 6.2 -> 7.7 us (profiles/r04/svc_pipeline/), so it is opt-in.
             v4u loA = {0, 0, 0, 0}, hiA = {0, 0, 0, 0}, loB = {0, 0, 0, 0}, hiB = {0, 0, 0, 0};
             uint64_t qA = 0, qB = 0;
             uint32_t sA = 0, sB = 0;
@@ -1211,7 +1213,7 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                 }
             }
         }
-        for (; HX;) {
+        for (; HX || !a.pipe;) {
             if (eager) {
                 elo = ld16_nt(box->data + 16 * tid);
                 ehi = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * tid);

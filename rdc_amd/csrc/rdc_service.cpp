@@ -58,6 +58,7 @@ SmallService::SmallService(int rank, int n, int device, char* const* region, uin
     ll_out_bytes_ = (uint64_t)std::min(env_double("RDC_HOST_SERVICE_LL_OUT_BYTES", 256), (double)RDC_SVC_LL_MAX);
     const int block = n <= 8 ? 512 : 256;  // Kernels::svc's block size
     args_.eager = std::max(0, std::min(block, (int)(env_double("RDC_HOST_SERVICE_EAGER_BYTES", 4096) / 16)));
+    args_.pipe = env_double("RDC_HOST_SERVICE_PIPELINE", 0) != 0 ? 1 : 0;  // two poll rounds in flight (k_svc)
     args_.hx_eager =
         std::max(0, std::min(block, (int)(env_double("RDC_HOST_SERVICE_HX_EAGER_BYTES", 8192) / (16.0 * n))));
     wall_khz_ = wall_khz;

@@ -510,7 +510,8 @@ def expected_host_mix(world, mincount=1):
                                        (3, {"RDC_HOST_SERVICE_HX_BYTES": "1048576", "RDC_HOST_SERVICE_HX_EAGER_BYTES": "0",
                                             "rdc_reduce_ring_mincount": "8K"}),
                                        (4, {"RDC_HOST_SERVICE_HX_BYTES": "1048576",
-                                            "RDC_HOST_SERVICE_HX_EAGER_BYTES": "65536"})])
+                                            "RDC_HOST_SERVICE_HX_EAGER_BYTES": "65536"}),
+                                       (3, {"RDC_HOST_SERVICE_PIPELINE": "1"})])
 def test_mp_host_small_service(world, env):
     """Small synchronous HOST allreduces (cfg1's path) through the resident
     service block (rdc_service.h): 12 calls of 1 B - 64 KiB over 8 (dtype, op)
@@ -521,7 +522,8 @@ def test_mp_host_small_service(world, env):
     kernel; RDC_HOST_SERVICE_SHARE_MAX lifts the one-GPU cap); the host
     exchange (RDC_HOST_SERVICE_HX_BYTES: every rank's input from one shared
     host region) at a 32 KiB budget and up to the 16 KiB LL limit, with no and
-    with whole-block eager polling; and the launch path with RDC_HOST_SERVICE=0.
+    with whole-block eager polling; two poll rounds in flight
+    (RDC_HOST_SERVICE_PIPELINE=1); and the launch path with RDC_HOST_SERVICE=0.
     Every result bit-exact against the oracle."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
