@@ -859,10 +859,11 @@ def test_mp_cfg5_exact_shape_eight_ranks():
 
 def test_mp_forced_oversized_grid_four_ranks():
     """RDC_NBLOCKS=4096 (4x what one GPU holds) on 4 processes sharing GPU 0:
-    every waiting launch is clamped to the resident share (ResidentGrid), so
-    the ring (>= 256 tiles per chunk), mesh, one-shot, broadcast and allgather
-    all complete bit-exact instead of timing out (round 1: k_ring at 768
-    blocks x 4 ranks on one GPU hit the device timeout)."""
+    every waiting launch is clamped to the resident share (ResidentGrid, per
+    XCD since round 4: a multiple of the 8 XCDs), so the ring (>= 256 tiles
+    per chunk), mesh, one-shot, broadcast and allgather all complete bit-exact
+    instead of timing out (round 1: k_ring at 768 blocks x 4 ranks on one GPU
+    hit the device timeout)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cases = [{"count": 16 << 20, "dtype": 6, "op": 2, "algo": 1, "last_launch": True, "reps": 2},
@@ -883,6 +884,8 @@ def test_mp_forced_oversized_grid_four_ranks():
         assert ll[0] < 4096 and ll[0] <= 8 * cus // 4, ll  # clamped (8 blocks per CU is the hardware ceiling)
     ll = json.load(open(os.path.join(tmp, "case0_rank0.launch")))
     assert (16 << 20) * 4 // 4 // ll[4] >= 256, ll  # ring: >= 256 tiles per chunk
+    if cus % 8 == 0:  # 8 XCDs: the clamp gives every XCD the same share of each rank's grid
+        assert ll[0] % 8 == 0, ll
 
 
 def test_mp_full_grid_beside_resident_service():
