@@ -98,6 +98,56 @@ __device__ __forceinline__ v4u reduce16(v4u d, v4u s) {
     return d;
 }
 
+// 8-bit integers, four lanes per dword without unpacking (the generic loop
+// spends ~12 VALU ops and a register per byte: the int8 / uint8 one-shot
+// needed 256 VGPRs and ran one wave per SIMD).  Sum wraps like the
+// reference's `dst += src` on a byte: low 7 bits added without carry-out,
+// top bit by XOR.  Max / Min: even and odd bytes as 16-bit lanes through
+// v_pk_max_u16 / v_pk_min_u16; signed bytes compare as unsigned after
+// flipping their sign bits.
+namespace swar8 {
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) {
+    return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
+}
+template <bool MAX>
+__device__ __forceinline__ uint32_t pick_u(uint32_t a, uint32_t b) {
+    const u16x2 ae = __builtin_bit_cast(u16x2, a & 0x00ff00ffu), be = __builtin_bit_cast(u16x2, b & 0x00ff00ffu);
+    const u16x2 ao = __builtin_bit_cast(u16x2, (a >> 8) & 0x00ff00ffu), bo = __builtin_bit_cast(u16x2, (b >> 8) & 0x00ff00ffu);
+    const u16x2 e = MAX ? __builtin_elementwise_max(ae, be) : __builtin_elementwise_min(ae, be);
+    const u16x2 o = MAX ? __builtin_elementwise_max(ao, bo) : __builtin_elementwise_min(ao, bo);
+    return __builtin_bit_cast(uint32_t, e) | (__builtin_bit_cast(uint32_t, o) << 8);
+}
+template <int OP, bool SIGNED>
+__device__ __forceinline__ v4u reduce(v4u d, v4u s) {
+    constexpr uint32_t flip = SIGNED ? 0x80808080u : 0u;
+    v4u out;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (OP == RDC_OP_SUM) out[k] = add(d[k], s[k]);
+        else if (OP == RDC_OP_BITOR) out[k] = d[k] | s[k];
+        else out[k] = pick_u<OP == RDC_OP_MAX>(d[k] ^ flip, s[k] ^ flip) ^ flip;
+    }
+    return out;
+}
+}  // namespace swar8
+template <>
+__device__ __forceinline__ v4u reduce16<RDC_OP_SUM, uint8_t>(v4u d, v4u s) { return swar8::reduce<RDC_OP_SUM, false>(d, s); }
+template <>
+__device__ __forceinline__ v4u reduce16<RDC_OP_SUM, int8_t>(v4u d, v4u s) { return swar8::reduce<RDC_OP_SUM, true>(d, s); }
+template <>
+__device__ __forceinline__ v4u reduce16<RDC_OP_BITOR, uint8_t>(v4u d, v4u s) { return swar8::reduce<RDC_OP_BITOR, false>(d, s); }
+template <>
+__device__ __forceinline__ v4u reduce16<RDC_OP_BITOR, int8_t>(v4u d, v4u s) { return swar8::reduce<RDC_OP_BITOR, true>(d, s); }
+template <>
+__device__ __forceinline__ v4u reduce16<RDC_OP_MAX, uint8_t>(v4u d, v4u s) { return swar8::reduce<RDC_OP_MAX, false>(d, s); }
+template <>
+__device__ __forceinline__ v4u reduce16<RDC_OP_MAX, int8_t>(v4u d, v4u s) { return swar8::reduce<RDC_OP_MAX, true>(d, s); }
+template <>
+__device__ __forceinline__ v4u reduce16<RDC_OP_MIN, uint8_t>(v4u d, v4u s) { return swar8::reduce<RDC_OP_MIN, false>(d, s); }
+template <>
+__device__ __forceinline__ v4u reduce16<RDC_OP_MIN, int8_t>(v4u d, v4u s) { return swar8::reduce<RDC_OP_MIN, true>(d, s); }
+
 // bf16 Sum, two lanes per dword: v_pk_add_f32 + v_cvt_pk_bf16_f32 instead of
 // a software round per element (the generic loop runs 4.35 TB/s, ALU-bound)
 template <>

@@ -153,8 +153,10 @@ def hw_queues_per_process(ranks_per_gpu):
     5 processes with 3 queues each ran time-sliced (the 5-rank host sweep took
     19 s instead of 11 s) and in about every second run a one-shot hand-off
     never arrived (its flag kept the previous launch's number), while 5 x 2,
-    5 x 4, 4 x 3 and 3 x 3 queues never showed it (profiles/r04/queues/);
-    the cause was not found, so 5 ranks per GPU get 2."""
+    5 x 4, 4 x 3 and 3 x 3 queues never showed it (profiles/r04/queues/;
+    every lost hand-off was in an int8 kernel at one wave per SIMD, and after
+    the byte folds shrank 5 x 3 passed 3 of 3 runs); the cause was not
+    found, so 5 ranks per GPU get 2."""
     if ranks_per_gpu * 4 <= QUEUE_BUDGET:
         return None
     q = max(1, QUEUE_BUDGET // ranks_per_gpu)
