@@ -1218,21 +1218,25 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                 elo = ld16_nt(box->data + 16 * tid);
                 ehi = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * tid);
             }
-            if (heager && hpend) {  // all pending ranks' loads in flight, then the matches
-                v4u hl[NMAX], hh[NMAX];
+            if (heager && hpend) {  // pending ranks' loads in flight four at a time, then the matches
+                constexpr int G = 4;      // (all NMAX at once spilled VGPRs to scratch)
 #pragma unroll
-                for (int q = 0; q < NMAX; ++q)
-                    if ((hpend >> q) & 1u) {
-                        const char* p = hxh + (uint64_t)q * RDC_SVC_HX_RANK_BYTES + 16 * tid;
-                        hl[q] = ld16_nt(p);
-                        hh[q] = ld16_nt(p + RDC_SVC_LL_MAX);
-                    }
+                for (int g = 0; g < NMAX; g += G) {
+                    v4u hl[G], hh[G];
 #pragma unroll
-                for (int q = 0; q < NMAX; ++q)
-                    if (((hpend >> q) & 1u) && ll_match(hl[q], hh[q], seq)) {
-                        s_pv[q * BS + tid] = v4u{hl[q].x, hl[q].z, hh[q].x, hh[q].z};
-                        hpend &= ~(1u << q);
-                    }
+                    for (int j = 0; j < G; ++j)
+                        if ((hpend >> (g + j)) & 1u) {
+                            const char* p = hxh + (uint64_t)(g + j) * RDC_SVC_HX_RANK_BYTES + 16 * tid;
+                            hl[j] = ld16_nt(p);
+                            hh[j] = ld16_nt(p + RDC_SVC_LL_MAX);
+                        }
+#pragma unroll
+                    for (int j = 0; j < G; ++j)
+                        if (((hpend >> (g + j)) & 1u) && ll_match(hl[j], hh[j], seq)) {
+                            s_pv[(g + j) * BS + tid] = v4u{hl[j].x, hl[j].z, hh[j].x, hh[j].z};
+                            hpend &= ~(1u << (g + j));
+                        }
+                }
             }
             if (tid == 0) {
                 const uint64_t q = box_load64(&box->hdr);

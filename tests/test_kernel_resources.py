@@ -6,9 +6,9 @@ k_mesh copied its 1.2 KiB argument block into per-lane scratch (1180 B/lane,
 `mesh_body` not inlined) and the int8 / uint8 folds took 256 VGPRs (one wave
 per SIMD).  Every collective kernel must stay free of scratch and below 256
 VGPRs, so that a waiting launch's grid clamp (rdc_plan.cpp ResidentGrid) and
-its occupancy stay what the planner assumes.  The opt-in host-exchange
-variant of the service kernel (k_svc<..., true>) is the one exception to the
-scratch rule (its polling arrays spill; it is off by default).
+its occupancy stay what the planner assumes.  (The opt-in host-exchange
+service variant spilled its polling arrays until it polled four ranks at a
+time.)
 """
 import os
 import re
@@ -77,9 +77,8 @@ def test_every_kernel_family_is_present(kernels):
         assert fam in names, fam
 
 
-def test_no_kernel_uses_scratch_except_the_opt_in_exchange_service(kernels):
-    bad = {k: v for k, v in kernels.items()
-           if v[0] != 0 and not re.search(r"k_svcI.*ELb1E", k)}
+def test_no_kernel_uses_scratch(kernels):
+    bad = {k: v for k, v in kernels.items() if v[0] != 0}
     assert not bad, bad
 
 
