@@ -396,16 +396,17 @@ void Communicator::AllocChannel() {
     ch->alloc_kind = std::max(std::max(std::max(k1, k2), k3), k5);
     // [0] error word, [16] block arrival counter, [32] completed-launch counter, [48] last kind.
     // [64..] the first timed-out wait (rdc_device.h block_wait: seq, flag value,
-    // flag address).  Uncached like the flags: every block of a launch reads
-    // the launch counter and the error word and adds to the arrival counter
-    // from whichever XCD it runs on, and the launch's last block rewrites them,
-    // so no XCD's L2 may keep a line of them.
-    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ch->err), 512, hipDeviceMallocUncached) != hipSuccess) {
+    // flag address).  Plain device memory, read and written with agent-scope
+    // atomics (sc1) only.  RDC_COUNTERS_UNCACHED=1 allocates it uncached like
+    // the flags; tried in round 4 while chasing the 5 x 3-queue hand-off loss,
+    // it did not change that, and small launches measured the same or a
+    // little slower (one-shot 4 B at n = 2 back to back: 7.54 vs 6.99-7.35 us
+    // per launch, profiles/r04/counters_ab/).
+    static const bool uc_counters = getenv("RDC_COUNTERS_UNCACHED") && atoi(getenv("RDC_COUNTERS_UNCACHED")) != 0;
+    if (!uc_counters ||
+        hipExtMallocWithFlags(reinterpret_cast<void**>(&ch->err), 512, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
-        if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ch->err), 512, hipDeviceMallocFinegrained) != hipSuccess) {
-            (void)hipGetLastError();
-            hip_check(hipMalloc(&ch->err, 512), "hipMalloc err");
-        }
+        hip_check(hipMalloc(&ch->err, 512), "hipMalloc err");
     }
     hip_check(hipMemset(ch->flags, 0, ch->L.flag_bytes), "memset flags");
     hip_check(hipMemset(ch->err, 0, 512), "memset err");
