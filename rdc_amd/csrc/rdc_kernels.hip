@@ -7,8 +7,8 @@
 namespace rdc_amd {
 
 __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
-    const uint64_t seq = launch_seq(a);
-    if (!channel_failed(a)) bcast_body(a, seq);
+    uint64_t seq;
+    if (!launch_begin(a, &seq)) bcast_body(a, seq);
     launch_done(a, seq);
 }
 
@@ -63,8 +63,8 @@ __device__ void allgather_body(const CollArgs& a, uint64_t seq) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_allgather(CollArgs a) {
-    const uint64_t seq = launch_seq(a);
-    if (!channel_failed(a)) allgather_body(a, seq);
+    uint64_t seq;
+    if (!launch_begin(a, &seq)) allgather_body(a, seq);
     launch_done(a, seq);
 }
 

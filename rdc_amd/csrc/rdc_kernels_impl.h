@@ -42,31 +42,36 @@ __device__ __forceinline__ uint64_t* done_word(const CollArgs& a, int owner, int
 // ranks issue the same collectives), and the launch's last block advances it.
 // seq = (counter << kTagBits) | the launching communicator's tag
 // (rdc_device.h).
-__device__ __forceinline__ uint64_t launch_seq(const CollArgs& a) {
-    const uint64_t done = __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.expect != 0 && done + 1ull != a.expect && threadIdx.x == 0) {  // RDC_SEQ_CHECK diagnostics
-        uint32_t expected = 0;
-        if (__hip_atomic_compare_exchange_strong(a.err + 72, &expected, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-            uint64_t* d = reinterpret_cast<uint64_t*>(a.err + 74);
-            __hip_atomic_store(d, done + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(d + 1, a.expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(d + 2, (uint64_t)blockIdx.x | ((uint64_t)gridDim.x << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    return ((done + 1ull) << kTagBits) | ((uint64_t)a.tag & kTagMask);
-}
+// Block start: thread 0 reads the launch counter and the channel's error word
+// together (one round trip instead of two), the block shares them through LDS.
 // A channel that failed (a peer missed a hand-off, an order violation) is
 // unusable: later launches move nothing — in particular they push nothing
 // into peers' scratch, where a peer still inside the failed launch would take
 // a later launch's flags (>= its seq) for its own — and only advance the
 // counters.  The host raises the recorded error at its next check.
-// (Block-uniform: one load by thread 0, shared with the block.)
-__device__ __forceinline__ bool channel_failed(const CollArgs& a) {
+// Returns true when the channel failed; *seq = this launch's sequence word.
+__device__ __forceinline__ bool launch_begin(const CollArgs& a, uint64_t* seq) {
+    __shared__ uint64_t s_done;
     __shared__ int s_failed;
-    if (threadIdx.x == 0) s_failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (threadIdx.x == 0) {
+        const uint64_t done = __hip_atomic_load(a.launch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_done = done;
+        s_failed = e != 0;
+        if (a.expect != 0 && done + 1ull != a.expect) {  // RDC_SEQ_CHECK diagnostics
+            uint32_t expected = 0;
+            if (__hip_atomic_compare_exchange_strong(a.err + 72, &expected, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                uint64_t* d = reinterpret_cast<uint64_t*>(a.err + 74);
+                __hip_atomic_store(d, done + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(d + 1, a.expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(d + 2, (uint64_t)blockIdx.x | ((uint64_t)gridDim.x << 32), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
     __syncthreads();
+    *seq = ((s_done + 1ull) << kTagBits) | ((uint64_t)a.tag & kTagMask);
     const bool f = s_failed != 0;
     __syncthreads();
     return f;
@@ -971,9 +976,11 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint64_t seq) {
     __syncthreads();
     if (threadIdx.x == 0) {
         if (fence) __threadfence_system();
-        const uint32_t prev = atomicAdd(a.done_ctr, 1u);
-        if (prev == gridDim.x - 1) {
-            __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // a one-block launch is its own last block: no arrival round trip
+        // (small messages run one block)
+        const bool last = gridDim.x == 1 || atomicAdd(a.done_ctr, 1u) == gridDim.x - 1;
+        if (last) {
+            if (gridDim.x > 1) __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int p = 0; p < a.n; ++p)
@@ -1003,8 +1010,8 @@ __device__ __forceinline__ void trace_block(const CollArgs& a, uint64_t t0) {
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
     const uint64_t t0 = wall_clock64();
-    const uint64_t seq = launch_seq(a);
-    if (!channel_failed(a)) {
+    uint64_t seq;
+    if (!launch_begin(a, &seq)) {
         if (a.pull) mesh_pull_body<OP, T, NMAX>(a, seq);
         else mesh_body<OP, T, NMAX>(a, seq);
     }
@@ -1014,23 +1021,23 @@ __global__ __launch_bounds__(kBlock) void k_mesh(CollArgs a) {
 
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_oneshot(CollArgs a) {
-    const uint64_t seq = launch_seq(a);
-    if (!channel_failed(a)) oneshot_body<OP, T, NMAX>(a, seq);
+    uint64_t seq;
+    if (!launch_begin(a, &seq)) oneshot_body<OP, T, NMAX>(a, seq);
     launch_done(a, seq);
 }
 
 template <int OP, typename T, int NMAX>
 __global__ __launch_bounds__(kBlock) void k_tree(CollArgs a) {
-    const uint64_t seq = launch_seq(a);
-    if (!channel_failed(a)) oneshot_body<OP, T, NMAX, true>(a, seq);
+    uint64_t seq;
+    if (!launch_begin(a, &seq)) oneshot_body<OP, T, NMAX, true>(a, seq);
     launch_done(a, seq);
 }
 
 template <int OP, typename T>
 __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
     const uint64_t t0 = wall_clock64();
-    const uint64_t seq = launch_seq(a);
-    if (!channel_failed(a)) ring_body<OP, T>(a, seq);
+    uint64_t seq;
+    if (!launch_begin(a, &seq)) ring_body<OP, T>(a, seq);
     trace_block(a, t0);
     launch_done(a, seq);
 }
