@@ -980,8 +980,11 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint64_t seq) {
         // (small messages run one block)
         const bool last = gridDim.x == 1 || atomicAdd(a.done_ctr, 1u) == gridDim.x - 1;
         if (last) {
+            // every block made its own writes visible (the fence above) before
+            // it arrived, so the last block adds no release fence of its own
+            // (each one is an L2 write-back): the done words say "finished
+            // reading", they publish nothing
             if (gridDim.x > 1) __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int p = 0; p < a.n; ++p)
                 if (p != a.rank) flag_store(done_word(a, p, a.rank), seq);
@@ -990,10 +993,14 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint64_t seq) {
             // the host reads the (sticky) error word here after a stream sync: no
             // copy needed.  The mirror starts at 0 and only ever changes to an
             // error, so the PCIe write (whose completion the kernel's end waits
-            // for) is made only when there is one.
+            // for) is made only when there is one — and then completed before
+            // the notify word, which the host reads first
             const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (e != 0) __hip_atomic_store(a.err_mirror, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (a.notify) __hip_atomic_store(a.notify, a.notify_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (e != 0) {
+                __hip_atomic_store(a.err_mirror, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (a.notify) __hip_atomic_store(a.notify, a.notify_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
