@@ -617,9 +617,8 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         const char* q = getenv("GPU_MAX_HW_QUEUES");
         const int per = q && *q ? atoi(q) : 4;
         static bool warned = false;
-        // (and 5 x 3 queues: time-sliced, hand-offs lost; rdc_amd/launcher.py hw_queues_per_process)
-        const int want = std::max(1, 16 / c->share_max_) == 3 ? 2 : std::max(1, 16 / c->share_max_);
-        if (c->rank_ == 0 && !warned && c->share_max_ > 1 && (c->share_max_ * per > 16 || (per == 3 && c->share_max_ > 4))) {
+        const int want = std::max(1, 16 / c->share_max_);
+        if (c->rank_ == 0 && !warned && c->share_max_ * per > 16) {
             warned = true;
             fprintf(stderr,
                     "rdc: %d ranks share one GPU with GPU_MAX_HW_QUEUES=%d each; the GPU time-slices that many "

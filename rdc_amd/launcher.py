@@ -149,18 +149,13 @@ QUEUE_BUDGET = 16
 
 def hw_queues_per_process(ranks_per_gpu):
     """GPU_MAX_HW_QUEUES for a process that shares its GPU with
-    ranks_per_gpu - 1 others (None: leave HIP's default of 4).  Never 3:
-    5 processes with 3 queues each ran time-sliced (the 5-rank host sweep took
-    19 s instead of 11 s) and in about every second run a one-shot hand-off
-    never arrived (its flag kept the previous launch's number), while 5 x 2,
-    5 x 4, 4 x 3 and 3 x 3 queues never showed it (profiles/r04/queues/;
-    every lost hand-off was in an int8 kernel at one wave per SIMD, and after
-    the byte folds shrank 5 x 3 passed 3 of 3 runs); the cause was not
-    found, so 5 ranks per GPU get 2."""
+    ranks_per_gpu - 1 others (None: leave HIP's default of 4).  (5 processes x
+    3 queues once lost a one-shot hand-off in about every second run — always
+    in an int8 kernel that then ran one wave per SIMD; since the byte folds
+    shrank 5 x 3 passed 13 of 13 runs, profiles/r04/queues/.)"""
     if ranks_per_gpu * 4 <= QUEUE_BUDGET:
         return None
-    q = max(1, QUEUE_BUDGET // ranks_per_gpu)
-    return 2 if q == 3 else q
+    return max(1, QUEUE_BUDGET // ranks_per_gpu)
 
 
 def queues_over_budget(current, q):
