@@ -70,8 +70,11 @@ def parse():
 
 
 def load_traffic(kernel_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None).
+    The summary lives at the top of the tree (traffic.json), not under
+    profiles/, which .gpurunignore keeps off the GPU box (the
+    round-4 bench line's traffic was null for that reason)."""
+    path = os.path.join(ROOT, "traffic.json")
     try:
         with open(path) as f:
             return json.load(f).get(kernel_key)
@@ -948,7 +951,7 @@ def main():
                   "frac": round(ach / HBM_PEAK_GBPS, 4)}
             # rank 0's own L2-to-memory bytes (rocprofv3 PMC, FETCH_SIZE x 2 +
             # WRITE_SIZE, the other ranks unprofiled: tools/pmc_rank0.sh),
-            # committed per (schedule, dtype, n, S) in profiles/traffic.json
+            # committed per (schedule, dtype, n, S) in traffic.json
             tr = load_traffic("%s_%s_n%d_%d" % (algo_name, DT_SHORT[args.dtype], world, S))
             hb["traffic_per_rank"] = tr
             hb["traffic_over_model"] = round(tr / (hm["read"] + hm["write"]), 4) if tr else None

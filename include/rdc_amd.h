@@ -224,6 +224,15 @@ int RdcCommProbe(void* comm, int mode, size_t bytes, int reps, void* stream, dou
  * the reference's schedule has no such knobs; bench.py sweeps them at N>1. */
 int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t tile_bytes);
 
+/* Debug mode (RDC_POISON_SCRATCH; every rank of `comm` should pass the same
+ * value, though ranks that differ stay correct): with on != 0 every consumer
+ * of a hand-off overwrites the scratch range it finished reading with 0xFF
+ * bytes before the signal that lets the producer reuse it, so a read of a
+ * range before its producer's next publish lands NaN / all-ones words instead
+ * of a plausible older value.  Results are unchanged; each launch stores its
+ * consumed scratch bytes once more.  No reference counterpart. */
+int RdcCommSetPoison(void* comm, int on);
+
 /* Autotune (collective: every rank of `comm`, same arguments, no collective in
  * flight; blocks the host): time the ring, the mesh pushed and pulled (RDC_ALGO_MESH_PULL) and
  * (where it fits half a

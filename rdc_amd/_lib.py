@@ -63,6 +63,7 @@ def _load():
         "RdcCommProbe": (i, [vp, i, sz, i, vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]),
         "RdcCommTraceNext": (i, [vp, vp, sz]),
         "RdcCommTune": (i, [vp, i, i, i, sz]),
+        "RdcCommSetPoison": (i, [vp, i]),
         "RdcCommAutotune": (i, [vp, sz, i, i, vp, vp, i, ctypes.POINTER(i), ctypes.POINTER(i)]),
         "RdcCommLastLaunch": (i, [vp, ctypes.POINTER(u64)]),
         "RdcCommLaunchCounter": (i, [vp, ctypes.POINTER(u64)]),

@@ -194,6 +194,12 @@ class Comm(object):
         rank must pass the same values.  Results stay bit-identical."""
         check_call(_LIB.RdcCommTune(self.handle, int(mesh_s16), int(mesh_r16), int(max_blocks), int(tile_bytes)))
 
+    def set_poison(self, on=True):
+        """Debug mode (RdcCommSetPoison, RDC_POISON_SCRATCH): consumers overwrite
+        every scratch range they finished reading with 0xFF bytes, so a read
+        before the producer's next publish lands NaN / all-ones words."""
+        check_call(_LIB.RdcCommSetPoison(self.handle, 1 if on else 0))
+
     def autotune(self, nbytes, dtype=None, reps=3, stream=None):
         """Collective (every rank, same arguments): time the ring, the mesh and
         (where it fits) the one-shot, then the launch shapes of the fastest for allreduces of `nbytes`

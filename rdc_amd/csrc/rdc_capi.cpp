@@ -103,6 +103,7 @@ void set_param(Manager& m, const char* name, const char* val) {
         m.cfg.mesh_split.r16 = r;
     }
     else if (k == "RDC_FUSE_BYTES_DIRECT") m.cfg.fuse_bytes_direct = std::max<size_t>(parse_unit(val), 1);
+    else if (k == "RDC_POISON_SCRATCH") m.cfg.poison = atoi(val) != 0 ? 1 : 0;
     else if (k == "RDC_P2P_SLOT_BYTES") m.cfg.p2p_slot_bytes = std::max<size_t>(parse_unit(val) / 4096 * 4096, 4096);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
     // to subsystems outside the device path and are accepted silently
@@ -214,7 +215,8 @@ int RdcInit(int argc, char** argv) {
                                      "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_TIMEOUT",
                                      "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES",
                                      "RDC_P2P_SLOT_BYTES", "RDC_COALESCE_FUSED", "RDC_HOST_ZC_BYTES",
-                                     "RDC_FUSE_BYTES_DIRECT", "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT"};
+                                     "RDC_FUSE_BYTES_DIRECT", "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT",
+                                     "RDC_POISON_SCRATCH"};
         for (const char* k : keys) env_param(m, k);
         m.env_loaded = true;
         for (int i = 0; i < argc; ++i) {
@@ -566,6 +568,10 @@ int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t t
     return guard([&] { as_comm(comm)->Tune(mesh_s16, mesh_r16, max_blocks, tile_bytes); });
 }
 
+int RdcCommSetPoison(void* comm, int on) {
+    return guard([&] { as_comm(comm)->SetPoison(on != 0); });
+}
+
 int RdcCommAutotune(void* comm, size_t bytes, int dtype, int reps, void* stream, RdcTuneCand* cand, int max_cand,
                     int* ncand, int* best) {
     return guard([&] {
@@ -645,7 +651,8 @@ int RdcCommInitAll(void** comms, int n, const int* devices, size_t scratch_bytes
         static const char* keys[] = {"RDC_SCRATCH_BYTES", "RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES",
                                      "RDC_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES", "RDC_P2P_SLOT_BYTES",
                                      "RDC_COALESCE_FUSED", "RDC_FUSE_BYTES_DIRECT",
-                                     "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "rdc_reduce_ring_mincount"};
+                                     "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT", "rdc_reduce_ring_mincount",
+                                     "RDC_POISON_SCRATCH"};
         if (!m.inited && !m.env_loaded) {
             for (const char* k : keys) env_param(m, k);
             m.env_loaded = true;

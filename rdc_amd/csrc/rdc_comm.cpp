@@ -900,7 +900,8 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     a->timeout_ticks = (uint64_t)(cfg_.timeout_s * (double)wall_khz_ * 1000.0);
     a->uc = (alloc_kind_ == 0 && !strict_fences()) ? 1 : 0;
     static const bool seq_check = getenv("RDC_SEQ_CHECK") && atoi(getenv("RDC_SEQ_CHECK")) != 0;
-    a->expect = seq_check ? (uint64_t)seq_ + 1 : 0;  // the launch about to be issued (one communicator per channel)
+    a->seq_check = seq_check ? 1 : 0;  // device-side: blocks of one launch agree (graph replays included)
+    a->poison = cfg_.poison;
 }
 
 Layout Communicator::layout() const {
@@ -1740,7 +1741,8 @@ void Communicator::RaiseIfError(uint32_t e) const {
         static const char* names[] = {"none", "reduce-scatter wait timed out", "allgather wait timed out",
                                       "broadcast wait timed out", "ring step wait timed out",
                                       "allgather (buffers) wait timed out",
-                                      "a peer's hand-off belongs to another communicator's collective"};
+                                      "a peer's hand-off belongs to another communicator's collective",
+                                      "blocks of one launch read different launch numbers (RDC_SEQ_CHECK)"};
         if (e == RDC_KERR_ORDER)
             throw std::runtime_error(std::string("rdc: device collective failed on rank ") + std::to_string(rank_) +
                                      ": " + names[e] +
@@ -1771,15 +1773,15 @@ void Communicator::RaiseIfError(uint32_t e) const {
             uint64_t d[3];
             memcpy(d, diag + 2, sizeof(d));
             char buf[160];
-            snprintf(buf, sizeof(buf), "; a block of launch %llu read launch number %llu (block %llu of %llu)",
-                     (unsigned long long)d[1], (unsigned long long)d[0], (unsigned long long)(d[2] & 0xffffffffu),
-                     (unsigned long long)(d[2] >> 32));
+            snprintf(buf, sizeof(buf), "; the launch's first block read launch number %llu, block %llu of %llu read %llu",
+                     (unsigned long long)d[1], (unsigned long long)(d[2] & 0xffffffffu),
+                     (unsigned long long)(d[2] >> 32), (unsigned long long)d[0]);
             waited += buf;
         } else {
             (void)hipGetLastError();
         }
         throw std::runtime_error(std::string("rdc: device collective failed on rank ") + std::to_string(rank_) +
-                                 ": " + (e < 7 ? names[e] : "unknown") +
+                                 ": " + (e < 8 ? names[e] : "unknown") +
                                  " (a peer did not join the collective; communicator is now unusable; this "
                                  "rank's last launch: " + (al < 6 ? algos[al] : "?") + ", grid " +
                                  std::to_string(last_launch_[0]) + ", tile " + std::to_string(last_launch_[4]) +

@@ -42,6 +42,9 @@ struct CommConfig {
     // byte): allreduces of at most this many bytes take the reference's tree
     // order instead of the ring's (communicator_collective.cc:6-13)
     size_t ring_mincount = 1;
+    // RDC_POISON_SCRATCH=1: consumers overwrite every scratch range they
+    // finished reading with 0xFF bytes (debug mode, rdc_device.h block_poison)
+    int poison = 0;
 };
 
 struct KernelSet;
@@ -170,6 +173,7 @@ public:
     // mesh role split in sixteenths (s16 + r16 <= 15), grid (0 = auto), tile
     // bytes (0 = auto).  Throws std::invalid_argument on a bad split.
     void Tune(int s16, int r16, int max_blocks, size_t tile_bytes);
+    void SetPoison(bool on) { cfg_.poison = on ? 1 : 0; }
 
     // Collective (every rank, same arguments, no collective in flight): time
     // the schedules (ring, mesh, one-shot where it fits) and then the launch

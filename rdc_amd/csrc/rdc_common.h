@@ -55,7 +55,9 @@ enum {
     // a peer's hand-off carried this launch's sequence number but another
     // communicator's tag: ranks issued the collectives of communicators that
     // share a channel in different orders (rdc_device.h kTagBits)
-    RDC_KERR_ORDER = 6
+    RDC_KERR_ORDER = 6,
+    // RDC_SEQ_CHECK: two blocks of one launch read different launch numbers
+    RDC_KERR_SEQ = 7
 };
 
 static inline size_t rdc_dtype_size(int dtype) {
@@ -118,8 +120,11 @@ struct CollArgs {
     int uc;                              // 1: every scratch region is uncached (hand-offs need no L2
                                          //   write-back, rdc_device.h block_publish)
     uint64_t* trace;                     // optional (mesh/ring): per block {start, end} wall_clock64 ticks
-    uint64_t expect;                     // RDC_SEQ_CHECK: the launch number the host issued (diagnostics;
-                                         //   a block that reads another one records it, err words 72..)
+    int seq_check;                       // RDC_SEQ_CHECK: every block checks it read the launch number the
+                                         //   launch's first block read (err words 80-81; a mismatch is
+                                         //   recorded in err words 72..79)
+    int poison;                          // RDC_POISON_SCRATCH: consumers overwrite scratch ranges they
+                                         //   finished reading with 0xFF (rdc_device.h block_poison)
 };
 
 // ------------------------------------------------ small-allreduce service --

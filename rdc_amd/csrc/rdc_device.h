@@ -389,17 +389,32 @@ __device__ __forceinline__ bool block_wait(uint64_t* const* flags, int nflags, u
 // only the <16-byte head/tail goes element-wise.  A rank whose pointer is
 // not 16-B aligned takes the narrow path (units of the widest common
 // alignment), still exact.
+//
+// Where a block_copy reads: this rank's own bytes (user buffers, kSrcLocal:
+// streaming `nt` loads) or bytes another rank handed off through scratch
+// (kSrcHandoff: `sc0 sc1` loads, ld16_sys / ld_sys) — every load of a
+// handed-off byte is a system-scope load, so the consumer side of every
+// hand-off is the "sc0 sc1 stores and loads both sides" form of
+// MI355X_MICROARCH.md ("Valid forms") whatever memory type backs the scratch
+// or its IPC import.
+enum { kSrcLocal = 0, kSrcHandoff = 1 };
 
 template <int DST, typename W>
 __device__ __forceinline__ void put_word(W* p, W v) {
     if (DST == kDstPeer) st_wt(p, v);
     else *p = v;
 }
+template <int SRC, typename W>
+__device__ __forceinline__ W get_word(const W* p) {
+    if (SRC == kSrcHandoff) return ld_sys(p);
+    return *p;
+}
 
 // dst[i] = src[i], dst and src congruent mod 16.  The 16-B body walks windows
 // of U x blockDim vectors; the window base is wave-uniform, so a peer
-// destination gets one buffer descriptor per window (offsets < 4 GiB).
-template <int DST>
+// destination or a handed-off source gets one buffer descriptor per window
+// (offsets < 4 GiB).
+template <int DST, int SRC>
 __device__ __forceinline__ void block_copy_vec(char* __restrict__ dst, const char* __restrict__ src,
                                                uint64_t len) {
     const uint64_t mis = (uint64_t)(uintptr_t)src & 15;
@@ -408,18 +423,25 @@ __device__ __forceinline__ void block_copy_vec(char* __restrict__ dst, const cha
     const uint64_t nvec = (len - head) >> 4;
     const uint64_t tail_start = head + (nvec << 4);
     const unsigned tid = threadIdx.x;
-    if (tid < head) put_word<DST, char>(dst + tid, src[tid]);
-    if (tid < len - tail_start) put_word<DST, char>(dst + tail_start + tid, src[tail_start + tid]);
+    if (tid < head) put_word<DST, char>(dst + tid, (char)get_word<SRC, uint8_t>(reinterpret_cast<const uint8_t*>(src) + tid));
+    if (tid < len - tail_start)
+        put_word<DST, char>(dst + tail_start + tid,
+                            (char)get_word<SRC, uint8_t>(reinterpret_cast<const uint8_t*>(src) + tail_start + tid));
     const v4u* s = reinterpret_cast<const v4u*>(src + head);
     v4u* d = reinterpret_cast<v4u*>(dst + head);
     constexpr int U = 8;  // 32 KiB in flight per 256-thread block
     const uint64_t step = (uint64_t)blockDim.x;
     for (uint64_t ib = 0; ib < nvec; ib += U * step) {
         const uint64_t i = ib + tid;
+        const __amdgpu_buffer_rsrc_t rsrc_s = wt_rsrc(SRC == kSrcHandoff ? s + ib : s);  // dead for kSrcLocal
+        auto load = [&](int u) -> v4u {
+            if (SRC == kSrcHandoff) return ld16_sys(rsrc_s, (uint32_t)((tid + u * step) * 16));
+            return ld16_nt(s + i + u * step);
+        };
         if (ib + U * step <= nvec) {
             v4u v[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = ld16_nt(s + i + u * step);
+            for (int u = 0; u < U; ++u) v[u] = load(u);
             if (DST == kDstPeer) {
                 const __amdgpu_buffer_rsrc_t rs = wt_rsrc(d + ib);
 #pragma unroll
@@ -432,7 +454,7 @@ __device__ __forceinline__ void block_copy_vec(char* __restrict__ dst, const cha
             const __amdgpu_buffer_rsrc_t rs = wt_rsrc(d + ib);
             for (int u = 0; u < U; ++u) {
                 if (i + u * step >= nvec) break;
-                const v4u v = ld16_nt(s + i + u * step);
+                const v4u v = load(u);
                 if (DST == kDstPeer) st16_wt(rs, (uint32_t)((tid + u * step) * 16), v);
                 else st16_nt(d + i + u * step, v);
             }
@@ -440,7 +462,7 @@ __device__ __forceinline__ void block_copy_vec(char* __restrict__ dst, const cha
     }
 }
 
-template <int DST, typename W>
+template <int DST, int SRC, typename W>
 __device__ __forceinline__ void block_copy_words(char* dst, const char* src, uint64_t len) {
     const uint64_t mis = (uint64_t)(uintptr_t)src & (sizeof(W) - 1);
     uint64_t head = mis ? sizeof(W) - mis : 0;
@@ -448,80 +470,56 @@ __device__ __forceinline__ void block_copy_words(char* dst, const char* src, uin
     const uint64_t nw = (len - head) / sizeof(W);
     const uint64_t tail_start = head + nw * sizeof(W);
     const unsigned tid = threadIdx.x;
-    if (tid < head) put_word<DST, char>(dst + tid, src[tid]);
-    if (tid < len - tail_start) put_word<DST, char>(dst + tail_start + tid, src[tail_start + tid]);
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(src);
+    if (tid < head) put_word<DST, char>(dst + tid, (char)get_word<SRC, uint8_t>(sb + tid));
+    if (tid < len - tail_start) put_word<DST, char>(dst + tail_start + tid, (char)get_word<SRC, uint8_t>(sb + tail_start + tid));
     const W* s = reinterpret_cast<const W*>(src + head);
     W* d = reinterpret_cast<W*>(dst + head);
-    for (uint64_t i = tid; i < nw; i += blockDim.x) put_word<DST, W>(d + i, s[i]);
+    for (uint64_t i = tid; i < nw; i += blockDim.x) put_word<DST, W>(d + i, get_word<SRC, W>(s + i));
 }
 
-// DST: kDstLocal (this GPU's memory) or kDstPeer (a peer's IPC-mapped scratch)
-template <int DST>
+// DST: kDstLocal (this GPU's memory) or kDstPeer (a peer's IPC-mapped scratch);
+// SRC: kSrcLocal (this rank's bytes) or kSrcHandoff (bytes a peer handed off)
+template <int DST, int SRC = kSrcLocal>
 __device__ __forceinline__ void block_copy(char* __restrict__ dst, const char* __restrict__ src, uint64_t len) {
     const uintptr_t x = ((uintptr_t)dst ^ (uintptr_t)src) & 15;
-    if (x == 0) block_copy_vec<DST>(dst, src, len);
-    else if ((x & 7) == 0) block_copy_words<DST, uint64_t>(dst, src, len);
-    else if ((x & 3) == 0) block_copy_words<DST, uint32_t>(dst, src, len);
-    else if ((x & 1) == 0) block_copy_words<DST, uint16_t>(dst, src, len);
-    else block_copy_words<DST, uint8_t>(dst, src, len);
+    if (x == 0) block_copy_vec<DST, SRC>(dst, src, len);
+    else if ((x & 7) == 0) block_copy_words<DST, SRC, uint64_t>(dst, src, len);
+    else if ((x & 3) == 0) block_copy_words<DST, SRC, uint32_t>(dst, src, len);
+    else if ((x & 1) == 0) block_copy_words<DST, SRC, uint16_t>(dst, src, len);
+    else block_copy_words<DST, SRC, uint8_t>(dst, src, len);
 }
 
-// dst (this GPU's memory) = src (a PEER's scratch), every load at system
-// scope (ld16_sys / ld_sys): the pull-mode mesh's gather.  Congruent mod 16:
-// 16-B lanes through one descriptor per window of U x blockDim vectors (8 KiB
-// x U in flight per 256-thread block); otherwise the widest common word.
-template <typename W>
-__device__ __forceinline__ void block_pull_words(char* dst, const char* src, uint64_t len) {
-    const uint64_t mis = (uint64_t)(uintptr_t)src & (sizeof(W) - 1);
-    uint64_t head = mis ? sizeof(W) - mis : 0;
-    if (head > len) head = len;
-    const uint64_t nw = (len - head) / sizeof(W);
-    const uint64_t tail_start = head + nw * sizeof(W);
-    const unsigned tid = threadIdx.x;
-    if (tid < head) dst[tid] = (char)ld_sys(reinterpret_cast<const uint8_t*>(src) + tid);
-    if (tid < len - tail_start)
-        dst[tail_start + tid] = (char)ld_sys(reinterpret_cast<const uint8_t*>(src) + tail_start + tid);
-    const W* s = reinterpret_cast<const W*>(src + head);
-    W* d = reinterpret_cast<W*>(dst + head);
-    for (uint64_t i = tid; i < nw; i += blockDim.x) d[i] = ld_sys(s + i);
-}
-
+// dst (this GPU's memory) = src (a PEER's scratch or this rank's own scratch
+// written by a peer), every load at system scope: landing handed-off bytes.
 __device__ __forceinline__ void block_copy_pull(char* __restrict__ dst, const char* __restrict__ src, uint64_t len) {
-    const uintptr_t x = ((uintptr_t)dst ^ (uintptr_t)src) & 15;
-    if (x != 0) {
-        if ((x & 7) == 0) block_pull_words<uint64_t>(dst, src, len);
-        else if ((x & 3) == 0) block_pull_words<uint32_t>(dst, src, len);
-        else if ((x & 1) == 0) block_pull_words<uint16_t>(dst, src, len);
-        else block_pull_words<uint8_t>(dst, src, len);
-        return;
-    }
-    const uint64_t mis = (uint64_t)(uintptr_t)src & 15;
-    uint64_t head = mis ? (16 - mis) : 0;
+    block_copy<kDstLocal, kSrcHandoff>(dst, src, len);
+}
+
+// ------------------------------------------------------------ poison mode ----
+// RDC_POISON_SCRATCH=1 (CollArgs::poison): after its last read of a scratch
+// range in a launch, the consumer overwrites it with 0xFF bytes (write-through:
+// the range may be a peer's), before the signal that lets the producer reuse
+// it.  A read of the range before the producer's next publish then folds or
+// lands NaN / all-ones words instead of a plausible older value (DESIGN.md
+// §4.2, debug mode; the tests run with it on).
+__device__ __forceinline__ void block_poison(char* p, uint64_t len) {
+    const uint64_t mis = (uint64_t)(uintptr_t)p & 15;
+    uint64_t head = mis ? 16 - mis : 0;
     if (head > len) head = len;
     const uint64_t nvec = (len - head) >> 4;
-    const uint64_t tail_start = head + (nvec << 4);
+    const uint64_t tail = head + (nvec << 4);
     const unsigned tid = threadIdx.x;
-    if (tid < head) dst[tid] = (char)ld_sys(reinterpret_cast<const uint8_t*>(src) + tid);
-    if (tid < len - tail_start)
-        dst[tail_start + tid] = (char)ld_sys(reinterpret_cast<const uint8_t*>(src) + tail_start + tid);
-    const v4u* s = reinterpret_cast<const v4u*>(src + head);
-    v4u* d = reinterpret_cast<v4u*>(dst + head);
-    constexpr int U = 8;
+    if (tid < head) st_wt<uint8_t>(reinterpret_cast<uint8_t*>(p) + tid, 0xff);
+    if (tid < len - tail) st_wt<uint8_t>(reinterpret_cast<uint8_t*>(p) + tail + tid, 0xff);
+    const v4u ones = {~0u, ~0u, ~0u, ~0u};
     const uint64_t step = (uint64_t)blockDim.x;
+    constexpr int U = 8;
     for (uint64_t ib = 0; ib < nvec; ib += U * step) {
-        const __amdgpu_buffer_rsrc_t rs = wt_rsrc(s + ib);
-        const uint64_t i = ib + tid;
-        if (ib + U * step <= nvec) {
-            v4u v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = ld16_sys(rs, (uint32_t)((tid + u * step) * 16));
-#pragma unroll
-            for (int u = 0; u < U; ++u) st16_nt(d + i + u * step, v[u]);
-        } else {
-            for (int u = 0; u < U; ++u) {
-                if (i + u * step >= nvec) break;
-                st16_nt(d + i + u * step, ld16_sys(rs, (uint32_t)((tid + u * step) * 16)));
-            }
+        const __amdgpu_buffer_rsrc_t rs = wt_rsrc(p + head + ib * 16);
+        for (int u = 0; u < U; ++u) {
+            if (ib + tid + u * step >= nvec) break;
+            st16_wt(rs, (uint32_t)((tid + u * step) * 16), ones);
         }
     }
 }

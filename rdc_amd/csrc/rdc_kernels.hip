@@ -57,8 +57,10 @@ __device__ void allgather_body(const CollArgs& a, uint64_t seq) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[c] - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-        block_copy<kDstLocal>(a.cbuf[c] + a.off[c] + toff, a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c] + toff, tlen);
+        char* land = a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c] + toff;
+        block_copy_pull(a.cbuf[c] + a.off[c] + toff, land, tlen);
         __syncthreads();
+        if (a.poison) block_poison(land, tlen);  // writers gate on this rank's done word
     }
 }
 

@@ -58,15 +58,30 @@ __device__ __forceinline__ bool launch_begin(const CollArgs& a, uint64_t* seq) {
         const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_done = done;
         s_failed = e != 0;
-        if (a.expect != 0 && done + 1ull != a.expect) {  // RDC_SEQ_CHECK diagnostics
-            uint32_t expected = 0;
-            if (__hip_atomic_compare_exchange_strong(a.err + 72, &expected, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)) {
-                uint64_t* d = reinterpret_cast<uint64_t*>(a.err + 74);
-                __hip_atomic_store(d, done + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(d + 1, a.expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(d + 2, (uint64_t)blockIdx.x | ((uint64_t)gridDim.x << 32), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (a.seq_check) {
+            // RDC_SEQ_CHECK: every block of one launch must read the same
+            // launch number.  The first block to start claims the launch's
+            // check word with its number (the launch's last block clears it
+            // in launch_done, after every block has started); a block that
+            // finds another number there records both (err words 72..).
+            // Device-side only, so graph replays are checked like eager launches.
+            unsigned long long want = 0;
+            unsigned long long* chk = reinterpret_cast<unsigned long long*>(a.err + 80);
+            if (!__hip_atomic_compare_exchange_strong(chk, &want, (unsigned long long)(done + 1ull), __ATOMIC_RELAXED,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+                want != done + 1ull) {
+                uint32_t expected = 0;
+                if (__hip_atomic_compare_exchange_strong(a.err + 72, &expected, 1u, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    uint64_t* d = reinterpret_cast<uint64_t*>(a.err + 74);
+                    __hip_atomic_store(d, done + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(d + 1, (uint64_t)want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(d + 2, (uint64_t)blockIdx.x | ((uint64_t)gridDim.x << 32), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+                expected = 0;
+                __hip_atomic_compare_exchange_strong(a.err, &expected, (uint32_t)RDC_KERR_SEQ, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
@@ -151,13 +166,12 @@ template <int OP, typename T>
 __device__ __forceinline__ void mesh_fold_elem(const CollArgs& a, char* own, const char* slot0, uint64_t soff,
                                                uint64_t e) {
     const int n = a.n, r = a.rank, f = a.fold[r];  // the ring order of chunk f
-    int q = (f - 1 + n) % n;
-    T acc = *reinterpret_cast<const T*>((q == r ? (const char*)own : slot0 + q * a.slot_bytes) + e);
-    for (int k = 2; k <= n; ++k) {
-        q = (f - k + n) % n;
-        const T v = *reinterpret_cast<const T*>((q == r ? (const char*)own : slot0 + q * a.slot_bytes) + e);
-        acc = OpF<OP>::apply(v, acc);
-    }
+    // own values are this rank's; every other rank's came through its RS slot
+    auto val = [&](int q) -> T {
+        return q == r ? *reinterpret_cast<const T*>(own + e) : ld_elem_sys<T>(slot0 + q * a.slot_bytes + e);
+    };
+    T acc = val((f - 1 + n) % n);
+    for (int k = 2; k <= n; ++k) acc = OpF<OP>::apply(val((f - k + n) % n), acc);
     *reinterpret_cast<T*>(own + e) = acc;
     for (int p = 0; p < n; ++p)
         if (p != r) st_elem_wt<T>(a.ag[p] + soff + e, acc);
@@ -207,10 +221,16 @@ __device__ __forceinline__ void mesh_reduce_range(const CollArgs& a, char* own, 
         for (int k = 1; k <= NMAX; ++k) {
             if (k <= n) {  // (a `break` here stops full unrolling: v would live in scratch)
                 const int q = (f - k + n) % n;  // k-th value in ring order: x[f-1], x[f-2], ..., x[f]
-                const char* src = (q == r ? (const char*)own : slot0 + q * a.slot_bytes) + head;
+                if (q == r) {
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (live[u]) v[u][k - 1] = ld16_nt(src + (i + u * stride) * 16);
+                    for (int u = 0; u < U; ++u)
+                        if (live[u]) v[u][k - 1] = ld16_nt(own + head + (i + u * stride) * 16);
+                } else {  // rank q's handed-off copy: system-scope loads (rdc_device.h kSrcHandoff)
+                    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(slot0 + q * a.slot_bytes + head + ib * 16);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (live[u]) v[u][k - 1] = ld16_sys(rs, (uint32_t)((tid + u * stride) * 16));
+                }
             }
         }
 #pragma unroll
@@ -344,6 +364,11 @@ __device__ __forceinline__ void mesh_body(const CollArgs& a, uint64_t seq) {
                 });
             else
                 mesh_reduce_tile<OP, T, NMAX>(a, t, tlen);
+            if (a.poison) {  // every peer's copy of this tile was read: before the result's publish
+                __syncthreads();
+                for (int k = 1; k < n; ++k)
+                    block_poison(a.rs[r] + (uint64_t)((r + k) % n) * a.slot_bytes + a.mis[r] + toff, tlen);
+            }
             if (threadIdx.x < (unsigned)(n - 1)) {
                 const int p = (r + 1 + threadIdx.x) % n;
                 s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
@@ -366,13 +391,19 @@ __device__ __forceinline__ void mesh_body(const CollArgs& a, uint64_t seq) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[c] - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-        const char* src = a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c];
+        char* src = a.ag[r] + (uint64_t)c * a.slot_bytes + a.mis[c];
         if (a.units)
             for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
-                block_copy<kDstLocal>(usr, src + (p - a.off[c]), l);
+                block_copy_pull(usr, src + (p - a.off[c]), l);
             });
         else
-            block_copy<kDstLocal>(a.user + a.off[c] + toff, src + toff, tlen);
+            block_copy_pull(a.user + a.off[c] + toff, src + toff, tlen);
+        // owner c rewrites this slot only in its next launch, after this
+        // rank's next scatter: after this kernel's end
+        if (a.poison) {
+            __syncthreads();
+            block_poison(src + toff, tlen);
+        }
     }
 }
 
@@ -519,6 +550,11 @@ __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) 
                 __syncthreads();
                 pull_fold_range<OP, T, NMAX>(a, a.user + a.off[r] + toff, s_src, a.ag[r] + slot_r + co, tlen);
             }
+            if (a.poison) {  // peer q restages its slot r only after gathering this tile's result
+                __syncthreads();
+                for (int k = 1; k < n; ++k)
+                    block_poison(a.rs[(r + k) % n] + slot_r + a.mis[r] + toff, tlen);
+            }
             if (threadIdx.x < (unsigned)(n - 1)) {
                 const int p = (r + 1 + threadIdx.x) % n;
                 s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
@@ -555,10 +591,16 @@ __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) 
 // ======================================================= ring allreduce ===
 // own[i] = OP(own[i], recv[i]) — reducer(src=reducebuf, dst=sendrecvbuf)
 // (communicator_collective.cc:174-176), element-wise head/tail + 16-B body.
+// recv is this rank's RS slot, written by the next rank: system-scope loads.
 template <int OP, typename T>
 __device__ void block_reduce_into(char* own, const char* recv, uint64_t len) {
+    const unsigned tid = threadIdx.x;
+    auto fold_elem = [&](uint64_t e) {
+        T* d = reinterpret_cast<T*>(own + e);
+        *d = OpF<OP>::apply(*d, ld_elem_sys<T>(recv + e));
+    };
     if ((((uintptr_t)own ^ (uintptr_t)recv) & 15) != 0) {  // buffer not 16-B aligned: element-wise
-        reduce_elems<OP, T>(own, recv, len / sizeof(T), threadIdx.x, kBlock);
+        for (uint64_t e = (uint64_t)tid * sizeof(T); e < len; e += (uint64_t)kBlock * sizeof(T)) fold_elem(e);
         return;
     }
     const uint64_t mis16 = (uint64_t)(uintptr_t)own & 15;
@@ -566,29 +608,29 @@ __device__ void block_reduce_into(char* own, const char* recv, uint64_t len) {
     if (head > len) head = len;
     const uint64_t nvec = (len - head) >> 4;
     const uint64_t tail = head + (nvec << 4);
-    const unsigned tid = threadIdx.x;
-    if (tid < head / sizeof(T)) {
-        T* d = reinterpret_cast<T*>(own) + tid;
-        *d = OpF<OP>::apply(*d, reinterpret_cast<const T*>(recv)[tid]);
-    }
-    if (tid < (len - tail) / sizeof(T)) {
-        T* d = reinterpret_cast<T*>(own + tail) + tid;
-        *d = OpF<OP>::apply(*d, reinterpret_cast<const T*>(recv + tail)[tid]);
-    }
+    if (tid < head / sizeof(T)) fold_elem(tid * sizeof(T));
+    if (tid < (len - tail) / sizeof(T)) fold_elem(tail + tid * sizeof(T));
     v4u* d = reinterpret_cast<v4u*>(own + head);
-    const v4u* s = reinterpret_cast<const v4u*>(recv + head);
     constexpr int U = 4;
-    uint64_t i = tid;
-    for (; i + (U - 1) * kBlock < nvec; i += U * kBlock) {
-        v4u x[U], y[U];
+    for (uint64_t ib = 0; ib < nvec; ib += U * kBlock) {
+        const __amdgpu_buffer_rsrc_t rs = wt_rsrc(recv + head + ib * 16);
+        const uint64_t i = ib + tid;
+        if (ib + U * kBlock <= nvec) {
+            v4u x[U], y[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = ld16(d + i + u * kBlock);
+            for (int u = 0; u < U; ++u) x[u] = ld16(d + i + u * kBlock);
 #pragma unroll
-        for (int u = 0; u < U; ++u) y[u] = ld16_nt(s + i + u * kBlock);
+            for (int u = 0; u < U; ++u) y[u] = ld16_sys(rs, (uint32_t)((tid + u * kBlock) * 16));
 #pragma unroll
-        for (int u = 0; u < U; ++u) st16(d + i + u * kBlock, reduce16<OP, T>(x[u], y[u]));
+            for (int u = 0; u < U; ++u) st16(d + i + u * kBlock, reduce16<OP, T>(x[u], y[u]));
+        } else {
+            for (int u = 0; u < U; ++u) {
+                if (i + u * kBlock >= nvec) break;
+                st16(d + i + u * kBlock,
+                     reduce16<OP, T>(ld16(d + i + u * kBlock), ld16_sys(rs, (uint32_t)((tid + u * kBlock) * 16))));
+            }
+        }
     }
-    for (; i < nvec; i += kBlock) st16(d + i, reduce16<OP, T>(ld16(d + i), ld16_nt(s + i)));
 }
 
 // Chunk c's user bytes [off[c] + toff, + tlen) as (user pointer, offset from
@@ -666,11 +708,12 @@ __device__ void ring_body(const CollArgs& a, uint64_t seq) {
                 if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING, a.uc)) return;
                 uint64_t tlen = a.len[cr] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                const char* src = a.rs[r] + (uint64_t)j * a.slot_bytes + a.mis[cr];
+                char* src = a.rs[r] + (uint64_t)j * a.slot_bytes + a.mis[cr];
                 chunk_pieces(a, cr, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
                     block_reduce_into<OP, T>(usr, src + co, l);
                 }, ucp);
                 __syncthreads();
+                if (a.poison) block_poison(src + toff, tlen);
             }
         }
         // ---- TryAllgatherRing: step j sends chunk (r+j)%n to prev and
@@ -693,11 +736,12 @@ __device__ void ring_body(const CollArgs& a, uint64_t seq) {
                 if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING, a.uc)) return;
                 uint64_t tlen = a.len[cr] - toff;
                 if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-                const char* src = a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr];
+                char* src = a.ag[r] + (uint64_t)j * a.slot_bytes + a.mis[cr];
                 chunk_pieces(a, cr, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
-                    block_copy<kDstLocal>(usr, src + co, l);
+                    block_copy_pull(usr, src + co, l);
                 }, ucp);
                 __syncthreads();
+                if (a.poison) block_poison(src + toff, tlen);
             }
         }
     }
@@ -737,9 +781,13 @@ __device__ void oneshot_fold_range(const FoldView& a, int c, uint64_t lo, uint64
     const char* slots = a.slots;
     const unsigned tid = threadIdx.x;
     auto src = [&](int q) -> const char* { return q == r ? own : slots + (uint64_t)q * a.slot_bytes; };
+    // own values are this rank's; the others were handed off (system-scope loads)
+    auto val = [&](int q, uint64_t x) -> T {
+        return q == r ? *reinterpret_cast<const T*>(own + x) : ld_elem_sys<T>(src(q) + x);
+    };
     auto fold_elem = [&](uint64_t x) {
-        T acc = *reinterpret_cast<const T*>(src((c - 1 + n) % n) + x);
-        for (int k = 2; k <= n; ++k) acc = OpF<OP>::apply(*reinterpret_cast<const T*>(src((c - k + n) % n) + x), acc);
+        T acc = val((c - 1 + n) % n, x);
+        for (int k = 2; k <= n; ++k) acc = OpF<OP>::apply(val((c - k + n) % n, x), acc);
         *reinterpret_cast<T*>(out + x) = acc;
     };
     if (((((uintptr_t)own ^ (uintptr_t)slots) | ((uintptr_t)out ^ (uintptr_t)slots)) & 15) != 0) {  // not 16-B aligned
@@ -756,7 +804,8 @@ __device__ void oneshot_fold_range(const FoldView& a, int c, uint64_t lo, uint64
     }
     constexpr int U = NMAX <= 8 ? 2 : 1;
     const uint64_t nvec = (vhi - vlo) >> 4;
-    for (uint64_t i = tid; i < nvec; i += U * kBlock) {
+    for (uint64_t ib = 0; ib < nvec; ib += U * kBlock) {
+        const uint64_t i = ib + tid;
         v4u v[U][NMAX];
         bool live[U];
 #pragma unroll
@@ -764,10 +813,17 @@ __device__ void oneshot_fold_range(const FoldView& a, int c, uint64_t lo, uint64
 #pragma unroll
         for (int k = 1; k <= NMAX; ++k) {
             if (k <= n) {
-                const char* p = src((c - k + n) % n) + vlo;
+                const int q = (c - k + n) % n;
+                if (q == r) {
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (live[u]) v[u][k - 1] = ld16_nt(p + (i + u * kBlock) * 16);
+                    for (int u = 0; u < U; ++u)
+                        if (live[u]) v[u][k - 1] = ld16_nt(own + vlo + (i + u * kBlock) * 16);
+                } else {
+                    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(src(q) + vlo + ib * 16);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (live[u]) v[u][k - 1] = ld16_sys(rs, (uint32_t)((tid + u * kBlock) * 16));
+                }
             }
         }
 #pragma unroll
@@ -802,7 +858,7 @@ __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
         constexpr int S = 16 / sizeof(T) * kBlock;
 #pragma unroll
         for (int k = 0; k < NMAX; ++k)
-            if (k < n) v[k * S] = *reinterpret_cast<const T*>(src(k) + x);
+            if (k < n) v[k * S] = k == r ? *reinterpret_cast<const T*>(own + x) : ld_elem_sys<T>(src(k) + x);
         for (int i = 0; i < a.tree_len; ++i) {
             const int d = a.tree_dst[i], s = a.tree_src[i];
             v[d * S] = OpF<OP>::apply(v[d * S], v[s * S]);
@@ -823,11 +879,14 @@ __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
     }
     const uint64_t nvec = (vhi - vlo) >> 4;
     v4u* v = s_acc + tid;  // v[q * kBlock]: rank q's vector
-    for (uint64_t i = tid; i < nvec; i += kBlock) {
+    for (uint64_t ib = 0; ib < nvec; ib += kBlock) {
+        const uint64_t i = ib + tid;
+        if (i >= nvec) break;  // the last window (no barrier inside the loop)
         v4u x[NMAX];
 #pragma unroll
         for (int k = 0; k < NMAX; ++k)
-            if (k < n) x[k] = ld16_nt(src(k) + vlo + i * 16);
+            if (k < n) x[k] = k == r ? ld16_nt(own + vlo + i * 16)
+                                     : ld16_sys(wt_rsrc(src(k) + vlo + ib * 16), (uint32_t)(tid * 16));
 #pragma unroll
         for (int k = 0; k < NMAX; ++k)
             if (k < n) v[k * kBlock] = x[k];
@@ -879,6 +938,9 @@ __device__ void oneshot_body(const CollArgs& a, uint64_t seq) {
             }
         }
         __syncthreads();
+        // a peer rewrites this half two launches later, after this kernel's end
+        if (a.poison)
+            for (int k = 1; k < n; ++k) block_poison(a.rs[r] + (uint64_t)((r + k) % n) * a.slot_bytes + half + lo, hi - lo);
     }
 }
 
@@ -939,11 +1001,11 @@ __device__ void bcast_body(const CollArgs& a, uint64_t seq) {
             if (threadIdx.x == 0) s_flags[0] = a.flags[r] + frow;
             __syncthreads();
             if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_BCAST, a.uc)) return;
-            const char* land = a.ag[r] + soff;
+            char* land = a.ag[r] + soff;
             if (split && bcast_forwarder(n, root, t) == r) {
                 for (int k = 1; k < n; ++k) {
                     const int q = (r + k) % n;
-                    if (q != root) block_copy<kDstPeer>(a.ag[q] + soff, land, tlen);
+                    if (q != root) block_copy<kDstPeer, kSrcHandoff>(a.ag[q] + soff, land, tlen);
                 }
                 if (threadIdx.x == 0) {
                     int k = 0;
@@ -952,8 +1014,10 @@ __device__ void bcast_body(const CollArgs& a, uint64_t seq) {
                 }
                 block_publish(s_flags, n - 2, seq, a.uc);  // its barrier orders thread 0's list before use
             }
-            block_copy<kDstLocal>(mine, land, tlen);
+            block_copy_pull(mine, land, tlen);
             __syncthreads();
+            // writers gate on this rank's done word (this kernel's end) before rewriting
+            if (a.poison) block_poison(land, tlen);
         }
     }
 }
@@ -980,11 +1044,16 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint64_t seq) {
         // (small messages run one block)
         const bool last = gridDim.x == 1 || atomicAdd(a.done_ctr, 1u) == gridDim.x - 1;
         if (last) {
-            // every block made its own writes visible (the fence above) before
-            // it arrived, so the last block adds no release fence of its own
-            // (each one is an L2 write-back): the done words say "finished
-            // reading", they publish nothing
             if (gridDim.x > 1) __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (a.seq_check)
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.err + 80), 0ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            // the other blocks' writes reach the host (zero-copy results) or
+            // cached scratch through this block's release, which its acquire
+            // side is the host's read of `notify` (the arrivals are
+            // relaxed agent-scope adds, so without it the host-visible order
+            // would rest on hardware ordering alone)
+            if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int p = 0; p < a.n; ++p)
                 if (p != a.rank) flag_store(done_word(a, p, a.rank), seq);
@@ -1000,7 +1069,7 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint64_t seq) {
                 __hip_atomic_store(a.err_mirror, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            if (a.notify) __hip_atomic_store(a.notify, a.notify_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (a.notify) __hip_atomic_store(a.notify, a.notify_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }

@@ -230,41 +230,106 @@ def test_group_launch_counter_far_past_zeroed_flags(start, algo_counts=((2, 3000
             c.destroy()
 
 
+def launch_counters(comms):
+    import ctypes
+    from rdc_amd._lib import _LIB
+    out = []
+    for c in comms:
+        v = ctypes.c_uint64()
+        assert _LIB.RdcCommLaunchCounter(c.handle, ctypes.byref(v)) == 0, _LIB.RdcGetLastError()
+        out.append(v.value)
+    return out
+
+
+def mismatch_report(got, want, n):
+    """Element ranges where got differs from want, with the Split chunk each
+    starts in (rank 0's own chunk is folded by its reduce role, the others
+    are gathered from their owners)."""
+    bad = np.flatnonzero(np.frombuffer(got.tobytes(), np.uint32) != np.frombuffer(want.tobytes(), np.uint32))
+    if bad.size == 0:
+        return "equal"
+    k, m = divmod(want.size, n)
+    starts = [c * k + min(c, m) for c in range(n)]
+    runs, lo, prev = [], bad[0], bad[0]
+    for i in bad[1:]:
+        if i != prev + 1:
+            runs.append((lo, prev + 1))
+            lo = i
+        prev = i
+    runs.append((lo, prev + 1))
+    return "; ".join("[%d, %d) in chunk %d" % (a, b, max(c for c in range(n) if starts[c] <= a)) for a, b in runs[:6])
+
+
 @pytest.mark.parametrize("algo", ["mesh", "ring", "oneshot", "mesh_pull"])
 def test_group_graph_capture_replay(group2, algo):
     """Launch sequence numbers live on the device, so a captured allreduce
-    replays correctly (graph per rank, several replays with fresh inputs)."""
+    replays correctly (graph per rank, several replays with fresh inputs),
+    and eager launches on the same communicators afterwards stay exact.
+    Runs in poison mode (RdcCommSetPoison): every consumed scratch range is
+    overwritten with 0xFF, so a read ahead of its producer's publish lands
+    NaNs.  Both ranks' device launch counters must agree after the replays
+    (GPUTEST_r04 failed here once: rank 0's own chunk wrong in the eager
+    mesh launch)."""
     import ctypes
     import rdc_amd
     rng = np.random.default_rng(21)
     count = 300007
-    ts = [torch.zeros(count, dtype=torch.float32, device="cuda") for _ in range(2)]
-    graphs = []
-    torch.cuda.synchronize()
-    for r in range(2):
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=group2.streams[r], capture_error_mode="thread_local"):
-            group2[r].allreduce(ts[r], rdc_amd.Op.SUM, algo=algo,
-                                stream=ctypes.c_void_p(group2.streams[r].cuda_stream))
-        graphs.append(g)
-    torch.cuda.synchronize()
-    for it in range(4):
-        xs = [rng.standard_normal(count).astype(np.float32) for _ in range(2)]
-        for r in range(2):
-            ts[r].copy_(torch.from_numpy(xs[r]))
+    for c in group2:
+        c.set_poison(True)
+    try:
+        ts = [torch.zeros(count, dtype=torch.float32, device="cuda") for _ in range(2)]
+        graphs = []
         torch.cuda.synchronize()
         for r in range(2):
-            with torch.cuda.stream(group2.streams[r]):
-                graphs[r].replay()
-        for r in range(2):
-            group2[r].check(ctypes.c_void_p(group2.streams[r].cuda_stream))
-        want = O.expected_allreduce(xs, O.DT_FLOAT32, O.OP_SUM)
-        for r in range(2):
-            assert ts[r].cpu().numpy().tobytes() == want.tobytes(), (algo, it, r)
-    # eager launches interleave with replays on the same communicators
-    xs = [rng.standard_normal(1001).astype(np.float32) for _ in range(2)]
-    got = run_group(group2, xs, O.DT_FLOAT32, O.OP_SUM, 2)
-    assert got[0].tobytes() == O.expected_allreduce(xs, O.DT_FLOAT32, O.OP_SUM).tobytes()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=group2.streams[r], capture_error_mode="thread_local"):
+                group2[r].allreduce(ts[r], rdc_amd.Op.SUM, algo=algo,
+                                    stream=ctypes.c_void_p(group2.streams[r].cuda_stream))
+            graphs.append(g)
+        torch.cuda.synchronize()
+        for it in range(4):
+            xs = [rng.standard_normal(count).astype(np.float32) for _ in range(2)]
+            for r in range(2):
+                ts[r].copy_(torch.from_numpy(xs[r]))
+            torch.cuda.synchronize()
+            for r in range(2):
+                with torch.cuda.stream(group2.streams[r]):
+                    graphs[r].replay()
+            for r in range(2):
+                group2[r].check(ctypes.c_void_p(group2.streams[r].cuda_stream))
+            want = O.expected_allreduce(xs, O.DT_FLOAT32, O.OP_SUM)
+            for r in range(2):
+                got = ts[r].cpu().numpy()
+                assert got.tobytes() == want.tobytes(), (algo, it, r, mismatch_report(got, want, 2))
+        ctr = launch_counters(group2)
+        assert ctr[0] == ctr[1], ("launch counters differ after the replays", ctr)
+        # eager launches interleave with replays on the same communicators
+        for eager_algo in (2, 5, 1, 0):
+            xs = [rng.standard_normal(1001).astype(np.float32) for _ in range(2)]
+            got = run_group(group2, xs, O.DT_FLOAT32, O.OP_SUM, eager_algo)
+            want = O.expected_allreduce(xs, O.DT_FLOAT32, O.OP_SUM)
+            for r in range(2):
+                assert got[r].tobytes() == want.tobytes(), (algo, eager_algo, r, launch_counters(group2),
+                                                            mismatch_report(got[r], want, 2))
+        for it in range(2):  # and replays again after them
+            xs = [rng.standard_normal(count).astype(np.float32) for _ in range(2)]
+            for r in range(2):
+                ts[r].copy_(torch.from_numpy(xs[r]))
+            torch.cuda.synchronize()
+            for r in range(2):
+                with torch.cuda.stream(group2.streams[r]):
+                    graphs[r].replay()
+            for r in range(2):
+                group2[r].check(ctypes.c_void_p(group2.streams[r].cuda_stream))
+            want = O.expected_allreduce(xs, O.DT_FLOAT32, O.OP_SUM)
+            for r in range(2):
+                got = ts[r].cpu().numpy()
+                assert got.tobytes() == want.tobytes(), (algo, "after eager", it, r, mismatch_report(got, want, 2))
+        ctr = launch_counters(group2)
+        assert ctr[0] == ctr[1], ("launch counters differ", ctr)
+    finally:
+        for c in group2:
+            c.set_poison(False)
 
 
 def test_group_broadcast(group3):

@@ -327,3 +327,24 @@ def test_bench_self_launch_forwards_exit_code():
     assert p.returncode != 0
     assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert "torch.distributed" in p.stderr or "ChildFailedError" in p.stderr or "local_rank" in p.stderr, p.stderr[-2000:]
+
+
+def test_bench_traffic_file_reaches_the_gpu_box():
+    """bench.py's roofline.traffic comes from the committed PMC summary
+    (it was null in BENCH_r04 because the summary sat under
+    profiles/, which .gpurunignore keeps off the GPU box).  The file must
+    exist at the path bench.py reads, hold the N = 1 kernel's bytes, and no
+    .gpurunignore pattern may exclude it."""
+    import fnmatch
+    import bench
+    path = os.path.join(ROOT, "traffic.json")
+    assert os.path.exists(path)
+    assert bench.load_traffic("reduce_sum_f32_1073741824") == 3221261312
+    rel = "traffic.json"
+    with open(os.path.join(ROOT, ".gpurunignore")) as f:
+        pats = [ln.strip() for ln in f if ln.strip() and not ln.startswith("#")]
+    for p in pats:
+        anchored = p.startswith("./")
+        q = p[2:] if anchored else p
+        assert not fnmatch.fnmatch(rel, q), (p, "excludes traffic.json from the GPU box")
+        assert not (not anchored and fnmatch.fnmatch(os.path.basename(rel), q)), p

@@ -1,7 +1,7 @@
 """Summarise rocprofv3 PMC passes into HBM bytes per launch.
 
     python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> \
-        <kernel-substring> <key> [profiles/traffic.json]
+        <kernel-substring> <key> [traffic.json]
 
 Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KB;
 on gfx950 FETCH_SIZE reports exactly half the bytes of a wide (16 B/lane)
@@ -29,8 +29,7 @@ def per_launch(path, counter, kern):
 
 def main():
     fetch_csv, write_csv, kern, key = sys.argv[1:5]
-    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles",
-                                                            "traffic.json")
+    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "traffic.json")
     f_kb, nf = per_launch(fetch_csv, "FETCH_SIZE", kern)
     w_kb, nw = per_launch(write_csv, "WRITE_SIZE", kern)
     read_b = 2 * f_kb * 1024      # gfx950: FETCH_SIZE = half the streamed bytes
