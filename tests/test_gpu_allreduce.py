@@ -684,7 +684,7 @@ HOST_SWEEP_BYTES = [
 ]
 
 
-@pytest.mark.parametrize("world,balance", [(2, "0"), (3, "0"), (3, "1"), (4, "1"), (5, "0"), (5, "1")])
+@pytest.mark.parametrize("world,balance", [(2, "0"), (3, "0"), (3, "1"), (4, "1"), (5, "0"), (5, "1"), (5, "diag")])
 def test_mp_host_size_sweep(world, balance):
     """Host buffers at every boundary of the host path (rdc_host.cpp: service,
     copy-pool parts, zero-copy / staged small path, inline piece, pipeline
@@ -693,14 +693,20 @@ def test_mp_host_size_sweep(world, balance):
     did not cover the buffer (bytes % parts left over) once dropped the last
     bytes of a piece: only sizes like these see it.  RDC_HOST_BALANCE=1: the
     pieces' balanced ranges (every rank folds a part of each piece in its
-    chunk's ring order; the default with one rank per GPU)."""
+    chunk's ring order; the default with one rank per GPU).  "diag": 5
+    processes on one GPU at the launcher's queue budget (round 4's lost
+    one-shot hand-off ran here) with poison mode and the device-side launch
+    number check on (RDC_POISON_SCRATCH=1, RDC_SEQ_CHECK=1)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    env = {"RDC_HOST_BALANCE": balance}
+    if balance == "diag":
+        env = {"RDC_HOST_BALANCE": "0", "RDC_POISON_SCRATCH": "1", "RDC_SEQ_CHECK": "1"}
     cases = []
     for k, nb in enumerate(HOST_SWEEP_BYTES):
         cases.append({"count": nb, "dtype": 1, "op": (0, 2)[k % 2], "kind": "host_allreduce", "seed": 0x5EEDA000 + k})
         cases.append({"count": nb // 4 + 1, "dtype": 6, "op": 2, "kind": "host_allreduce", "seed": 0x5EEDB000 + k})
-    tmp = run_mp(world, cases, timeout=400, env_extra={"RDC_HOST_BALANCE": balance})
+    tmp = run_mp(world, cases, timeout=400, env_extra=env)
     for i, c in enumerate(cases):
         want = expected_for(c, world)
         for r in range(world):
