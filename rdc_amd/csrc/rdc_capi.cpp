@@ -363,7 +363,9 @@ void allreduce_sync(Manager& m, Communicator* c, void* sendrecv, size_t count, i
     // host-resident buffer: pieces of every chunk through pinned slots, H2D /
     // allreduce / D2H overlapped on three streams
     if (!m.host) m.host.reset(new HostPath(c->device(), m.host_zc_bytes));
-    m.host->Warm(s);
+    // the copy path comes up only for buffers that use it (the service and
+    // the zero-copy path below HostPath::kSmall never DMA)
+    if (count * rdc_dtype_size(dtype) > HostPath::kSmall) m.host->Warm(s);
     m.host->Allreduce(c, sendrecv, count, dtype, op, s);
 }
 
@@ -891,7 +893,9 @@ int RdcNewBuffer(void** out, void* addr, size_t size, int pinned) {
                 if (m.inited && it != m.comms.end() && it->second->size() > 1) {
                     Communicator* c = it->second.get();
                     if (!m.host) m.host.reset(new HostPath(c->device(), m.host_zc_bytes));
-                    m.host->Warm(manager_stream(m, c->device()));
+                    // the path's own copy streams, not the manager stream
+                    // (which may hold queued collectives: ADVICE r4)
+                    if (size > HostPath::kSmall) m.host->Warm(nullptr);
                 }
             }
         }

@@ -902,6 +902,10 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     static const bool seq_check = getenv("RDC_SEQ_CHECK") && atoi(getenv("RDC_SEQ_CHECK")) != 0;
     a->seq_check = seq_check ? 1 : 0;  // device-side: blocks of one launch agree (graph replays included)
     a->poison = cfg_.poison;
+    static const bool verify = getenv("RDC_VERIFY_PUBLISH") && atoi(getenv("RDC_VERIFY_PUBLISH")) != 0;
+    a->verify = verify ? err_ + 84 : nullptr;
+    static const bool poll_rmw = getenv("RDC_POLL_RMW") && atoi(getenv("RDC_POLL_RMW")) != 0;
+    a->poll_rmw = poll_rmw ? 1 : 0;
 }
 
 Layout Communicator::layout() const {
@@ -943,9 +947,14 @@ int Communicator::mesh_blocks() const { return cfg_.max_blocks > 0 ? cfg_.max_bl
 // for a collective block on its CU.  A grid sized to every CU would then not
 // be co-resident while the service runs (RDC_NBLOCKS / Tune / Autotune can
 // ask for 4 blocks per CU) and its waits would time out.
+// The reservation applies only where a service can run at all: the channel's
+// agreed svc_enabled and ranks per GPU within RDC_HOST_SERVICE_SHARE_MAX (both
+// the same on every rank, so every rank still computes the same grid) —
+// otherwise (RDC_HOST_SERVICE=0, more ranks per GPU) the CUs stay in the
+// grid (8 ranks on one GPU held back 64 of 256 CUs for nothing).
 int Communicator::LaunchGrid(int want, int blocks_per_cu) const {
-    // one CU per rank on the GPU kept for its resident service block (LDS-heavy)
-    return ResidentGrid(want, blocks_per_cu, cus_min_, share_max_, xcds_max_, share_max_);
+    const bool svc = ch_ && ch_->svc_enabled && share_max_ <= SmallService::ShareMax();
+    return ResidentGrid(want, blocks_per_cu, cus_min_, share_max_, xcds_max_, svc ? share_max_ : 0);
 }
 
 void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStream_t stream, int algo) {
@@ -1758,7 +1767,7 @@ void Communicator::RaiseIfError(uint32_t e) const {
         if (err_ && hipMemcpy(diag, err_ + 64, sizeof(diag), hipMemcpyDeviceToHost) == hipSuccess && diag[0] == 1) {
             uint64_t d[3];
             memcpy(d, diag + 2, sizeof(d));
-            const uint64_t at = (d[2] - (uint64_t)(uintptr_t)flags_) / sizeof(uint64_t);
+            const uint64_t at = (d[2] - (uint64_t)(uintptr_t)flags_) / (sizeof(uint64_t) * RDC_FLAG_STRIDE);
             const uint64_t mt = max_tiles_ ? max_tiles_ : 1;
             char buf[200];
             snprintf(buf, sizeof(buf), "; waited for launch %llu (tag %llu) at flag row %llu tile %llu, saw launch %llu "
@@ -1766,8 +1775,56 @@ void Communicator::RaiseIfError(uint32_t e) const {
                      (unsigned long long)(at / mt), (unsigned long long)(at % mt), (unsigned long long)(d[1] >> 8),
                      (unsigned long long)(d[1] & 255));
             waited = buf;
+            uint64_t pr[5] = {0};
+            uint64_t host = 0;
+            if (hipMemcpy(pr, err_ + 96, sizeof(pr), hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(&host, reinterpret_cast<void*>((uintptr_t)d[2]), 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                snprintf(buf, sizeof(buf), " [after giving up, the flag read by the device: load %llu, atomic %llu, "
+                         "after acquire %llu, nt %llu (XCC %llu); by the host: %llu]",
+                         (unsigned long long)(pr[0] >> 8), (unsigned long long)(pr[1] >> 8),
+                         (unsigned long long)(pr[2] >> 8), (unsigned long long)(pr[3] >> 8), (unsigned long long)pr[4],
+                         (unsigned long long)(host >> 8));
+                waited += buf;
+            } else {
+                (void)hipGetLastError();
+            }
         } else {
             (void)hipGetLastError();
+        }
+        if (getenv("RDC_FLAG_DUMP") && atoi(getenv("RDC_FLAG_DUMP")) != 0) {
+            // debug: the reduce-scatter rows as this rank sees them, in its own
+            // flag array (row q: written by rank q) and, through its mappings,
+            // its own row in every peer's array (what it wrote there), as
+            // launch numbers, first 48 tiles; read by the host (hipMemcpy)
+            const uint32_t T = std::min<uint32_t>(max_tiles_, 48);
+            std::vector<uint64_t> w((size_t)T * RDC_FLAG_STRIDE);
+            auto row = [&](const uint64_t* base, int r) {
+                std::string out;
+                if (hipMemcpy(w.data(), base + (uint64_t)r * max_tiles_ * RDC_FLAG_STRIDE, w.size() * 8,
+                              hipMemcpyDeviceToHost) != hipSuccess) {
+                    (void)hipGetLastError();
+                    return std::string("?");
+                }
+                for (uint32_t t = 0; t < T; ++t) out += std::to_string(w[(size_t)t * RDC_FLAG_STRIDE] >> 8) + " ";
+                return out;
+            };
+            std::string d = "; flag dump:";
+            for (int q = 0; q < n_; ++q)
+                if (q != rank_) d += " [own row " + std::to_string(q) + ": " + row(flags_, q) + "]";
+            for (int p = 0; p < n_; ++p)
+                if (p != rank_ && peer_flags_[p])
+                    d += " [rank " + std::to_string(p) + "'s row " + std::to_string(rank_) + ": " +
+                         row(peer_flags_[p], rank_) + "]";
+            waited += d;
+        }
+        uint32_t vr[4] = {0};
+        if (err_ && hipMemcpy(vr, err_ + 84, sizeof(vr), hipMemcpyDeviceToHost) == hipSuccess && vr[0] != 0) {
+            uint64_t va;
+            memcpy(&va, vr + 2, sizeof(va));
+            char buf[160];
+            snprintf(buf, sizeof(buf), "; RDC_VERIFY_PUBLISH: %u flag stores this rank never read back (last at %#llx)",
+                     vr[0], (unsigned long long)va);
+            waited += buf;
         }
         if (err_ && hipMemcpy(diag, err_ + 72, sizeof(diag), hipMemcpyDeviceToHost) == hipSuccess && diag[0] == 1) {
             uint64_t d[3];
@@ -1785,7 +1842,8 @@ void Communicator::RaiseIfError(uint32_t e) const {
                                  " (a peer did not join the collective; communicator is now unusable; this "
                                  "rank's last launch: " + (al < 6 ? algos[al] : "?") + ", grid " +
                                  std::to_string(last_launch_[0]) + ", tile " + std::to_string(last_launch_[4]) +
-                                 " B, launches issued " + std::to_string(seq_) + waited + ")");
+                                 " B, launches issued " + std::to_string(seq_) + ", scratch kind " +
+                                 std::to_string(alloc_kind_) + waited + ")");
     }
 }
 

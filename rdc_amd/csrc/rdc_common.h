@@ -41,6 +41,11 @@ enum { RDC_KIND_NONE = 0, RDC_KIND_MESH = 1, RDC_KIND_RING = 2, RDC_KIND_BCAST =
        RDC_KIND_ONESHOT = 5, RDC_KIND_TREE = 6 };
 
 #define RDC_MAX_RANKS 16
+// 64-bit words from one hand-off flag to the next (CollArgs::flag_stride):
+// 16 = each flag in a 128-B line of its own
+#ifndef RDC_FLAG_STRIDE
+#define RDC_FLAG_STRIDE 16
+#endif
 #define RDC_SLOT_ALIGN 256         // scratch images keep the user buffer's address mod 256
 #define RDC_MIN_TILE (16u << 10)   // smallest tile, bytes
 
@@ -92,7 +97,7 @@ struct CollArgs {
                                          //   (= c for a whole buffer; host pieces cut one chunk's range
                                          //   into n ranges, one per owner, all folding in its order)
     uint64_t slot_bytes;                 // scratch slot stride
-    uint32_t max_tiles;                  // flag array row stride
+    uint32_t max_tiles;                  // flag array row stride (in flags)
     char* rs[RDC_MAX_RANKS];             // rank p's reduce-scatter scratch region
     char* ag[RDC_MAX_RANKS];             // rank p's allgather scratch region
     uint64_t* flags[RDC_MAX_RANKS];      // rank p's flag region: [2n][max_tiles] + done[n] (rdc_device.h seq)
@@ -123,6 +128,8 @@ struct CollArgs {
     int seq_check;                       // RDC_SEQ_CHECK: every block checks it read the launch number the
                                          //   launch's first block read (err words 80-81; a mismatch is
                                          //   recorded in err words 72..79)
+    uint32_t* verify;                    // RDC_VERIFY_PUBLISH (debug): publish read-back counters (err words 84..)
+    int poll_rmw;                        // RDC_POLL_RMW (debug): hand-off polls as atomic adds of 0
     int poison;                          // RDC_POISON_SCRATCH: consumers overwrite scratch ranges they
                                          //   finished reading with 0xFF (rdc_device.h block_poison)
 };

@@ -276,7 +276,22 @@ __device__ __forceinline__ uint64_t seq_prev(uint64_t seq) { return seq - (1ull 
 // only add an L2 write-back (buffer_wbl2 sc0 sc1, 1.7-6.5 us per call) of
 // cached lines no peer reads, so it is issued only for fine- / coarse-grained
 // scratch (alloc fallbacks).
-__device__ __forceinline__ void block_publish(uint64_t* const* flags, int nflags, uint64_t seq, int uc) {
+// verify (RDC_VERIFY_PUBLISH, debug): each storing lane reads its flag back
+// through the same mapping until it sees seq (bounded), and counts in
+// verify[0] the stores it never saw, recording the last such flag address in
+// verify[2..3] — does a store the writer made stay invisible to the writer too?
+__device__ __forceinline__ void verify_flag(uint64_t* f, uint64_t seq, uint32_t* verify) {
+    for (int i = 0; i < (1 << 14); ++i) {
+        if (seq_counter(flag_load(f)) == seq_counter(seq)) return;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __hip_atomic_fetch_add(verify, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(verify + 2), (uint64_t)(uintptr_t)f, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void block_publish(uint64_t* const* flags, int nflags, uint64_t seq, int uc,
+                                              uint32_t* verify = nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < (unsigned)nflags) {
@@ -285,6 +300,7 @@ __device__ __forceinline__ void block_publish(uint64_t* const* flags, int nflags
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         flag_store(flags[threadIdx.x], seq);
+        if (verify) verify_flag(flags[threadIdx.x], seq, verify);
     }
 }
 
@@ -303,6 +319,7 @@ __device__ __forceinline__ void block_publish1(uint64_t* flag, uint64_t seq, int
 struct Abort {
     uint32_t* err;          // local error word (device memory), 0 = ok
     uint64_t deadline;      // wall_clock64() value after which we give up
+    int poll_rmw = 0;       // RDC_POLL_RMW (debug): poll with a system-scope atomic add of 0
 };
 
 // Block-wide wait until every flags[i] (i < nflags <= 64) reached seq.  Wave 0
@@ -327,7 +344,9 @@ __device__ __forceinline__ bool block_wait(uint64_t* const* flags, int nflags, u
         uint64_t seen = 0;   // this lane's last flag value
         while (true) {
             if (!mine) {
-                const uint64_t v = flag_load(flags[lane]);
+                const uint64_t v = ab.poll_rmw ? __hip_atomic_fetch_add(flags[lane], (uint64_t)0, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_SYSTEM)
+                                               : flag_load(flags[lane]);
                 seen = v;
                 if (seq_reached(v, seq)) {
                     if (!tagged || same_tag(v, seq)) mine = true;
@@ -361,6 +380,24 @@ __device__ __forceinline__ bool block_wait(uint64_t* const* flags, int nflags, u
                     __hip_atomic_store(d + 1, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(d + 2, (uint64_t)(uintptr_t)flags[lane], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+                    // the same flag read five ways once more (err words 96..107):
+                    // a relaxed system-scope load, an atomic add of 0 at system
+                    // scope, a load after a system-scope acquire (L1 / L2
+                    // invalidate), a non-temporal load, and this wave's XCC —
+                    // which view still shows the old value after the wait gave up
+                    uint64_t* f = flags[lane];
+                    const uint64_t v1 = flag_load(f);
+                    const uint64_t v2 = __hip_atomic_fetch_add(f, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                    const uint64_t v3 = flag_load(f);
+                    const uint64_t v4 = __builtin_nontemporal_load(f);
+                    const uint64_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf;
+                    uint64_t* pr = reinterpret_cast<uint64_t*>(ab.err + 96);
+                    __hip_atomic_store(pr, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(pr + 1, v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(pr + 2, v3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(pr + 3, v4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(pr + 4, xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }

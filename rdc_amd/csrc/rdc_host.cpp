@@ -226,12 +226,16 @@ void HostPath::Warm(hipStream_t comm_stream) {
     char* pin = nullptr;
     hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin), kMax, hipHostMallocDefault), "hipHostMalloc");
     try {
-        for (hipStream_t s : {h2d_, d2h_, comm_stream})
+        // comm_stream null (RdcNewBuffer): the path's own copy streams only —
+        // never a sync of a stream that may hold queued collectives
+        for (hipStream_t s : {h2d_, d2h_, comm_stream}) {
+            if (!s) continue;
             for (size_t b : {(size_t)64 << 10, (size_t)1 << 20, kMax}) {
                 hip_check(hipMemcpyAsync(dev_, pin, b, hipMemcpyHostToDevice, s), "warm H2D");
                 hip_check(hipMemcpyAsync(pin, dev_, b, hipMemcpyDeviceToHost, s), "warm D2H");
                 hip_check(hipStreamSynchronize(s), "warm sync");
             }
+        }
     } catch (...) {
         (void)hipHostFree(pin);
         throw;
@@ -246,7 +250,7 @@ void HostPath::Warm(hipStream_t comm_stream) {
 void HostPath::QuiesceForRegrow(hipStream_t comm_stream) {
     hip_check(hipStreamSynchronize(h2d_), "sync before regrow");
     hip_check(hipStreamSynchronize(d2h_), "sync before regrow");
-    hip_check(hipStreamSynchronize(comm_stream), "sync before regrow");
+    if (comm_stream) hip_check(hipStreamSynchronize(comm_stream), "sync before regrow");
 }
 
 void HostPath::Reserve(size_t piece_bytes, size_t total_bytes, int pieces, hipStream_t comm_stream) {

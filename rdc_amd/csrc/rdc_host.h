@@ -63,6 +63,8 @@ uint64_t HostRegisteredCalls();
 
 class HostPath {
 public:
+    // buffers up to kSmall: one pinned round trip, one synchronisation (no DMA)
+    static constexpr size_t kSmall = (size_t)1 << 20;
     // zc_max: buffers up to this many bytes run zero-copy on pinned memory
     HostPath(int device, size_t zc_max);
     ~HostPath();
@@ -91,8 +93,6 @@ private:
     void Copy(char* dst, const char* src, size_t bytes, bool to_pinned = false);
     void DrainLoop();
 
-    // buffers up to kSmall: one pinned round trip, one synchronisation
-    static constexpr size_t kSmall = (size_t)1 << 20;
     void AllreduceSmall(Communicator* c, char* host, size_t count, size_t bytes, int dtype, int op,
                         hipStream_t comm_stream);
     // the same pieces and collectives as the pipeline, with the H2D / D2H DMA

@@ -22,7 +22,7 @@ __global__ __launch_bounds__(kBlock) void k_bcast(CollArgs a) {
 // receivers never answer, so pushes wait for the targets' done words.
 __device__ void allgather_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
-    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks, a.poll_rmw};
     __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
     int b = blockIdx.x;
     if (b < a.nb_scatter) {
@@ -39,7 +39,7 @@ __device__ void allgather_body(const CollArgs& a, uint64_t seq) {
             uint64_t tlen = a.len[r] - toff;
             if (tlen > a.tile_bytes) tlen = a.tile_bytes;
             block_copy<kDstPeer>(a.ag[p] + (uint64_t)r * a.slot_bytes + a.mis[r] + toff, a.cbuf[r] + a.off[r] + toff, tlen);
-            block_publish1(a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t, seq, a.uc);
+            block_publish1(flag_word(a, p, (uint64_t)(n + r) * a.max_tiles + t), seq, a.uc);
         }
         return;
     }
@@ -51,7 +51,7 @@ __device__ void allgather_body(const CollArgs& a, uint64_t seq) {
         const int t = it / (n - 1);
         const int c = (r + 1 + it % (n - 1)) % n;
         if (t >= a.tiles[c]) continue;
-        if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
+        if (threadIdx.x == 0) s_flags[0] = flag_word(a, r, (uint64_t)(n + c) * a.max_tiles + t);
         __syncthreads();
         if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_ALLGATHER, a.uc)) return;
         const uint64_t toff = (uint64_t)t * a.tile_bytes;

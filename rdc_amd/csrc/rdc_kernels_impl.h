@@ -21,6 +21,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "rdc_device.h"
@@ -30,9 +32,14 @@ namespace rdc_amd {
 
 constexpr int kBlock = 256;
 
+// flag number `idx` (row * max_tiles + tile, or a done word) of rank p's flag
+// array: RDC_FLAG_STRIDE words apart, each flag in a line of its own
+__device__ __forceinline__ uint64_t* flag_word(const CollArgs& a, int p, uint64_t idx) {
+    return a.flags[p] + idx * RDC_FLAG_STRIDE;
+}
 // rank `owner`'s flag word that rank `writer` sets when it finished a launch
 __device__ __forceinline__ uint64_t* done_word(const CollArgs& a, int owner, int writer) {
-    return a.flags[owner] + (uint64_t)(2 * a.n) * a.max_tiles + writer;
+    return flag_word(a, owner, (uint64_t)(2 * a.n) * a.max_tiles + writer);
 }
 
 // ====================================================== launch sequencing ===
@@ -312,7 +319,7 @@ __device__ __forceinline__ void for_unit_pieces(const CollArgs& a, uint64_t p0, 
 template <int OP, typename T, int NMAX>
 __device__ __forceinline__ void mesh_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
-    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks, a.poll_rmw};
     int b = blockIdx.x;
     int tmax = 0;
     for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
@@ -340,7 +347,7 @@ __device__ __forceinline__ void mesh_body(const CollArgs& a, uint64_t seq) {
                 });
             else
                 block_copy<kDstPeer>(dst + toff, a.user + a.off[c] + toff, tlen);
-            block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, seq, a.uc);
+            block_publish1(flag_word(a, c, (uint64_t)r * a.max_tiles + t), seq, a.uc);
         }
         return;
     }
@@ -350,7 +357,7 @@ __device__ __forceinline__ void mesh_body(const CollArgs& a, uint64_t seq) {
         for (int t = b; t < a.tiles[r]; t += a.nb_reduce) {
             if (threadIdx.x < (unsigned)(n - 1)) {
                 const int p = (r + 1 + threadIdx.x) % n;
-                s_flags[threadIdx.x] = a.flags[r] + (uint64_t)p * a.max_tiles + t;
+                s_flags[threadIdx.x] = flag_word(a, r, (uint64_t)p * a.max_tiles + t);
             }
             __syncthreads();
             if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return;
@@ -371,7 +378,7 @@ __device__ __forceinline__ void mesh_body(const CollArgs& a, uint64_t seq) {
             }
             if (threadIdx.x < (unsigned)(n - 1)) {
                 const int p = (r + 1 + threadIdx.x) % n;
-                s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
+                s_flags[threadIdx.x] = flag_word(a, p, (uint64_t)(n + r) * a.max_tiles + t);
             }
             block_publish(s_flags, n - 1, seq, a.uc);
             __syncthreads();
@@ -385,7 +392,7 @@ __device__ __forceinline__ void mesh_body(const CollArgs& a, uint64_t seq) {
         const int t = it / (n - 1);
         const int c = (r + 1 + it % (n - 1)) % n;
         if (t >= a.tiles[c]) continue;
-        if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
+        if (threadIdx.x == 0) s_flags[0] = flag_word(a, r, (uint64_t)(n + c) * a.max_tiles + t);
         __syncthreads();
         if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_AG, a.uc)) return;
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
@@ -494,7 +501,7 @@ __device__ __forceinline__ void pull_fold_range(const CollArgs& a, char* own, co
 template <int OP, typename T, int NMAX>
 __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
-    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks, a.poll_rmw};
     int b = blockIdx.x;
     int tmax = 0;
     for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
@@ -517,7 +524,7 @@ __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) 
                 });
             else
                 block_copy<kDstPeer>(dst + toff, a.user + a.off[c] + toff, tlen);
-            block_publish1(a.flags[c] + (uint64_t)r * a.max_tiles + t, seq, a.uc);
+            block_publish1(flag_word(a, c, (uint64_t)r * a.max_tiles + t), seq, a.uc);
         }
         return;
     }
@@ -528,7 +535,7 @@ __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) 
         for (int t = b; t < a.tiles[r]; t += a.nb_reduce) {
             if (threadIdx.x < (unsigned)(n - 1)) {
                 const int p = (r + 1 + threadIdx.x) % n;
-                s_flags[threadIdx.x] = a.flags[r] + (uint64_t)p * a.max_tiles + t;
+                s_flags[threadIdx.x] = flag_word(a, r, (uint64_t)p * a.max_tiles + t);
             }
             __syncthreads();
             if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return;
@@ -557,7 +564,7 @@ __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) 
             }
             if (threadIdx.x < (unsigned)(n - 1)) {
                 const int p = (r + 1 + threadIdx.x) % n;
-                s_flags[threadIdx.x] = a.flags[p] + (uint64_t)(n + r) * a.max_tiles + t;
+                s_flags[threadIdx.x] = flag_word(a, p, (uint64_t)(n + r) * a.max_tiles + t);
             }
             block_publish(s_flags, n - 1, seq, a.uc);
             __syncthreads();
@@ -571,7 +578,7 @@ __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) 
         const int t = it / (n - 1);
         const int c = (r + 1 + it % (n - 1)) % n;
         if (t >= a.tiles[c]) continue;
-        if (threadIdx.x == 0) s_flags[0] = a.flags[r] + (uint64_t)(n + c) * a.max_tiles + t;
+        if (threadIdx.x == 0) s_flags[0] = flag_word(a, r, (uint64_t)(n + c) * a.max_tiles + t);
         __syncthreads();
         if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_AG, a.uc)) return;
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
@@ -678,7 +685,7 @@ template <int OP, typename T>
 __device__ void ring_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
     const int prev = (r - 1 + n) % n;
-    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks, a.poll_rmw};
     if (prev_kind(a) == RDC_KIND_ONESHOT && !gate_on_peers(a, seq, prev, 1, ab, RDC_KERR_TIMEOUT_RING)) return;
     __shared__ uint64_t* s_flag[1];
     __shared__ UnitCache s_units;
@@ -699,11 +706,11 @@ __device__ void ring_body(const CollArgs& a, uint64_t seq) {
                 chunk_pieces(a, cs, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
                     block_copy<kDstPeer>(dst + co, usr, l);
                 }, ucp);
-                block_publish1(a.flags[prev] + (uint64_t)j * a.max_tiles + t, seq, a.uc);
+                block_publish1(flag_word(a, prev, (uint64_t)j * a.max_tiles + t), seq, a.uc);
             }
             const int cr = (r + 2 + j) % n;
             if (t < a.tiles[cr]) {
-                if (threadIdx.x == 0) s_flag[0] = a.flags[r] + (uint64_t)j * a.max_tiles + t;
+                if (threadIdx.x == 0) s_flag[0] = flag_word(a, r, (uint64_t)j * a.max_tiles + t);
                 __syncthreads();
                 if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING, a.uc)) return;
                 uint64_t tlen = a.len[cr] - toff;
@@ -727,11 +734,11 @@ __device__ void ring_body(const CollArgs& a, uint64_t seq) {
                 chunk_pieces(a, cs, toff, tlen, [&](char* usr, uint64_t co, uint64_t l) {
                     block_copy<kDstPeer>(dst + co, usr, l);
                 }, ucp);
-                block_publish1(a.flags[prev] + (uint64_t)(n + j) * a.max_tiles + t, seq, a.uc);
+                block_publish1(flag_word(a, prev, (uint64_t)(n + j) * a.max_tiles + t), seq, a.uc);
             }
             const int cr = (r + 1 + j) % n;
             if (t < a.tiles[cr]) {
-                if (threadIdx.x == 0) s_flag[0] = a.flags[r] + (uint64_t)(n + j) * a.max_tiles + t;
+                if (threadIdx.x == 0) s_flag[0] = flag_word(a, r, (uint64_t)(n + j) * a.max_tiles + t);
                 __syncthreads();
                 if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_RING, a.uc)) return;
                 uint64_t tlen = a.len[cr] - toff;
@@ -901,7 +908,7 @@ __device__ void tree_fold_range(const FoldView& a, uint64_t lo, uint64_t hi) {
 template <int OP, typename T, int NMAX, bool TREE = false>
 __device__ void oneshot_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
-    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks, a.poll_rmw};
     __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
     const uint64_t half = (seq_counter(seq) & 1u) ? a.half_bytes : 0;
     const uint64_t total = a.total_bytes;
@@ -914,15 +921,15 @@ __device__ void oneshot_body(const CollArgs& a, uint64_t seq) {
         for (int k = 1; k < n; ++k)
             block_copy<kDstPeer>(a.rs[(r + k) % n] + (uint64_t)r * a.slot_bytes + half + toff, a.user + toff, tlen);
         if (threadIdx.x < (unsigned)(n - 1))
-            s_flags[threadIdx.x] = a.flags[(r + 1 + threadIdx.x) % n] + (uint64_t)r * a.max_tiles + t;
-        block_publish(s_flags, n - 1, seq, a.uc);
+            s_flags[threadIdx.x] = flag_word(a, (r + 1 + threadIdx.x) % n, (uint64_t)r * a.max_tiles + t);
+        block_publish(s_flags, n - 1, seq, a.uc, a.verify);
         __syncthreads();
     }
     // 2) fold my tiles once every peer's copy landed
     const FoldView fv{n, r, a.user, a.user, a.rs[r] + half, a.slot_bytes, a.tree_len, a.tree_dst, a.tree_src};
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         if (threadIdx.x < (unsigned)(n - 1))
-            s_flags[threadIdx.x] = a.flags[r] + (uint64_t)((r + 1 + threadIdx.x) % n) * a.max_tiles + t;
+            s_flags[threadIdx.x] = flag_word(a, r, (uint64_t)((r + 1 + threadIdx.x) % n) * a.max_tiles + t);
         __syncthreads();
         if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return;
         const uint64_t lo = (uint64_t)t * a.tile_bytes;
@@ -960,7 +967,7 @@ __device__ __forceinline__ int bcast_forwarder(int n, int root, int t) { return 
 __device__ void bcast_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank, root = a.root;
     const bool split = a.bcast_split != 0 && n >= 3;
-    Abort ab{a.err, wall_clock64() + a.timeout_ticks};
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks, a.poll_rmw};
     __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
     __shared__ int s_cnt;
     if (blockIdx.x < a.tiles[0] && (r == root || split)) {
@@ -990,15 +997,15 @@ __device__ void bcast_body(const CollArgs& a, uint64_t seq) {
             if (split) {
                 const int f = bcast_forwarder(n, root, t);
                 block_copy<kDstPeer>(a.ag[f] + soff, mine, tlen);
-                block_publish1(a.flags[f] + frow, seq, a.uc);
+                block_publish1(flag_word(a, f, frow), seq, a.uc);
             } else {
                 for (int k = 1; k < n; ++k) block_copy<kDstPeer>(a.ag[(root + k) % n] + soff, mine, tlen);
-                if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = a.flags[(root + 1 + threadIdx.x) % n] + frow;
+                if (threadIdx.x < (unsigned)(n - 1)) s_flags[threadIdx.x] = flag_word(a, (root + 1 + threadIdx.x) % n, frow);
                 block_publish(s_flags, n - 1, seq, a.uc);
             }
             __syncthreads();
         } else {
-            if (threadIdx.x == 0) s_flags[0] = a.flags[r] + frow;
+            if (threadIdx.x == 0) s_flags[0] = flag_word(a, r, frow);
             __syncthreads();
             if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_BCAST, a.uc)) return;
             char* land = a.ag[r] + soff;
@@ -1010,7 +1017,7 @@ __device__ void bcast_body(const CollArgs& a, uint64_t seq) {
                 if (threadIdx.x == 0) {
                     int k = 0;
                     for (int q = 0; q < n; ++q)
-                        if (q != r && q != root) s_flags[k++] = a.flags[q] + frow;
+                        if (q != r && q != root) s_flags[k++] = flag_word(a, q, frow);
                 }
                 block_publish(s_flags, n - 2, seq, a.uc);  // its barrier orders thread 0's list before use
             }
@@ -1500,6 +1507,20 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
 }
 
 // ============================================================ dispatch ===
+// RDC_DEBUG_LDS_PAD=<bytes>: dynamic LDS reserved by every collective launch
+// (and counted by the occupancy queries, so the resident-grid clamp follows):
+// a debug knob that lowers the blocks per CU, e.g. 96 KiB = one block per CU,
+// to rehearse a kernel at another occupancy without changing its code
+// (round 4's lost one-shot hand-off happened at one block per CU).
+inline unsigned debug_lds_pad() {
+    static const unsigned pad = [] {
+        const char* v = getenv("RDC_DEBUG_LDS_PAD");
+        const long x = v ? atol(v) : 0;
+        return (unsigned)(x > 0 && x <= (150l << 10) ? x : 0);
+    }();
+    return pad;
+}
+
 template <int OP, typename T>
 struct Kernels {
     static hipError_t reduce(char* dst, const char* src, uint64_t nbytes, int grid, hipStream_t s) {
@@ -1513,20 +1534,20 @@ struct Kernels {
     }
     static hipError_t mesh(const CollArgs& a, int grid, hipStream_t s) {
         if (a.n <= 8)
-            hipLaunchKernelGGL((k_mesh<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_mesh<OP, T, 8>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
         else
-            hipLaunchKernelGGL((k_mesh<OP, T, 16>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_mesh<OP, T, 16>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
         return hipGetLastError();
     }
     static hipError_t oneshot(const CollArgs& a, int grid, hipStream_t s) {
         if (a.n <= 8)
-            hipLaunchKernelGGL((k_oneshot<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_oneshot<OP, T, 8>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
         else
-            hipLaunchKernelGGL((k_oneshot<OP, T, 16>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_oneshot<OP, T, 16>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
         return hipGetLastError();
     }
     static hipError_t ring(const CollArgs& a, int grid, hipStream_t s) {
-        hipLaunchKernelGGL((k_ring<OP, T>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_ring<OP, T>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
         return hipGetLastError();
     }
     static hipError_t svc(const SvcArgs& a, hipStream_t s) {
@@ -1543,9 +1564,9 @@ struct Kernels {
     }
     static hipError_t tree(const CollArgs& a, int grid, hipStream_t s) {
         if (a.n <= 8)
-            hipLaunchKernelGGL((k_tree<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_tree<OP, T, 8>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
         else
-            hipLaunchKernelGGL((k_tree<OP, T, 16>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_tree<OP, T, 16>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
         return hipGetLastError();
     }
     static int occupancy(int kind, int n) {
@@ -1560,13 +1581,13 @@ struct Kernels {
         int b = 0;
         hipError_t e = hipSuccess;
         switch (slot) {
-            case 0: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_mesh<OP, T, 8>, kBlock, 0); break;
-            case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_mesh<OP, T, 16>, kBlock, 0); break;
-            case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_oneshot<OP, T, 8>, kBlock, 0); break;
-            case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_oneshot<OP, T, 16>, kBlock, 0); break;
-            case 5: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_tree<OP, T, 8>, kBlock, 0); break;
-            case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_tree<OP, T, 16>, kBlock, 0); break;
-            default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_ring<OP, T>, kBlock, 0); break;
+            case 0: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_mesh<OP, T, 8>, kBlock, debug_lds_pad()); break;
+            case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_mesh<OP, T, 16>, kBlock, debug_lds_pad()); break;
+            case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_oneshot<OP, T, 8>, kBlock, debug_lds_pad()); break;
+            case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_oneshot<OP, T, 16>, kBlock, debug_lds_pad()); break;
+            case 5: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_tree<OP, T, 8>, kBlock, debug_lds_pad()); break;
+            case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_tree<OP, T, 16>, kBlock, debug_lds_pad()); break;
+            default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_ring<OP, T>, kBlock, debug_lds_pad()); break;
         }
         if (e != hipSuccess || b <= 0) {
             (void)hipGetLastError();

@@ -25,7 +25,7 @@ Layout MakeLayout(int n, size_t scratch_bytes) {
     L.region_bytes = slot * (size_t)n;
     L.max_tiles = (uint32_t)(L.region_bytes / RDC_MIN_TILE + 2);
     // [2n][max_tiles] hand-off flags + done[n] (one word per peer, rdc_kernels.hip launch_done)
-    L.flag_bytes = round_up(((size_t)2 * n * L.max_tiles + (size_t)n) * sizeof(uint64_t), 4096);
+    L.flag_bytes = round_up(((size_t)2 * n * L.max_tiles + (size_t)n) * sizeof(uint64_t) * RDC_FLAG_STRIDE, 4096);
     return L;
 }
 

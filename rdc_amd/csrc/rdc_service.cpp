@@ -155,9 +155,13 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
     if (bytes > RDC_SVC_MAX_BYTES) throw std::logic_error("rdc service: buffer too large");
     if (launched_ && kind != kind_) Stop();  // another (dtype, op) needs another kernel
     const uint32_t r = ++req_;
-    const bool ll = bytes <= ll_bytes_;
-    // host exchange: the same choice on every rank (n, bytes and the budget agree)
-    const bool hx = hx_ != nullptr && ll && bytes * (uint64_t)n_ <= HxBytes();
+    // host exchange: the same choice on every rank — it depends only on n,
+    // bytes, the LL limit and the budget (a plan key), never on this
+    // process's RDC_HOST_SERVICE_LL_BYTES (ranks that set that
+    // differently would write to different places and wait on words never
+    // written); it carries its input as LL words, so it forces LL input
+    const bool hx = hx_ != nullptr && bytes <= RDC_SVC_LL_MAX && bytes * (uint64_t)n_ <= HxBytes();
+    const bool ll = hx || bytes <= ll_bytes_;
     const uint64_t nwords = ((bytes + 15) / 16) * 4;  // whole 16-byte vectors of 4-byte LL payloads
     const auto t0 = std::chrono::steady_clock::now();
     if (ll) {

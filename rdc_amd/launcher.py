@@ -149,13 +149,21 @@ QUEUE_BUDGET = 16
 
 def hw_queues_per_process(ranks_per_gpu):
     """GPU_MAX_HW_QUEUES for a process that shares its GPU with
-    ranks_per_gpu - 1 others (None: leave HIP's default of 4).  (5 processes x
-    3 queues once lost a one-shot hand-off in about every second run — always
-    in an int8 kernel that then ran one wave per SIMD; since the byte folds
-    shrank 5 x 3 passed 13 of 13 runs, profiles/r04/queues/.)"""
+    ranks_per_gpu - 1 others (None: leave HIP's default of 4): the budget's
+    share rounded down to a power of two, so never 3.  Three queues per
+    process with 5 or more processes on one GPU lose hand-offs (DESIGN.md
+    §4.2, round 5): a rank's device reads of a peer's flag keep returning the
+    previous launch's number — every load kind, atomics and reads after a
+    system acquire alike — while the host reads the new one at the same
+    address.  At one block per CU (RDC_DEBUG_LDS_PAD=96K) 5 x 3 and 6 x 3
+    failed every run, 5 x 1, 5 x 2, 5 x 4, 6 x 2, 8 x 2, 4 x 2, 4 x 3 and 3 x 3
+    never (profiles/r05/queues/)."""
     if ranks_per_gpu * 4 <= QUEUE_BUDGET:
         return None
-    return max(1, QUEUE_BUDGET // ranks_per_gpu)
+    q = max(1, QUEUE_BUDGET // ranks_per_gpu)
+    while q & (q - 1):
+        q &= q - 1
+    return q
 
 
 def queues_over_budget(current, q):

@@ -684,7 +684,8 @@ HOST_SWEEP_BYTES = [
 ]
 
 
-@pytest.mark.parametrize("world,balance", [(2, "0"), (3, "0"), (3, "1"), (4, "1"), (5, "0"), (5, "1"), (5, "diag")])
+@pytest.mark.parametrize("world,balance", [(2, "0"), (3, "0"), (3, "1"), (4, "1"), (5, "0"), (5, "1"), (5, "diag"),
+                                           (5, "one_block_per_cu")])
 def test_mp_host_size_sweep(world, balance):
     """Host buffers at every boundary of the host path (rdc_host.cpp: service,
     copy-pool parts, zero-copy / staged small path, inline piece, pipeline
@@ -696,12 +697,19 @@ def test_mp_host_size_sweep(world, balance):
     chunk's ring order; the default with one rank per GPU).  "diag": 5
     processes on one GPU at the launcher's queue budget (round 4's lost
     one-shot hand-off ran here) with poison mode and the device-side launch
-    number check on (RDC_POISON_SCRATCH=1, RDC_SEQ_CHECK=1)."""
+    number check on (RDC_POISON_SCRATCH=1, RDC_SEQ_CHECK=1).
+    "one_block_per_cu": the same with every collective held to one block per
+    CU (RDC_DEBUG_LDS_PAD=96K) — at round 4's budget of 3 queues per process
+    this lost a hand-off in every run; the launcher's budget is now a power of
+    two (2 queues for 5 ranks)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     env = {"RDC_HOST_BALANCE": balance}
     if balance == "diag":
         env = {"RDC_HOST_BALANCE": "0", "RDC_POISON_SCRATCH": "1", "RDC_SEQ_CHECK": "1"}
+    elif balance == "one_block_per_cu":
+        env = {"RDC_HOST_BALANCE": "0", "RDC_POISON_SCRATCH": "1", "RDC_SEQ_CHECK": "1",
+               "RDC_DEBUG_LDS_PAD": str(96 << 10)}
     cases = []
     for k, nb in enumerate(HOST_SWEEP_BYTES):
         cases.append({"count": nb, "dtype": 1, "op": (0, 2)[k % 2], "kind": "host_allreduce", "seed": 0x5EEDA000 + k})

@@ -277,7 +277,9 @@ def test_launcher_queue_budget(tmp_path, monkeypatch):
     1; a GPU_MAX_HW_QUEUES above the budget is lowered, one below it kept; the KFD GPU count from sysfs."""
     import argparse
     from rdc_amd.launcher import hw_queues_per_process, kfd_gpu_count, visible_gpu_count, worker_env
-    assert [hw_queues_per_process(k) for k in (1, 2, 4, 5, 8, 16, 32)] == [None, None, None, 3, 2, 1, 1]
+    assert [hw_queues_per_process(k) for k in (1, 2, 4, 5, 8, 16, 32)] == [None, None, None, 2, 2, 1, 1]
+    # never 3 queues per process (DESIGN.md §4.2: 5 x 3 and 6 x 3 lose hand-offs)
+    assert all(hw_queues_per_process(k) in (None, 1, 2, 4) for k in range(1, 65))
     monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
     a = argparse.Namespace(host_ip="127.0.0.1", num_workers=8)
     assert worker_env(a, 3, 1234, 1)["GPU_MAX_HW_QUEUES"] == "2"
