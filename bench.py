@@ -574,6 +574,9 @@ def trace_roles(lib, comm, buf, count, dt_enum, sp, dist, torch):
     grid, s, r, g, tile, algo = [int(x) for x in ll]
     t = tr[:2 * grid].cpu().numpy().view(np.uint64).reshape(grid, 2).astype(np.float64)
     t0 = t[:, 0].min()
+    dump = os.environ.get("RDC_BENCH_TRACE_DUMP")  # per-rank raw {start, end} ticks per block
+    if dump:
+        np.save("%s.rank%d.npy" % (dump, dist.get_rank()), np.concatenate([[grid, s, r, g, tile, algo], t.ravel()]))
     names = {1: "ring", 2: "mesh", 3: "oneshot", 5: "mesh_pull"}
     roles = {"all": (0, grid)} if algo not in (2, 5) else {"scatter": (0, s), "reduce": (s, s + r),
                                                            "gather": (s + r, grid)}

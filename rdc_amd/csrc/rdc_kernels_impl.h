@@ -498,6 +498,88 @@ __device__ __forceinline__ void pull_fold_range(const CollArgs& a, char* own, co
     }
 }
 
+// One work item of each pull-mesh role.
+// stage: my copy of chunk c's tile t -> my RS slot c, then owner c's flag
+__device__ __forceinline__ void pull_stage_item(const CollArgs& a, uint64_t seq, int t, int c) {
+    const int r = a.rank;
+    const uint64_t toff = (uint64_t)t * a.tile_bytes;
+    uint64_t tlen = a.len[c] - toff;
+    if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+    char* dst = a.rs[r] + (uint64_t)c * a.slot_bytes + a.mis[c];
+    if (a.units)
+        for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
+            block_copy<kDstPeer>(dst + (p - a.off[c]), usr, l);
+        });
+    else
+        block_copy<kDstPeer>(dst + toff, a.user + a.off[c] + toff, tlen);
+    block_publish1(flag_word(a, c, (uint64_t)r * a.max_tiles + t), seq, a.uc);
+    __syncthreads();
+}
+
+// reduce: chunk r, tile t, once all n-1 peers staged it; false: the wait gave up
+template <int OP, typename T, int NMAX>
+__device__ __forceinline__ bool pull_reduce_item(const CollArgs& a, uint64_t seq, const Abort& ab, int t) {
+    const int n = a.n, r = a.rank;
+    __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
+    __shared__ const char* s_src[RDC_MAX_RANKS];
+    if (threadIdx.x < (unsigned)(n - 1)) {
+        const int p = (r + 1 + threadIdx.x) % n;
+        s_flags[threadIdx.x] = flag_word(a, r, (uint64_t)p * a.max_tiles + t);
+    }
+    __syncthreads();
+    if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return false;
+    const uint64_t toff = (uint64_t)t * a.tile_bytes;
+    uint64_t tlen = a.len[r] - toff;
+    if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+    const uint64_t slot_r = (uint64_t)r * a.slot_bytes;
+    if (a.units) {
+        for_unit_pieces(a, a.off[r] + toff, a.off[r] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
+            const uint64_t co = a.mis[r] + (p - a.off[r]);
+            if (threadIdx.x < (unsigned)n) s_src[threadIdx.x] = a.rs[threadIdx.x] + slot_r + co;
+            __syncthreads();
+            pull_fold_range<OP, T, NMAX>(a, usr, s_src, a.ag[r] + slot_r + co, l);
+            __syncthreads();  // s_src is rewritten for the next piece
+        });
+    } else {
+        const uint64_t co = a.mis[r] + toff;
+        if (threadIdx.x < (unsigned)n) s_src[threadIdx.x] = a.rs[threadIdx.x] + slot_r + co;
+        __syncthreads();
+        pull_fold_range<OP, T, NMAX>(a, a.user + a.off[r] + toff, s_src, a.ag[r] + slot_r + co, tlen);
+    }
+    if (a.poison) {  // peer q restages its slot r only after gathering this tile's result
+        __syncthreads();
+        for (int k = 1; k < n; ++k) block_poison(a.rs[(r + k) % n] + slot_r + a.mis[r] + toff, tlen);
+    }
+    if (threadIdx.x < (unsigned)(n - 1)) {
+        const int p = (r + 1 + threadIdx.x) % n;
+        s_flags[threadIdx.x] = flag_word(a, p, (uint64_t)(n + r) * a.max_tiles + t);
+    }
+    block_publish(s_flags, n - 1, seq, a.uc);
+    __syncthreads();
+    return true;
+}
+
+// gather: owner c's result tile t (its AG slot c) -> my user buffer; false: gave up
+__device__ __forceinline__ bool pull_gather_item(const CollArgs& a, uint64_t seq, const Abort& ab, int t, int c) {
+    const int n = a.n, r = a.rank;
+    __shared__ uint64_t* s_flag[1];
+    if (threadIdx.x == 0) s_flag[0] = flag_word(a, r, (uint64_t)(n + c) * a.max_tiles + t);
+    __syncthreads();
+    if (!block_wait(s_flag, 1, seq, ab, RDC_KERR_TIMEOUT_AG, a.uc)) return false;
+    const uint64_t toff = (uint64_t)t * a.tile_bytes;
+    uint64_t tlen = a.len[c] - toff;
+    if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+    const char* src = a.ag[c] + (uint64_t)c * a.slot_bytes + a.mis[c];
+    if (a.units)
+        for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
+            block_copy_pull(usr, src + (p - a.off[c]), l);
+        });
+    else
+        block_copy_pull(a.user + a.off[c] + toff, src + toff, tlen);
+    __syncthreads();
+    return true;
+}
+
 template <int OP, typename T, int NMAX>
 __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) {
     const int n = a.n, r = a.rank;
@@ -505,93 +587,27 @@ __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) 
     int b = blockIdx.x;
     int tmax = 0;
     for (int c = 0; c < n; ++c) tmax = a.tiles[c] > tmax ? a.tiles[c] : tmax;
-    __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
-
     if (b < a.nb_scatter) {
-        // ---- stage: my copy of chunk c's tile t -> my RS slot c, then owner c's flag
         const int items = (n - 1) * tmax;
         for (int it = b; it < items; it += a.nb_scatter) {
             const int t = it / (n - 1);
             const int c = (r + 1 + it % (n - 1)) % n;
-            if (t >= a.tiles[c]) continue;
-            const uint64_t toff = (uint64_t)t * a.tile_bytes;
-            uint64_t tlen = a.len[c] - toff;
-            if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-            char* dst = a.rs[r] + (uint64_t)c * a.slot_bytes + a.mis[c];
-            if (a.units)
-                for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
-                    block_copy<kDstPeer>(dst + (p - a.off[c]), usr, l);
-                });
-            else
-                block_copy<kDstPeer>(dst + toff, a.user + a.off[c] + toff, tlen);
-            block_publish1(flag_word(a, c, (uint64_t)r * a.max_tiles + t), seq, a.uc);
+            if (t < a.tiles[c]) pull_stage_item(a, seq, t, c);
         }
         return;
     }
     b -= a.nb_scatter;
     if (b < a.nb_reduce) {
-        // ---- reduce: chunk r, tile t, once all n-1 peers staged it
-        __shared__ const char* s_src[RDC_MAX_RANKS];
-        for (int t = b; t < a.tiles[r]; t += a.nb_reduce) {
-            if (threadIdx.x < (unsigned)(n - 1)) {
-                const int p = (r + 1 + threadIdx.x) % n;
-                s_flags[threadIdx.x] = flag_word(a, r, (uint64_t)p * a.max_tiles + t);
-            }
-            __syncthreads();
-            if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return;
-            const uint64_t toff = (uint64_t)t * a.tile_bytes;
-            uint64_t tlen = a.len[r] - toff;
-            if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-            const uint64_t slot_r = (uint64_t)r * a.slot_bytes;
-            if (a.units) {
-                for_unit_pieces(a, a.off[r] + toff, a.off[r] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
-                    const uint64_t co = a.mis[r] + (p - a.off[r]);
-                    if (threadIdx.x < (unsigned)n) s_src[threadIdx.x] = a.rs[threadIdx.x] + slot_r + co;
-                    __syncthreads();
-                    pull_fold_range<OP, T, NMAX>(a, usr, s_src, a.ag[r] + slot_r + co, l);
-                    __syncthreads();  // s_src is rewritten for the next piece
-                });
-            } else {
-                const uint64_t co = a.mis[r] + toff;
-                if (threadIdx.x < (unsigned)n) s_src[threadIdx.x] = a.rs[threadIdx.x] + slot_r + co;
-                __syncthreads();
-                pull_fold_range<OP, T, NMAX>(a, a.user + a.off[r] + toff, s_src, a.ag[r] + slot_r + co, tlen);
-            }
-            if (a.poison) {  // peer q restages its slot r only after gathering this tile's result
-                __syncthreads();
-                for (int k = 1; k < n; ++k)
-                    block_poison(a.rs[(r + k) % n] + slot_r + a.mis[r] + toff, tlen);
-            }
-            if (threadIdx.x < (unsigned)(n - 1)) {
-                const int p = (r + 1 + threadIdx.x) % n;
-                s_flags[threadIdx.x] = flag_word(a, p, (uint64_t)(n + r) * a.max_tiles + t);
-            }
-            block_publish(s_flags, n - 1, seq, a.uc);
-            __syncthreads();
-        }
+        for (int t = b; t < a.tiles[r]; t += a.nb_reduce)
+            if (!pull_reduce_item<OP, T, NMAX>(a, seq, ab, t)) return;
         return;
     }
     b -= a.nb_reduce;
-    // ---- gather: owner c's result tile t (its AG slot c) -> my user buffer
     const int items = (n - 1) * tmax;
     for (int it = b; it < items; it += a.nb_gather) {
         const int t = it / (n - 1);
         const int c = (r + 1 + it % (n - 1)) % n;
-        if (t >= a.tiles[c]) continue;
-        if (threadIdx.x == 0) s_flags[0] = flag_word(a, r, (uint64_t)(n + c) * a.max_tiles + t);
-        __syncthreads();
-        if (!block_wait(s_flags, 1, seq, ab, RDC_KERR_TIMEOUT_AG, a.uc)) return;
-        const uint64_t toff = (uint64_t)t * a.tile_bytes;
-        uint64_t tlen = a.len[c] - toff;
-        if (tlen > a.tile_bytes) tlen = a.tile_bytes;
-        const char* src = a.ag[c] + (uint64_t)c * a.slot_bytes + a.mis[c];
-        if (a.units)
-            for_unit_pieces(a, a.off[c] + toff, a.off[c] + toff + tlen, [&](char* usr, uint64_t p, uint64_t l) {
-                block_copy_pull(usr, src + (p - a.off[c]), l);
-            });
-        else
-            block_copy_pull(a.user + a.off[c] + toff, src + toff, tlen);
-        __syncthreads();
+        if (t < a.tiles[c] && !pull_gather_item(a, seq, ab, t, c)) return;
     }
 }
 

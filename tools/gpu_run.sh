@@ -72,7 +72,7 @@ for step in "$@"; do
     benchN)
         tagged=$OUT/bench_n$a1$(echo "${a2:+_$a2}" | tr ',-' '__').txt   # one file per (n, args)
         run_bench_n $a1 $tagged $(echo "$a2" | tr ',' ' ') || { tail -20 $tagged.err; exit 1; }
-        cp $tagged $OUT/bench_n$a1.txt
+        [ "$tagged" = "$OUT/bench_n$a1.txt" ] || cp $tagged $OUT/bench_n$a1.txt
         grep '^{' $tagged | head -c 400; echo ;;
     pmc1)
         P=$OUT/pmc_n1
