@@ -41,10 +41,12 @@ enum { RDC_KIND_NONE = 0, RDC_KIND_MESH = 1, RDC_KIND_RING = 2, RDC_KIND_BCAST =
        RDC_KIND_ONESHOT = 5, RDC_KIND_TREE = 6 };
 
 #define RDC_MAX_RANKS 16
-// 64-bit words from one hand-off flag to the next (CollArgs::flag_stride):
-// 16 = each flag in a 128-B line of its own
+// 64-bit words from one hand-off flag to the next: 1 = packed (the default);
+// a build with 16 puts each flag in a 128-B line of its own (tried in round 5
+// against the lost hand-off of DESIGN.md §4.2: no effect; it costs 16x the
+// flag memory, 255 MiB per rank at n = 8 and the default scratch)
 #ifndef RDC_FLAG_STRIDE
-#define RDC_FLAG_STRIDE 16
+#define RDC_FLAG_STRIDE 1
 #endif
 #define RDC_SLOT_ALIGN 256         // scratch images keep the user buffer's address mod 256
 #define RDC_MIN_TILE (16u << 10)   // smallest tile, bytes
