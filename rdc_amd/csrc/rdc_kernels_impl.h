@@ -1226,6 +1226,7 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
     const int n = a.n, r = a.rank;
     const unsigned tid = threadIdx.x;
     SvcBox* box = a.box;
+    SvcIn* in = a.in;
     const bool hxm = HX && a.hx != nullptr;
     const uint32_t all = (n >= 32 ? ~0u : (1u << n) - 1u);
     __shared__ v4u s_in[RDC_SVC_MAX_BYTES / 16];  // this rank's input, read once over PCIe
@@ -1263,7 +1264,7 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                 box_store(&box->state, RDC_SVC_EXITING);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
                 g = -1;
-                q = box_load64(&box->hdr);
+                q = box_load64(&in->hdr);
                 if ((uint32_t)(q >> 32) == seq) {
                     box_store(&box->state, RDC_SVC_RUNNING);
                     g = 1;
@@ -1289,10 +1290,10 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
             // next round's in flight
             const uint64_t ev = eager ? tid : 0;
             auto issue = [&](v4u& lo, v4u& hi, uint64_t& q, uint32_t& st) {
-                lo = ld16_nt(box->data + 16 * ev);
-                hi = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * ev);
-                q = box_load64(&box->hdr);
-                st = box_load(&box->stop);
+                lo = ld16_nt(in->data + 16 * ev);
+                hi = ld16_nt(in->data + RDC_SVC_LL_MAX + 16 * ev);
+                q = box_load64(&in->hdr);
+                st = box_load(&in->stop);
             };
             auto round = [&](uint64_t q, uint32_t st) {
                 if (tid == 0) decide(q, st);
@@ -1321,8 +1322,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
         }
         for (; HX || !a.pipe;) {
             if (eager) {
-                elo = ld16_nt(box->data + 16 * tid);
-                ehi = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * tid);
+                elo = ld16_nt(in->data + 16 * tid);
+                ehi = ld16_nt(in->data + RDC_SVC_LL_MAX + 16 * tid);
             }
             if (heager && hpend) {  // pending ranks' loads in flight four at a time, then the matches
                 constexpr int G = 4;      // (all NMAX at once spilled VGPRs to scratch)
@@ -1345,8 +1346,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                 }
             }
             if (tid == 0) {
-                const uint64_t q = box_load64(&box->hdr);
-                const uint32_t stop = box_load(&box->stop);  // issued with the header read: one round trip
+                const uint64_t q = box_load64(&in->hdr);
+                const uint32_t stop = box_load(&in->stop);  // issued with the header read: one round trip
                 decide(q, stop);
             }
             __syncthreads();
@@ -1390,8 +1391,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                         lo[u] = elo;
                         hi[u] = ehi;
                     } else if (i < nvec) {
-                        lo[u] = ld16_nt(box->data + 16 * i);
-                        hi[u] = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * i);
+                        lo[u] = ld16_nt(in->data + 16 * i);
+                        hi[u] = ld16_nt(in->data + RDC_SVC_LL_MAX + 16 * i);
                     }
                 }
 #pragma unroll
@@ -1405,8 +1406,8 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                             break;
                         }
                         asm volatile("" ::: "memory");
-                        lo[u] = ld16_nt(box->data + 16 * i);
-                        hi[u] = ld16_nt(box->data + RDC_SVC_LL_MAX + 16 * i);
+                        lo[u] = ld16_nt(in->data + 16 * i);
+                        hi[u] = ld16_nt(in->data + RDC_SVC_LL_MAX + 16 * i);
                     }
                     if (ok) send(i, v4u{lo[u].x, lo[u].z, hi[u].x, hi[u].z});
                 }
@@ -1416,7 +1417,7 @@ __global__ __launch_bounds__(BS) void k_svc(SvcArgs a) {
                 v4u x[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    if (i0 + (uint64_t)u * BS < nvec) x[u] = ld16_nt(box->data + 16 * (i0 + (uint64_t)u * BS));
+                    if (i0 + (uint64_t)u * BS < nvec) x[u] = ld16_nt(in->data + 16 * (i0 + (uint64_t)u * BS));
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if (i0 + (uint64_t)u * BS < nvec) send(i0 + (uint64_t)u * BS, x[u]);

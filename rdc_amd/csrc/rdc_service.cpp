@@ -1,6 +1,9 @@
 // Small-allreduce service (see rdc_service.h).
 #include "rdc_service.h"
 
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -30,6 +33,91 @@ bool SmallService::Enabled() {
         return !(v && *v && atoi(v) == 0);
     }();
     return on;
+}
+
+namespace {
+// sfence: orders and drains stores to write-combining memory (the BAR mapping
+// of a VRAM mailbox); on write-back memory it costs a few cycles
+inline void wc_flush() { __builtin_ia32_sfence(); }
+
+struct PoolPick {
+    hsa_agent_t gpu{}, cpu{};
+    uint32_t want_bdf = 0, want_domain = 0;
+    bool have_gpu = false, have_cpu = false, have_pool = false;
+    hsa_amd_memory_pool_t pool{};
+};
+hsa_status_t pick_agent(hsa_agent_t a, void* d) {
+    PoolPick* p = static_cast<PoolPick*>(d);
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+    if (t == HSA_DEVICE_TYPE_CPU && !p->have_cpu) {
+        p->cpu = a;
+        p->have_cpu = true;
+    } else if (t == HSA_DEVICE_TYPE_GPU && !p->have_gpu) {
+        uint32_t bdf = 0, dom = 0;
+        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+        if ((bdf >> 3) == (p->want_bdf >> 3) && dom == p->want_domain) {
+            p->gpu = a;
+            p->have_gpu = true;
+        }
+    }
+    return HSA_STATUS_SUCCESS;
+}
+hsa_status_t pick_pool(hsa_amd_memory_pool_t pool, void* d) {
+    PoolPick* p = static_cast<PoolPick*>(d);
+    hsa_amd_segment_t seg;
+    uint32_t flags = 0;
+    if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS)
+        return HSA_STATUS_SUCCESS;
+    hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+    if (seg == HSA_AMD_SEGMENT_GLOBAL && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) && !p->have_pool) {
+        p->pool = pool;
+        p->have_pool = true;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+}  // namespace
+
+// Device memory of HIP device `device` that this process's CPU can write
+// through the PCIe BAR (the GPU's fine-grained pool, uncached, CPU given
+// access), or null when the runtime refuses any step (small BAR, no such
+// pool).  The HSA runtime is the one HIP runs on.  Opt-in
+// (RDC_HOST_SERVICE_VRAM=1): a bare word round trip through it is faster
+// (1.8 vs 2.6 us, tools/mailbox_rtt.hip), but the service with its request
+// side in VRAM measured slower on one shared GPU — n = 2, 4 B 10.4-11.4 vs
+// 6.4-6.5 us, 4 KiB 11.8-12.8 vs 8.2 us, also without eager data reads
+// (profiles/r05/svc_vram/).
+void* AllocVramMailbox(int device, size_t bytes) {
+    const char* e = getenv("RDC_HOST_SERVICE_VRAM");
+    if (!(e && *e && atoi(e) != 0)) return nullptr;
+    int bus = 0, dev = 0, dom = 0;
+    if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+        hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
+        hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (hsa_init() != HSA_STATUS_SUCCESS) return nullptr;  // reference-counted; HIP holds it already
+    PoolPick p;
+    p.want_bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
+    p.want_domain = (uint32_t)dom;
+    void* mem = nullptr;
+    if (hsa_iterate_agents(pick_agent, &p) == HSA_STATUS_SUCCESS && p.have_gpu && p.have_cpu &&
+        hsa_amd_agent_iterate_memory_pools(p.gpu, pick_pool, &p) == HSA_STATUS_SUCCESS && p.have_pool &&
+        hsa_amd_memory_pool_allocate(p.pool, bytes, HSA_AMD_MEMORY_POOL_UNCACHED_FLAG, &mem) == HSA_STATUS_SUCCESS) {
+        hsa_agent_t both[2] = {p.gpu, p.cpu};
+        if (hsa_amd_agents_allow_access(2, both, nullptr, mem) != HSA_STATUS_SUCCESS) {
+            hsa_amd_memory_pool_free(mem);
+            mem = nullptr;
+        }
+    }
+    hsa_shut_down();  // drops this call's reference only
+    return mem;
+}
+
+void FreeVramMailbox(void* p) {
+    if (p) hsa_amd_memory_pool_free(p);
 }
 
 uint64_t SmallService::HxBytes() {
@@ -82,6 +170,25 @@ SmallService::SmallService(int rank, int n, int device, char* const* region, uin
     void* d = nullptr;
     hip_check(hipHostGetDevicePointer(&d, box_, 0), "mailbox device address");
     args_.box = static_cast<SvcBox*>(d);
+    // the request side: VRAM the CPU writes through the BAR, else pinned host memory
+    in_ = static_cast<SvcIn*>(AllocVramMailbox(device_, sizeof(SvcIn)));
+    in_vram_ = in_ != nullptr;
+    if (in_vram_) {
+        args_.in = in_;  // one address for the CPU and the GPU
+    } else {
+        if (hipHostMalloc(reinterpret_cast<void**>(&in_), sizeof(SvcIn), hipHostMallocUncached | hipHostMallocMapped) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipHostFree(box_);
+            box_ = nullptr;
+            in_ = nullptr;
+            return;
+        }
+        hip_check(hipHostGetDevicePointer(&d, in_, 0), "mailbox device address");
+        args_.in = static_cast<SvcIn*>(d);
+    }
+    memset(static_cast<void*>(in_), 0, sizeof(SvcIn));
+    wc_flush();
     if (hx && HxBytes() > 0) {
         void* hd = nullptr;
         hip_check(hipHostGetDevicePointer(&hd, hx, 0), "host exchange device address");
@@ -117,16 +224,20 @@ SmallService::~SmallService() {
     }
     if (stream_) (void)hipStreamDestroy(stream_);
     if (box_) (void)hipHostFree(box_);
+    if (in_ && in_vram_) FreeVramMailbox(in_);
+    else if (in_) (void)hipHostFree(in_);
 }
 
 // the kernel leaves at its next poll (or when a request it serves completes
 // or times out); the stream sync makes sure it is gone
 void SmallService::Stop() {
     if (!launched_) return;
-    host_store(&box_->stop, 1);
+    host_store(&in_->stop, 1);
+    wc_flush();
     (void)hipSetDevice(device_);
     hip_check(hipStreamSynchronize(stream_), "stop service");
-    host_store(&box_->stop, 0);
+    host_store(&in_->stop, 0);
+    wc_flush();
     launched_ = false;
 }
 
@@ -187,7 +298,7 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
         // memcpy gives no such guarantee (rep movsb, overlapping vector
         // stores); aligned 8-byte atomic stores do.
         char* dst = hx ? hx_ + ((uint64_t)(r & 1u) * (uint64_t)n_ + (uint64_t)rank_) * RDC_SVC_HX_RANK_BYTES
-                       : box_->data;
+                       : in_->data;
         uint64_t* p0 = reinterpret_cast<uint64_t*>(dst);
         uint64_t* p1 = reinterpret_cast<uint64_t*>(dst + RDC_SVC_LL_MAX);
         const uint64_t* s0 = stage_.data();
@@ -198,14 +309,18 @@ void SmallService::Allreduce(const KernelSet& ks, int kind, char* host, uint64_t
         }
         if (args_.trace) ht_[0] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     } else {
-        memcpy(box_->data, host, bytes);
+        memcpy(in_->data, host, bytes);
     }
-    // the header, after the data (x86 stores stay in order)
+    // the header, after the data: x86 stores to write-back host memory stay in
+    // order, stores to the write-combining BAR mapping of VRAM only behind an
+    // sfence (wc_flush), which also sends them out at once
+    wc_flush();
     const bool ll_out = bytes <= ll_out_bytes_;
-    __atomic_store_n(&box_->hdr,
+    __atomic_store_n(&in_->hdr,
                      ((uint64_t)r << 32) | (tree ? 1ull << 31 : 0ull) | (ll ? 1ull << 30 : 0ull) |
                          (ll_out ? 1ull << 29 : 0ull) | (hx ? 1ull << 28 : 0ull) | bytes,
                      __ATOMIC_SEQ_CST);
+    wc_flush();
     EnsureRunning(ks, kind);
     const double limit = timeout_s_ * 2 + 10;
     auto check = [&](uint32_t spins) {

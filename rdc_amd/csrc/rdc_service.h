@@ -82,6 +82,8 @@ private:
     double timeout_s_;
     SvcArgs args_;
     SvcBox* box_ = nullptr;       // host address
+    SvcIn* in_ = nullptr;         // host (CPU) address of the request side
+    bool in_vram_ = false;        // in_ is device memory written through the BAR (else pinned host memory)
     hipStream_t stream_ = nullptr;
     int kind_ = -1;               // (dtype, op) of the kernel launched last, -1 none
     bool launched_ = false;

@@ -41,6 +41,68 @@ __global__ void k_echo(const uint32_t* req, uint32_t* resp, int n) {
     }
 }
 
+// payload round trip: the request is B bytes as LL words {4 payload bytes,
+// k} (2B bytes) in the mailbox; the block (256 threads) polls the words until
+// every one carries k, writes B result bytes to the host, drains, then `done`
+__global__ __launch_bounds__(256) void k_echo_ll(const uint64_t* ll, uint32_t* out, uint32_t* done, int nwords, int n) {
+    const uint64_t deadline0 = wall_clock64() + 300000000ull;  // 3 s
+    __shared__ int s_ok;
+    for (int k = 1; k <= n; ++k) {
+        while (true) {
+            bool mine = true;
+            for (int w = threadIdx.x; w < nwords; w += 256)
+                mine = mine && (uint32_t)(__hip_atomic_load(ll + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32) == (uint32_t)k;
+            if (__syncthreads_and(mine)) break;
+            if (wall_clock64() > deadline0) return;
+        }
+        for (int w = threadIdx.x; w < nwords; w += 256)
+            out[w] = (uint32_t)__hip_atomic_load(ll + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(done, (uint32_t)k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    (void)s_ok;
+}
+
+static void run_ll(const char* name, uint64_t* ll_host_view, uint64_t* ll_dev_view, uint32_t* out, uint32_t* done,
+                   int bytes, int n) {
+    const int nwords = bytes / 4;
+    *done = 0;
+    for (int w = 0; w < nwords; ++w) ll_host_view[w] = 0;
+    __builtin_ia32_sfence();
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipLaunchKernelGGL(k_echo_ll, dim3(1), dim3(256), 0, s, ll_dev_view, out, done, nwords, n);
+    CK(hipGetLastError());
+    std::vector<double> t;
+    volatile uint32_t* d = done;
+    for (int k = 1; k <= n; ++k) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const uint64_t tag = (uint64_t)k << 32;
+        for (int w = 0; w < nwords; ++w) __atomic_store_n(ll_host_view + w, tag | (uint32_t)w, __ATOMIC_RELAXED);
+        __builtin_ia32_sfence();
+        const auto tl = t0 + std::chrono::seconds(4);
+        bool lost = false;
+        while (*d != (uint32_t)k)
+            if (std::chrono::steady_clock::now() > tl) {
+                lost = true;
+                break;
+            }
+        if (lost) {
+            CK(hipStreamSynchronize(s));
+            printf("{\"mailbox\": \"%s LL %d B\", \"error\": \"request %d lost\"}\n", name, bytes, k);
+            return;
+        }
+        t.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    CK(hipStreamSynchronize(s));
+    std::vector<double> w(t.begin() + n / 10, t.end());
+    std::sort(w.begin(), w.end());
+    printf("{\"mailbox\": \"%s LL %d B\", \"round_trips\": %zu, \"median_us\": %.3f, \"p10_us\": %.3f, \"p90_us\": %.3f}\n",
+           name, bytes, w.size(), w[w.size() / 2], w[w.size() / 10], w[w.size() * 9 / 10]);
+    fflush(stdout);
+}
+
 struct Ctx {
     hsa_agent_t gpu{}, cpu{};
     hsa_amd_memory_pool_t pool{};
@@ -117,6 +179,11 @@ int main(int argc, char** argv) {
     uint32_t* req = nullptr;
     CK(hipHostMalloc(reinterpret_cast<void**>(&req), 4096, hipHostMallocUncached));
     run("host", req, req, resp, n);
+    uint64_t* llh = nullptr;
+    uint32_t* outh = nullptr;
+    CK(hipHostMalloc(reinterpret_cast<void**>(&llh), 1 << 16, hipHostMallocUncached));
+    CK(hipHostMalloc(reinterpret_cast<void**>(&outh), 1 << 16, hipHostMallocUncached));
+    for (int b : {4, 1024, 4096}) run_ll("host", llh, llh, outh, resp, b, n / 4);
     // 2) VRAM request word, written by the CPU through the BAR: the GPU's
     //    fine-grained pool, then its coarse-grained one
     for (int variant = 0; variant < 4; ++variant) {
@@ -140,6 +207,13 @@ int main(int argc, char** argv) {
             continue;
         }
         run(name, static_cast<uint32_t*>(v), static_cast<uint32_t*>(v), resp, n);
+        if (uc && fine) {
+            void* lv = nullptr;
+            if (hsa_amd_memory_pool_allocate(c.pool, 1 << 16, HSA_AMD_MEMORY_POOL_UNCACHED_FLAG, &lv) == HSA_STATUS_SUCCESS &&
+                hsa_amd_agents_allow_access(2, both, nullptr, lv) == HSA_STATUS_SUCCESS)
+                for (int b : {4, 1024, 4096})
+                    run_ll(name, static_cast<uint64_t*>(lv), static_cast<uint64_t*>(lv), outh, resp, b, n / 4);
+        }
     }
     return 0;
 }
