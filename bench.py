@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bytes", type=int, default=1 << 30, help="buffer size per GPU")
     ap.add_argument("--dtype", default="float32", choices=sorted(DTYPES))
-    ap.add_argument("--algo", default="auto", choices=["auto", "mesh", "mesh_pull", "ring", "oneshot"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "mesh", "mesh_pull", "ring", "oneshot", "direct"])
     ap.add_argument("--buckets", type=int, default=1,
                     help="N>1: split the buffer into this many equal buckets (cfg5: --buckets 1024)")
     ap.add_argument("--unfused", action="store_true", help="buckets as separate allreduce calls (no coalescing)")
@@ -85,7 +85,7 @@ def load_traffic(kernel_key):
 def hbm_model(lib, world, count, dt_enum, algo_name):
     """RdcPlanHbmBytes for the schedule the timed launches used: per-rank
     (max) and all-rank loads / stores of one allreduce, or None."""
-    algo = {"ring": 1, "mesh": 2, "oneshot": 3, "tree": 4, "mesh_pull": 5}.get(algo_name)
+    algo = {"ring": 1, "mesh": 2, "oneshot": 3, "tree": 4, "mesh_pull": 5, "direct": 6}.get(algo_name)
     if algo is None:
         return None
     out = (ctypes.c_uint64 * 5)()
@@ -329,7 +329,7 @@ def parity_checks(lib, comm, S, world, rank, sp, dist, torch, out, budget=None):
     """Bit-exact checks at the bench's own shapes (after all timing), each on
     fresh synthetic inputs, every key its own boolean (AND over ranks):
 
-    * cfg3_mesh / cfg3_ring / cfg3_mesh_pull / cfg4_fp16: ONE allreduce of the whole S-byte
+    * cfg3_direct / cfg3_mesh / cfg3_ring / cfg3_mesh_pull / cfg4_fp16: ONE allreduce of the whole S-byte
       buffer.  Every rank hashes its WHOLE result (sha256) and the ranks
       compare digests; rank r compares Split chunk r of its result, every
       element, with the oracle's ring order.  Identical digests + every chunk
@@ -393,8 +393,9 @@ def parity_checks(lib, comm, S, world, rank, sp, dist, torch, out, budget=None):
             return False
         return True
 
-    for name, dt, algo, tdt in (("cfg3_mesh", 6, 2, torch.float32), ("cfg3_ring", 6, 1, torch.float32),
-                                ("cfg3_mesh_pull", 6, 5, torch.float32), ("cfg4_fp16", 10, 0, torch.float16)):
+    for name, dt, algo, tdt in (("cfg3_direct", 6, 6, torch.float32), ("cfg3_mesh", 6, 2, torch.float32),
+                                ("cfg3_ring", 6, 1, torch.float32), ("cfg3_mesh_pull", 6, 5, torch.float32),
+                                ("cfg4_fp16", 10, 0, torch.float16)):
         if not should_run(name, 20):
             continue
         t0 = time.perf_counter()
@@ -405,6 +406,10 @@ def parity_checks(lib, comm, S, world, rank, sp, dist, torch, out, budget=None):
         fill(t, count, dt, seed, rank)
         check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(t.data_ptr()), count, dt, 2, algo, sp))
         sync_check(comm, sp, dist, torch)
+        ll = (ctypes.c_uint64 * 6)()
+        check_call(lib.RdcCommLastLaunch(comm.handle, ll))
+        out.setdefault("schedule", {})[name] = {1: "ring", 2: "mesh", 3: "oneshot", 4: "tree", 5: "mesh_pull",
+                                                6: "direct"}.get(int(ll[5]), int(ll[5]))
         u8 = host_u8(t)
         del t
         lo, hi = O.split(count, world)[rank]
@@ -577,7 +582,7 @@ def trace_roles(lib, comm, buf, count, dt_enum, sp, dist, torch):
     dump = os.environ.get("RDC_BENCH_TRACE_DUMP")  # per-rank raw {start, end} ticks per block
     if dump:
         np.save("%s.rank%d.npy" % (dump, dist.get_rank()), np.concatenate([[grid, s, r, g, tile, algo], t.ravel()]))
-    names = {1: "ring", 2: "mesh", 3: "oneshot", 5: "mesh_pull"}
+    names = {1: "ring", 2: "mesh", 3: "oneshot", 5: "mesh_pull", 6: "direct"}
     roles = {"all": (0, grid)} if algo not in (2, 5) else {"scatter": (0, s), "reduce": (s, s + r),
                                                            "gather": (s + r, grid)}
     vals = []
@@ -698,7 +703,7 @@ def main():
         dist.init_process_group("gloo")
         rdc_amd.init([])          # RANK/WORLD_SIZE + MASTER_ADDR:MASTER_PORT+1 bootstrap
         comm = rdc_amd.get_comm("main")
-        algo = {"auto": 0, "ring": 1, "mesh": 2, "oneshot": 3, "mesh_pull": 5}[args.algo]
+        algo = {"auto": 0, "ring": 1, "mesh": 2, "oneshot": 3, "mesh_pull": 5, "direct": 6}[args.algo]
         K = max(1, args.buckets)
         if K == 1:
             buf = torch.empty(count, dtype=tdtype, device="cuda")
@@ -797,7 +802,7 @@ def main():
     if world > 1:  # the schedule and launch shape the library used for the timed launches
         ll = (ctypes.c_uint64 * 6)()
         if _LIB.RdcCommLastLaunch(comm.handle, ll) == 0:
-            timed_algo = {1: "ring", 2: "mesh", 3: "oneshot", 4: "tree", 5: "mesh_pull"}.get(int(ll[5]))
+            timed_algo = {1: "ring", 2: "mesh", 3: "oneshot", 4: "tree", 5: "mesh_pull", 6: "direct"}.get(int(ll[5]))
             timed_launch = {"schedule": timed_algo, "grid": int(ll[0]), "scatter_blocks": int(ll[1]),
                             "reduce_blocks": int(ll[2]), "gather_blocks": int(ll[3]), "tile_bytes": int(ll[4])}
     if world > 1:
@@ -856,14 +861,18 @@ def main():
     if multi:
         roles = guarded("role_timeline", lambda: trace_roles(_LIB, comm, buf, count, dt_enum, sp, dist, torch),
                         need_s=2)
-    if multi:
-        del buf  # room for the other configs' buffers
-        torch.cuda.empty_cache()
     if multi and f32 and not args.no_check:
+        # before the timed buffer is freed: the direct schedule does not
+        # export an address it exported for another allocation (a freed
+        # buffer's address handed out again falls back to the scratch
+        # schedules), so the direct check's buffer must be a fresh address
         part_c = {}
         checks = guarded("parity_checks", lambda: parity_checks(_LIB, comm, S, world, rank, sp, dist, torch, part_c,
                                                                 budget),
                          partial=part_c, need_s=30)
+    if multi:
+        del buf  # room for the other configs' buffers
+        torch.cuda.empty_cache()
     if multi and args.ring_steps > 0:
         # the reference's own schedule on a buffer of the same size (same
         # bits, one link direction per GPU).  Grids are clamped to what stays

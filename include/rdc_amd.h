@@ -164,6 +164,13 @@ int RdcCommIRecv(void** wc, void* comm, void* buf, size_t bytes, int src, void* 
  * the kernels (a peer that never joins) surface at RdcCommCheck. */
 int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op, void* stream);
 /* algo: 0 auto, 1 ring (the reference schedule), 2 mesh (all links, pushed by remote stores),
+ * 6 direct (registered buffers, one process per rank: every rank's buffer is mapped into every
+ * peer through HIP IPC once per allocation — a host rendezvous over shared memory agrees on the
+ * buffers each call — and owner r folds chunk r straight out of the n buffers and writes the
+ * result back into all of them: no scratch, one read and one write of each buffer; falls back
+ * to the automatic rule on every rank when any buffer cannot be mapped, the addresses differ mod
+ * 16, the stream is being captured or the ranks share one process; RDC_DIRECT_BYTES=<n> takes it
+ * automatically from n bytes),
  * 5 pull-mode mesh (the same exchange by remote loads: ranks stage their chunks in their own
  * scratch, owners load and fold, peers load the results; RdcCommAutotune times it against
  * the push mesh), 3 one-shot (small buffers:
@@ -233,10 +240,20 @@ int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t t
  * consumed scratch bytes once more.  No reference counterpart. */
 int RdcCommSetPoison(void* comm, int on);
 
+/* The direct schedule (algo 6) maps each peer's buffer into this process once
+ * per allocation and keeps the mapping while the communicator lives; a
+ * mapping keeps the peer's allocation alive after the peer frees it, and an
+ * allocation at an address this rank exported before for another allocation
+ * is not exported again (those calls take the scratch schedules).  This
+ * closes all of this rank's mappings (after waiting for the device) and turns
+ * the direct schedule off for the communicator, releasing the peers' freed
+ * allocations.  Call it on every rank.  No reference counterpart. */
+int RdcCommDirectRelease(void* comm);
+
 /* Autotune (collective: every rank of `comm`, same arguments, no collective in
- * flight; blocks the host): time the ring, the mesh pushed and pulled (RDC_ALGO_MESH_PULL) and
- * (where it fits half a
- * slot) the one-shot schedule, then the launch shapes of the fastest, for
+ * flight; blocks the host): time the ring, the mesh pushed and pulled (RDC_ALGO_MESH_PULL),
+ * (where it fits half a slot) the one-shot schedule and (ranks in processes of
+ * their own) the direct schedule, then the launch shapes of the fastest, for
  * `bytes` of `dtype` on this node — mesh: role split, then grid, then
  * tiles per reduce block; ring: grid, then tiles per block (a granularity, so
  * the chosen tiles scale with later buffers' sizes) — `reps` Max allreduces of synthetic data each on a scratch
@@ -351,7 +368,7 @@ int RdcPlanHostPieceRanges(int n, size_t count, int dtype, uint64_t lo, uint64_t
  * oneshot_bytes = RDC_ONESHOT_BYTES (0 = the default size / rank-aware rule). */
 int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_bytes);
 /* HBM byte model of one allreduce of `count` elements over n ranks with
- * schedule `algo` (1 ring, 2 mesh, 3 one-shot, 4 tree, 5 pull-mode mesh): the
+ * schedule `algo` (1 ring, 2 mesh, 3 one-shot, 4 tree, 5 pull-mode mesh, 6 direct): the
  * bytes the kernels load and store, counted per access as their loops issue
  * them, a remote store or load counted at the rank that issues it.  out5 = {read bytes, write bytes
  * (both the most of any rank), read bytes, write bytes (both summed over the

@@ -64,6 +64,7 @@ def _load():
         "RdcCommTraceNext": (i, [vp, vp, sz]),
         "RdcCommTune": (i, [vp, i, i, i, sz]),
         "RdcCommSetPoison": (i, [vp, i]),
+        "RdcCommDirectRelease": (i, [vp]),
         "RdcCommAutotune": (i, [vp, sz, i, i, vp, vp, i, ctypes.POINTER(i), ctypes.POINTER(i)]),
         "RdcCommLastLaunch": (i, [vp, ctypes.POINTER(u64)]),
         "RdcCommLaunchCounter": (i, [vp, ctypes.POINTER(u64)]),

@@ -51,9 +51,9 @@ class WorkComp(object):
 def _is_tensor(x):
     return hasattr(x, "data_ptr") and hasattr(x, "is_cuda")
 
-ALGO_AUTO, ALGO_RING, ALGO_MESH, ALGO_ONESHOT, ALGO_TREE, ALGO_MESH_PULL = 0, 1, 2, 3, 4, 5
+ALGO_AUTO, ALGO_RING, ALGO_MESH, ALGO_ONESHOT, ALGO_TREE, ALGO_MESH_PULL, ALGO_DIRECT = 0, 1, 2, 3, 4, 5, 6
 _ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "mesh": ALGO_MESH, "oneshot": ALGO_ONESHOT, "tree": ALGO_TREE,
-          "mesh_pull": ALGO_MESH_PULL}
+          "mesh_pull": ALGO_MESH_PULL, "direct": ALGO_DIRECT}
 
 
 class Comm(object):
@@ -200,6 +200,13 @@ class Comm(object):
         before the producer's next publish lands NaN / all-ones words."""
         check_call(_LIB.RdcCommSetPoison(self.handle, 1 if on else 0))
 
+    def direct_release(self):
+        """Close this rank's mappings of peer buffers of the direct schedule
+        and turn the schedule off for this communicator (RdcCommDirectRelease):
+        call on every rank to release peers' freed allocations that the
+        mappings keep alive."""
+        check_call(_LIB.RdcCommDirectRelease(self.handle))
+
     def autotune(self, nbytes, dtype=None, reps=3, stream=None):
         """Collective (every rank, same arguments): time the ring, the mesh and
         (where it fits) the one-shot, then the launch shapes of the fastest for allreduces of `nbytes`
@@ -222,7 +229,7 @@ class Comm(object):
                                         ctypes.byref(best)))
 
         def row(c):
-            return {"schedule": {1: "ring", 2: "mesh", 3: "oneshot", 5: "mesh_pull"}.get(c.algo, c.algo),
+            return {"schedule": {1: "ring", 2: "mesh", 3: "oneshot", 5: "mesh_pull", 6: "direct"}.get(c.algo, c.algo),
                     "split": [c.mesh_s16, c.mesh_r16], "grid": c.max_blocks or "auto",
                     "tiles_per_block": c.tiles_per_block or "auto", "ms": round(c.ms, 4),
                     "spread_ms": [round(c.ms_min, 4), round(c.ms_max, 4)]}

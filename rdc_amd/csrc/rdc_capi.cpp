@@ -84,6 +84,7 @@ void set_param(Manager& m, const char* name, const char* val) {
     else if (k == "RDC_ALGO") {
         std::string v(val);
         m.cfg.algo = v == "ring" ? RDC_ALGO_RING : v == "mesh" ? RDC_ALGO_MESH : v == "mesh_pull" ? RDC_ALGO_MESH_PULL
+                     : v == "direct" ? RDC_ALGO_DIRECT
                      : v == "oneshot" ? RDC_ALGO_ONESHOT : RDC_ALGO_AUTO;
         // (the tree is chosen by size through rdc_reduce_ring_mincount, as in the reference)
     } else if (k == "RDC_NBLOCKS") m.cfg.max_blocks = atoi(val);
@@ -104,6 +105,7 @@ void set_param(Manager& m, const char* name, const char* val) {
     }
     else if (k == "RDC_FUSE_BYTES_DIRECT") m.cfg.fuse_bytes_direct = std::max<size_t>(parse_unit(val), 1);
     else if (k == "RDC_POISON_SCRATCH") m.cfg.poison = atoi(val) != 0 ? 1 : 0;
+    else if (k == "RDC_DIRECT_BYTES") m.cfg.direct_min = parse_unit(val);
     else if (k == "RDC_P2P_SLOT_BYTES") m.cfg.p2p_slot_bytes = std::max<size_t>(parse_unit(val) / 4096 * 4096, 4096);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
     // to subsystems outside the device path and are accepted silently
@@ -216,7 +218,7 @@ int RdcInit(int argc, char** argv) {
                                      "RDC_BOOTSTRAP_TIMEOUT", "RDC_ONESHOT_BYTES", "RDC_FUSE_BYTES",
                                      "RDC_P2P_SLOT_BYTES", "RDC_COALESCE_FUSED", "RDC_HOST_ZC_BYTES",
                                      "RDC_FUSE_BYTES_DIRECT", "RDC_BCAST_SPLIT_BYTES", "RDC_MESH_SPLIT",
-                                     "RDC_POISON_SCRATCH"};
+                                     "RDC_POISON_SCRATCH", "RDC_DIRECT_BYTES"};
         for (const char* k : keys) env_param(m, k);
         m.env_loaded = true;
         for (int i = 0; i < argc; ++i) {
@@ -553,7 +555,7 @@ int RdcCommAllreduce(void* comm, void* dev_buf, size_t count, int dtype, int op,
 
 int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int op, int algo, void* stream) {
     return guard([&] {
-        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_MESH_PULL) throw std::invalid_argument("rdc: bad algo");
+        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_DIRECT) throw std::invalid_argument("rdc: bad algo");
         as_comm(comm)->Allreduce(dev_buf, count, dtype, op, static_cast<hipStream_t>(stream), algo);
     });
 }
@@ -572,6 +574,10 @@ int RdcCommTune(void* comm, int mesh_s16, int mesh_r16, int max_blocks, size_t t
 
 int RdcCommSetPoison(void* comm, int on) {
     return guard([&] { as_comm(comm)->SetPoison(on != 0); });
+}
+
+int RdcCommDirectRelease(void* comm) {
+    return guard([&] { as_comm(comm)->DirectUnmapAll(); });
 }
 
 int RdcCommAutotune(void* comm, size_t bytes, int dtype, int reps, void* stream, RdcTuneCand* cand, int max_cand,
@@ -749,7 +755,7 @@ int RdcPlanHbmBytes(int n, size_t count, int dtype, int algo, uint64_t* out5) {
         const size_t esz = rdc_dtype_size(dtype);
         if (n < 1 || n > RDC_MAX_RANKS || esz == 0 || !out5 ||
             (algo != RDC_ALGO_RING && algo != RDC_ALGO_MESH && algo != RDC_ALGO_ONESHOT && algo != RDC_ALGO_TREE &&
-             algo != RDC_ALGO_MESH_PULL))
+             algo != RDC_ALGO_MESH_PULL && algo != RDC_ALGO_DIRECT))
             throw std::invalid_argument("rdc: bad argument");
         const HbmBytes h = ModelHbmBytes(n, count, esz, algo);
         out5[0] = h.read_max;

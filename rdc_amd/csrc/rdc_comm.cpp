@@ -67,7 +67,7 @@ void dbg(const char* fmt, int rank, const char* what) {
     }
 }
 
-constexpr int kPlanKeys = 19;  // PlanKey below; sizes PeerInfo::plan
+constexpr int kPlanKeys = 20;  // PlanKey below; sizes PeerInfo::plan
 
 struct PeerInfo {
     uint64_t channel;   // id of the live channel this rank would share (0 = none)
@@ -108,7 +108,7 @@ void PlanKey(const CommConfig& c, uint64_t tune_hash, uint64_t (&k)[kPlanKeys]) 
                                    (uint64_t)SmallService::ShareMax(),
                                    (uint64_t)HostPieceBytes() | ((uint64_t)HostPieceRamp() << 63), tune_hash,
                                    (uint64_t)HostInlineBytes(), (uint64_t)(HostBalanceSetting() + 1),
-                                   SmallService::HxBytes()};
+                                   SmallService::HxBytes(), (uint64_t)c.direct_min};
     memcpy(k, v, sizeof(v));
 }
 const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYTES", "RDC_ONESHOT_BYTES",
@@ -117,7 +117,7 @@ const char* kPlanKeyNames[kPlanKeys] = {"RDC_ALGO", "RDC_NBLOCKS", "RDC_TILE_BYT
                                         "rdc_reduce_ring_mincount", "RDC_SCRATCH_BYTES", "RDC_HOST_SERVICE",
                                         "RDC_HOST_SERVICE_SHARE_MAX", "RDC_HOST_PIECE_BYTES / RDC_HOST_PIECE_RAMP",
                                         "RDC_TUNE_FILE (set or not)", "RDC_HOST_INLINE_BYTES", "RDC_HOST_BALANCE",
-                                        "RDC_HOST_SERVICE_HX_BYTES"};
+                                        "RDC_HOST_SERVICE_HX_BYTES", "RDC_DIRECT_BYTES"};
 
 // Autotune results kept across runs (RDC_TUNE_FILE): one line per winner,
 // "rdc-tune 2 <ranks> <cus> <ranks per gpu> <size class> <algo> <s16> <r16>
@@ -149,7 +149,7 @@ std::vector<TuneEntry> read_tune_file(const std::string& path) {
                    &e.s16, &e.r16, &e.grid, &e.tpb, &ms) == 11 &&
             ver == 2 && e.rpg >= 1 && e.cls >= 0 && e.cls < 64 &&
             (e.algo == RDC_ALGO_RING || e.algo == RDC_ALGO_MESH || e.algo == RDC_ALGO_MESH_PULL ||
-             e.algo == RDC_ALGO_ONESHOT) && e.s16 >= 1 &&
+             e.algo == RDC_ALGO_ONESHOT || e.algo == RDC_ALGO_DIRECT) && e.s16 >= 1 &&
             e.r16 >= 1 && e.s16 + e.r16 <= 15 && e.grid >= 0 && e.tpb >= 0)
             out.push_back(e);
     }
@@ -172,6 +172,8 @@ std::vector<TuneEntry> shared_tune_table(Bootstrap* bs) {
     bs->broadcast(&msg, sizeof(msg), 0);
     return std::vector<TuneEntry>(msg.e, msg.e + std::max(0, std::min(msg.count, kTuneEntriesMax)));
 }
+
+size_t round_up_bytes(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // `bytes` of POSIX shared memory every rank of bs maps and registers for its
 // device (hipHostRegister `flags`): rank 0 creates it, every rank maps it,
@@ -323,12 +325,15 @@ Channel::~Channel() {
                 if (peer_flags[p]) (void)hipIpcCloseMemHandle(peer_flags[p]);
                 if (peer_svc_region[p]) (void)hipIpcCloseMemHandle(peer_svc_region[p]);
             }
+        for (auto& m : dmaps) (void)hipIpcCloseMemHandle(m.second);  // registered peers' buffers
+        dmaps.clear();
         try {
             bs->barrier();  // every importer closed its mapping
         } catch (...) {
         }
     }
     if (last_ev) (void)hipEventDestroy(last_ev);
+    if (tune_buf) (void)hipFree(tune_buf);
     if (scratch) (void)hipFree(scratch);
     if (scratch_ag) (void)hipFree(scratch_ag);
     if (flags) (void)hipFree(flags);
@@ -709,6 +714,9 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     }
     if (!share) c->Alias();  // the aliases now include the peers' mappings
     c->p2p_ctl_ = map_p2p_ctl(bs);
+    if (!share)  // registered-buffer rendezvous slots, [2 parities][n]
+        ch->dreg = map_shared_host(bs, round_up_bytes(2 * (size_t)c->n_ * sizeof(DirectDesc), 4096), "direct",
+                                   hipHostRegisterDefault);
     if (!share && svc_all && SmallService::HxBytes() > 0)  // the same branch on every rank (agreed above)
         ch->svc_hx = map_shared_host(bs, svc_hx_bytes(c->n_), "svc",
                                      hipHostRegisterMapped | hipHostRegisterPortable | hipExtHostRegisterUncached);
@@ -857,12 +865,15 @@ WorkComp* Communicator::IRecv(void* buf, size_t bytes, int src, hipStream_t afte
 
 int Communicator::PickAlgo(int algo) const {
     if (algo == RDC_ALGO_AUTO) algo = cfg_.algo;
-    if (algo == RDC_ALGO_AUTO) algo = RDC_ALGO_MESH;
+    if (algo == RDC_ALGO_AUTO || algo == RDC_ALGO_DIRECT) algo = RDC_ALGO_MESH;
     return algo;
 }
 
 int Communicator::PickAlgo(int algo, uint64_t bytes) const {
     if (algo == RDC_ALGO_AUTO) algo = cfg_.algo;
+    // the registered-buffer schedule is taken before any plan (DirectEligible /
+    // AllreduceDirect); here it means "not possible for this call"
+    if (algo == RDC_ALGO_DIRECT) algo = RDC_ALGO_AUTO;
     if (algo == RDC_ALGO_AUTO) {
         algo = AutoAlgo(n_, bytes, layout(), cfg_.oneshot_push_max);
         // a schedule Autotune measured for this size class replaces the
@@ -870,7 +881,7 @@ int Communicator::PickAlgo(int algo, uint64_t bytes) const {
         // one-shot that does not fit half a slot falls back below)
         if (algo == RDC_ALGO_MESH || algo == RDC_ALGO_RING || algo == RDC_ALGO_ONESHOT) {
             const auto it = tuned_algo_.find(SizeClass(bytes));  // may be RDC_ALGO_MESH_PULL
-            if (it != tuned_algo_.end()) algo = it->second;
+            if (it != tuned_algo_.end() && it->second != RDC_ALGO_DIRECT) algo = it->second;
         }
     }
     if (algo == RDC_ALGO_ONESHOT && !OneshotEligible(n_, bytes, layout(), (uint64_t)-1))
@@ -975,6 +986,10 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
         LaunchTree(ks, static_cast<char*>(buf), (uint64_t)count * esz, stream);
         return;
     }
+    if (DirectEligible(algo, (uint64_t)count * esz, stream) &&
+        AllreduceDirect(ks, static_cast<char*>(buf), (uint64_t)count * esz, esz, stream))
+        return;
+    if (algo == RDC_ALGO_DIRECT) algo = RDC_ALGO_AUTO;  // not registrable here: the scratch schedules
     int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
     SplitRanges((int64_t)count, n_, cb, ce);  // utils::Split (include/utils/utils.h:59-70)
     uint64_t off[RDC_MAX_RANKS] = {0}, len[RDC_MAX_RANKS] = {0};
@@ -983,6 +998,224 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
         len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
     }
     LaunchRanges(ks, static_cast<char*>(buf), off, len, (uint64_t)count * esz, esz, algo, stream);
+}
+
+// ------------------------------------------------- registered buffers ----
+// Every check here uses values identical on every rank (the schedule asked
+// for, the byte count, the channel kind, whether the stream is being
+// captured — ranks capture alike), so either all ranks rendezvous or none.
+bool Communicator::DirectEligible(int algo, uint64_t bytes, hipStream_t stream) const {
+    if (!ch_ || !ch_->dreg || n_ < 2) return false;  // multi-process channels only
+    bool want = algo == RDC_ALGO_DIRECT || (algo == RDC_ALGO_AUTO && cfg_.algo == RDC_ALGO_DIRECT);
+    if (algo == RDC_ALGO_AUTO && cfg_.algo == RDC_ALGO_AUTO) {
+        const auto it = tuned_algo_.find(SizeClass(bytes));
+        want = it != tuned_algo_.end() ? it->second == RDC_ALGO_DIRECT
+                                       : cfg_.direct_min > 0 && bytes >= cfg_.direct_min;
+    }
+    if (!want) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return cs == hipStreamCaptureStatusNone;  // a rendezvous per replay is not possible
+}
+
+namespace {
+// RDC_DIRECT_LOG=1: one stderr line per export and mapping of the direct
+// schedule, for debugging the mapping cache
+constexpr size_t kDirectExportsMax = 4096;  // allocations one rank exports over a channel's life
+constexpr size_t kDirectMapsMax = 4096;     // peer allocations one rank maps
+
+bool direct_log() {
+    static const bool on = [] {
+        const char* e = getenv("RDC_DIRECT_LOG");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
+// spin until every slot of `slots` carries `stamp` in the field `field`
+// (release-stored last by its owner); false on timeout
+bool rendezvous_wait(DirectDesc* slots, int n, uint64_t DirectDesc::*field, uint64_t stamp, double timeout_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int p = 0; p < n; ++p) {
+        uint32_t spins = 0;
+        while (__atomic_load_n(&(slots[p].*field), __ATOMIC_ACQUIRE) != stamp) {
+            __builtin_ia32_pause();
+            if ((++spins & 1023) == 0 &&
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+                return false;
+        }
+    }
+    return true;
+}
+}  // namespace
+
+bool Communicator::AllreduceDirect(const KernelSet& ks, char* buf, uint64_t bytes, size_t esz, hipStream_t stream) {
+    Channel& ch = *ch_;
+    const uint64_t call = ++ch.dcalls;  // the same on every rank (DirectEligible)
+    DirectDesc* slots = reinterpret_cast<DirectDesc*>(ch.dreg.get()) + (call & 1) * (uint64_t)n_;
+    DirectDesc& me = slots[rank_];
+    // 1) this rank's buffer: its allocation, offset and IPC handle.
+    //
+    // Mapping life cycle (measured round 5, tools/direct_check.py,
+    // profiles/r05/direct/): a HIP IPC handle names an allocation by
+    // (exporting process, base address), and an importer that still holds a
+    // mapping from an earlier allocation at the same base gets that old
+    // mapping back — stale memory — when it opens the new handle.  Closing
+    // the old mapping first fixes the data, but re-mapping into address
+    // ranges just unmapped faulted the GPU at n = 3.  So mappings are never
+    // closed while the channel lives (RdcCommDirectRelease / channel close),
+    // and an allocation whose base address — or any byte of whose range —
+    // this rank exported before for ANOTHER allocation is not exported: the
+    // call falls back to the scratch schedules on every rank.  The cost: a
+    // freed allocation stays alive while peers keep its mapping.
+    me.valid = 0;
+    me.bytes = bytes;
+    me.mis16 = (uint64_t)(uintptr_t)buf & 15;
+    if (!ch.direct_off) {
+        unsigned long long id = 0;
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, buf) == hipSuccess && at.type == hipMemoryTypeDevice &&
+            hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)buf) == hipSuccess &&
+            hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)buf) == hipSuccess && base != nullptr &&
+            (char*)buf + bytes <= (char*)base + size) {
+            const uintptr_t b = (uintptr_t)base;
+            const char* why = nullptr;
+            auto it = ch.dexports.find(b);
+            if (it != ch.dexports.end()) {
+                if (it->second.id != (uint64_t)id) why = "address reused";
+            } else {
+                // an earlier export overlapping [b, b + size) is a dead allocation
+                auto nx = ch.dexports.lower_bound(b);
+                if ((nx != ch.dexports.end() && nx->first < b + size) ||
+                    (nx != ch.dexports.begin() && std::prev(nx)->first + std::prev(nx)->second.size > b))
+                    why = "range reused";
+                else if (ch.dexports.size() >= kDirectExportsMax)
+                    why = "export table full";
+                else {
+                    Channel::DirectExport ex;
+                    ex.id = (uint64_t)id;
+                    ex.size = size;
+                    if (hipIpcGetMemHandle(&ex.handle, base) == hipSuccess) it = ch.dexports.emplace(b, ex).first;
+                    else why = "no IPC handle";
+                }
+            }
+            if (direct_log())
+                fprintf(stderr, "rdc-direct r%d call %llu: buffer %p id %llu base %p size %zu%s%s\n", rank_,
+                        (unsigned long long)call, (void*)buf, id, (void*)base, size, why ? ": not exported, " : "",
+                        why ? why : "");
+            if (!why) {
+                me.buffer_id = (uint64_t)id;
+                me.offset = (uint64_t)((char*)buf - (char*)base);
+                me.handle = it->second.handle;
+                me.valid = 1;
+            }
+        }
+        (void)hipGetLastError();
+    }
+    __atomic_store_n(&me.stamp0, call, __ATOMIC_RELEASE);
+    if (!rendezvous_wait(slots, n_, &DirectDesc::stamp0, call, cfg_.timeout_s))
+        throw std::runtime_error("rdc: registered-buffer rendezvous timed out (a peer did not join the allreduce)");
+    // 2) every buffer usable and alike?  Then map the peers' (cached per allocation)
+    bool usable = true;
+    for (int p = 0; p < n_; ++p)
+        usable = usable && slots[p].valid && slots[p].bytes == bytes && slots[p].mis16 == me.mis16;
+    char* peer[RDC_MAX_RANKS] = {};
+    peer[rank_] = buf;
+    int ok = usable ? 1 : 0;
+    for (int p = 0; p < n_ && ok; ++p) {
+        if (p == rank_) continue;
+        auto key = std::make_pair(p, slots[p].buffer_id);
+        auto it = ch.dmaps.find(key);
+        if (it == ch.dmaps.end()) {
+            if (ch.dmaps.size() >= kDirectMapsMax) {  // full: no new mappings (fallback)
+                ok = 0;
+                break;
+            }
+            void* m = nullptr;
+            if (hipIpcOpenMemHandle(&m, slots[p].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !m) {
+                (void)hipGetLastError();
+                ok = 0;
+                break;
+            }
+            // a pointer this rank already holds for another allocation would
+            // be the stale mapping described above: never use it
+            bool dup = false;
+            for (auto& o : ch.dmaps) dup = dup || o.second == (char*)m;
+            if (direct_log())
+                fprintf(stderr, "rdc-direct r%d call %llu: open peer %d id %llu -> %p%s\n", rank_,
+                        (unsigned long long)call, p, (unsigned long long)slots[p].buffer_id, m,
+                        dup ? " (a mapping already held: not used)" : "");
+            if (dup) {
+                ok = 0;
+                break;
+            }
+            it = ch.dmaps.emplace(key, static_cast<char*>(m)).first;
+        }
+        peer[p] = it->second + slots[p].offset;
+    }
+    me.ok = ok;
+    __atomic_store_n(&me.stamp1, call, __ATOMIC_RELEASE);
+    if (!rendezvous_wait(slots, n_, &DirectDesc::stamp1, call, cfg_.timeout_s))
+        throw std::runtime_error("rdc: registered-buffer rendezvous timed out (a peer did not join the allreduce)");
+    for (int p = 0; p < n_; ++p) usable = usable && slots[p].ok;
+    if (!usable) return false;  // every rank saw the same slots: all fall back together
+    // 3) one launch: owner r folds chunk r of every buffer in place
+    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+    SplitRanges((int64_t)(bytes / esz), n_, cb, ce);
+    CollArgs a;
+    FillArgsCommon(&a);
+    a.kind = RDC_KIND_DIRECT;
+    a.user = buf;
+    for (int c = 0; c < n_; ++c) {
+        a.off[c] = (uint64_t)cb[c] * esz;
+        a.len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
+        a.cbuf[c] = peer[c];
+    }
+    const Shape sh = ShapeFor(bytes, RDC_ALGO_DIRECT);  // an Autotune'd grid, else the mesh's
+    const int grid_cap = LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : mesh_blocks(),
+                                    ks.occupancy(RDC_KIND_DIRECT, n_));
+    // ~2 tiles per block, 64 KiB .. 4 MiB, a multiple of 256 B
+    uint64_t tile = a.len[rank_] / (2 * (uint64_t)grid_cap) + 1;
+    tile = std::min<uint64_t>(std::max<uint64_t>(tile, 64 << 10), 4 << 20);
+    tile = (tile + 255) & ~(uint64_t)255;
+    const int tiles = (int)std::max<uint64_t>(1, (a.len[rank_] + tile - 1) / tile);
+    a.tile_bytes = tile;
+    a.tiles[rank_] = a.len[rank_] ? tiles : 0;
+    const int grid = std::max(1, std::min(tiles, grid_cap));
+    if (notify_) {
+        a.notify = notify_;
+        a.notify_val = notify_val_;
+        notify_ = nullptr;
+    }
+    last_launch_[0] = (uint64_t)grid;
+    last_launch_[1] = last_launch_[2] = last_launch_[3] = 0;
+    last_launch_[4] = tile;
+    last_launch_[5] = RDC_ALGO_DIRECT;
+    ++seq_;
+    log_launch(this, seq_, RDC_ALGO_DIRECT, bytes, grid, tile);
+    hip_check(ks.direct(a, grid, stream), "launch direct allreduce");
+    trace_ = nullptr;
+    return true;
+}
+
+// Closes every peer-buffer mapping of the direct schedule and turns the
+// schedule off for the channel (re-mapping into just-unmapped address ranges
+// faulted the GPU in round 5's tests, so nothing is mapped again).  A mapping
+// keeps the peer's allocation alive after the peer frees it: this releases
+// them.  Every rank should call it (a rank that has it off makes every call
+// fall back anyway).
+void Communicator::DirectUnmapAll() {
+    if (!ch_) return;
+    if (!ch_->dmaps.empty()) (void)hipDeviceSynchronize();  // no launch still reads through them
+    for (auto& m : ch_->dmaps) (void)hipIpcCloseMemHandle(m.second);
+    ch_->dmaps.clear();
+    ch_->direct_off = true;
+    (void)hipGetLastError();
 }
 
 void Communicator::AllreduceRanges(void* buf, const uint64_t* off, const uint64_t* len, int dtype, int op,
@@ -1429,15 +1662,33 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     const std::map<int, Shape> saved_shapes = tuned_;
     const std::map<int, int> saved_algos = tuned_algo_;
     int nc = 0;
+    // the direct schedule maps every rank's buffer into its peers: then the
+    // buffer is the channel's own hipMalloc allocation (stream-ordered pool
+    // memory has no IPC handle), kept for later autotunes — freed, it would
+    // stay alive in the peers' mappings and its address could not be
+    // exported again (AllreduceDirect)
+    const bool direct_cand = ch_ && ch_->dreg && !ch_->direct_off;
     auto release = [&] {
-        if (buf) (void)hipFreeAsync(buf, stream);
+        if (buf && !direct_cand) (void)hipFreeAsync(buf, stream);
         if (dms) (void)hipFreeAsync(dms, stream);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         (void)hipStreamSynchronize(stream);
     };
     try {
-        hip_check(hipMallocAsync(&buf, count * esz, stream), "autotune buffer");
+        if (direct_cand) {
+            if (ch_->tune_bytes < count * esz) {
+                hip_check(hipStreamSynchronize(stream), "sync");
+                if (ch_->tune_buf) hip_check(hipFree(ch_->tune_buf), "autotune buffer");
+                ch_->tune_buf = nullptr;
+                ch_->tune_bytes = 0;
+                hip_check(hipMalloc(&ch_->tune_buf, count * esz), "autotune buffer");
+                ch_->tune_bytes = count * esz;
+            }
+            buf = ch_->tune_buf;
+        } else {
+            hip_check(hipMallocAsync(&buf, count * esz, stream), "autotune buffer");
+        }
         // per-round times of one stage, agreed across ranks
         constexpr int kStageMax = 16;
         hip_check(hipMallocAsync(reinterpret_cast<void**>(&dms), sizeof(double) * kStageMax * kTuneRounds, stream),
@@ -1515,11 +1766,20 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
         add(rule, s0, r0, g0, t0);
         // (the mesh twice: pushed by remote stores and pulled by remote loads —
         // which direction the links serve faster is this node's answer)
-        for (int a : {RDC_ALGO_RING, RDC_ALGO_MESH, RDC_ALGO_MESH_PULL, RDC_ALGO_ONESHOT})
-            if (a != rule && (a != RDC_ALGO_ONESHOT || oneshot_fits)) add(a, s0, r0, g0, t0);
+        // (and the direct schedule on registered buffers where the ranks are
+        // processes: no scratch, each buffer read and written once)
+        for (int a : {RDC_ALGO_RING, RDC_ALGO_MESH, RDC_ALGO_MESH_PULL, RDC_ALGO_ONESHOT, RDC_ALGO_DIRECT})
+            if (a != rule && (a != RDC_ALGO_ONESHOT || oneshot_fits) && (a != RDC_ALGO_DIRECT || direct_cand))
+                add(a, s0, r0, g0, t0);
         int w = stage(lo);
         if (cand[w].algo == RDC_ALGO_ONESHOT) {
             // no roles or tiles to shape: the schedule is the result
+        } else if (cand[w].algo == RDC_ALGO_DIRECT) {
+            lo = nc;
+            add(RDC_ALGO_DIRECT, s0, r0, cand[w].grid, cand[w].tpb);
+            for (int bpc : {1, 2, 3, 4})  // (grid 0 = automatic = 2 per CU)
+                if (bpc * cus != (cand[lo].grid ? cand[lo].grid : 2 * cus)) add(RDC_ALGO_DIRECT, s0, r0, bpc * cus, 0);
+            w = stage(lo);
         } else if (cand[w].algo == RDC_ALGO_MESH || cand[w].algo == RDC_ALGO_MESH_PULL) {
             static const int kSplits[][2] = {{4, 8}, {3, 9}, {5, 8}, {6, 6}, {3, 10}, {2, 10}, {5, 7}};
             const int ma = cand[w].algo;

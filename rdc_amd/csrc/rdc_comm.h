@@ -42,6 +42,10 @@ struct CommConfig {
     // byte): allreduces of at most this many bytes take the reference's tree
     // order instead of the ring's (communicator_collective.cc:6-13)
     size_t ring_mincount = 1;
+    // RDC_DIRECT_BYTES: allreduces of at least this many bytes on multi-process
+    // channels use the registered-buffer schedule (RDC_ALGO_DIRECT) when every
+    // rank's buffer can be mapped (0 = only when asked for or autotuned)
+    size_t direct_min = 0;
     // RDC_POISON_SCRATCH=1: consumers overwrite every scratch range they
     // finished reading with 0xFF bytes (debug mode, rdc_device.h block_poison)
     int poison = 0;
@@ -104,6 +108,38 @@ struct Channel {
     hipEvent_t last_ev = nullptr;
     hipStream_t last_stream = nullptr;
     bool have_last = false;
+    // registered-buffer allreduce (RDC_ALGO_DIRECT, Communicator::AllreduceDirect):
+    // per-call rendezvous slots in shared host memory ([2 parities][n] DirectDesc,
+    // multi-process channels only), the rendezvous count, the peers' buffers
+    // mapped here (by (peer, HIP buffer id); open until the channel closes or
+    // RdcCommDirectRelease) and this rank's exported allocations by base
+    // address (kept for the channel's life: see AllreduceDirect)
+    std::shared_ptr<char> dreg;
+    uint64_t dcalls = 0;
+    std::map<std::pair<int, uint64_t>, char*> dmaps;
+    struct DirectExport {
+        hipIpcMemHandle_t handle;
+        uint64_t id = 0;
+        size_t size = 0;
+    };
+    std::map<uintptr_t, DirectExport> dexports;
+    bool direct_off = false;  // RdcCommDirectRelease ran: the direct schedule stays off
+    void* tune_buf = nullptr;  // Autotune's buffer, kept (peers map it) until the channel closes
+    size_t tune_bytes = 0;
+};
+
+// One rank's slot of the registered-buffer rendezvous (shared host memory).
+struct DirectDesc {
+    uint64_t stamp0;          // rendezvous number whose descriptor this slot holds (release-stored last)
+    uint64_t buffer_id;       // HIP_POINTER_ATTRIBUTE_BUFFER_ID of the buffer's allocation
+    uint64_t offset;          // buffer - allocation base
+    uint64_t bytes;
+    uint64_t mis16;           // buffer address % 16 (every rank's must agree)
+    int32_t valid;            // an exportable device allocation
+    int32_t ok;               // phase 1: every peer's buffer is mapped here
+    uint64_t stamp1;          // rendezvous number of `ok` (release-stored last)
+    hipIpcMemHandle_t handle;
+    char pad[64];
 };
 
 class Communicator {
@@ -174,6 +210,9 @@ public:
     // bytes (0 = auto).  Throws std::invalid_argument on a bad split.
     void Tune(int s16, int r16, int max_blocks, size_t tile_bytes);
     void SetPoison(bool on) { cfg_.poison = on ? 1 : 0; }
+    // closes this rank's mappings of peer buffers and turns the direct
+    // schedule off for this communicator's channel (RdcCommDirectRelease)
+    void DirectUnmapAll();
 
     // Collective (every rank, same arguments, no collective in flight): time
     // the schedules (ring, mesh, one-shot where it fits) and then the launch
@@ -285,6 +324,11 @@ private:
     const PackEntry& PackTable(void* const* bufs, const size_t* counts, int nbuf, size_t esz, hipStream_t stream);
     char* Image(uint64_t bytes, hipStream_t stream);
     void LaunchTree(const KernelSet& ks, char* buf, uint64_t total, hipStream_t stream);
+    // registered user buffers (k_direct): false when the rendezvous finds any
+    // rank's buffer unusable (the caller takes the scratch schedules; every
+    // rank decides alike)
+    bool DirectEligible(int algo, uint64_t bytes, hipStream_t stream) const;
+    bool AllreduceDirect(const KernelSet& ks, char* buf, uint64_t bytes, size_t esz, hipStream_t stream);
     void CoalescedTree(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, size_t esz,
                        hipStream_t stream);
     void CoalescedStaged(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, int dtype, int op,

@@ -30,15 +30,17 @@ enum {
     RDC_ALGO_ONESHOT = 3,  // small buffers: every rank pushes all of it, every rank folds (one hand-off)
     RDC_ALGO_TREE = 4,     // the reference's tree ORDER (TryAllreduceTree, buffers <= rdc_reduce_ring_mincount),
                            // moved like the one-shot: every rank folds all n inputs in the tree's order
-    RDC_ALGO_MESH_PULL = 5  // the mesh moved by remote LOADS: ranks stage their chunks in their own scratch,
-                            // owners pull and fold, peers pull the results (same fold order)
+    RDC_ALGO_MESH_PULL = 5,  // the mesh moved by remote LOADS: ranks stage their chunks in their own scratch,
+                             // owners pull and fold, peers pull the results (same fold order)
+    RDC_ALGO_DIRECT = 6      // registered user buffers: owners fold straight out of every rank's buffer and
+                             // write the result straight back (no scratch; multi-process, device buffers)
 };
 
 // launch kinds (recorded on the device: the next launch reads the previous kind)
 // (tree launches use the one-shot's slot protocol and record RDC_KIND_ONESHOT;
 // RDC_KIND_TREE only names the kernel in occupancy queries)
 enum { RDC_KIND_NONE = 0, RDC_KIND_MESH = 1, RDC_KIND_RING = 2, RDC_KIND_BCAST = 3, RDC_KIND_ALLGATHER = 4,
-       RDC_KIND_ONESHOT = 5, RDC_KIND_TREE = 6 };
+       RDC_KIND_ONESHOT = 5, RDC_KIND_TREE = 6, RDC_KIND_DIRECT = 7 };
 
 #define RDC_MAX_RANKS 16
 // 64-bit words from one hand-off flag to the next: 1 = packed (the default);

@@ -13,6 +13,7 @@ struct KernelSet {
     hipError_t (*ring)(const CollArgs& a, int grid, hipStream_t s);
     hipError_t (*oneshot)(const CollArgs& a, int grid, hipStream_t s);
     hipError_t (*tree)(const CollArgs& a, int grid, hipStream_t s);
+    hipError_t (*direct)(const CollArgs& a, int grid, hipStream_t s);  // registered user buffers (k_direct)
     hipError_t (*svc)(const SvcArgs& a, hipStream_t s);  // the small-allreduce service (one block)
     // resident blocks per CU of the kernel a launch of `kind` (RDC_KIND_MESH /
     // RING / ONESHOT / TREE) on n ranks uses (hipOccupancyMaxActiveBlocksPerMultiprocessor,

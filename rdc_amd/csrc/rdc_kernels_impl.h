@@ -611,6 +611,123 @@ __device__ __forceinline__ void mesh_pull_body(const CollArgs& a, uint64_t seq) 
     }
 }
 
+// ============================================ direct (registered buffers) ===
+// RDC_ALGO_DIRECT (Communicator::AllreduceDirect): every rank's user buffer
+// is mapped into every peer (HIP IPC, once per allocation; a host rendezvous
+// per call agrees on the buffers), so owner r folds chunk r straight out of
+// the n user buffers and writes the result straight back into all of them.
+// No scratch: each rank's kernels read its buffer once and write it once
+// (2 S of memory traffic per rank, against the pull mesh's (5n-2)/n S).
+// Hand-offs (rows of the ordinary flag array, tile 0):
+//   ready: first thing in its launch, rank q tells every owner r its buffer
+//          holds this launch's input (owner r's row q) — stream order made it so;
+//   done : launch_done's done words (every owner tile written and drained),
+//          and a direct launch ends only once every peer's done word arrived,
+//          so no owner reads or writes a rank's buffer after that rank's
+//          stream moves on.
+// Fold order per element: chunk r's ring order, as every schedule.  All ranks'
+// buffers are congruent mod 16 (checked at the rendezvous), so one 16-B path.
+template <int OP, typename T, int NMAX>
+__device__ __forceinline__ void direct_fold_range(const CollArgs& a, char* const* buf, uint64_t tlen) {
+    const int n = a.n, r = a.rank, f = a.fold[r];
+    const unsigned tid = threadIdx.x;
+    auto fold_elem = [&](uint64_t e) {
+        auto val = [&](int q) -> T {
+            return q == r ? *reinterpret_cast<const T*>(buf[q] + e) : ld_elem_sys<T>(buf[q] + e);
+        };
+        T acc = val((f - 1 + n) % n);
+        for (int k = 2; k <= n; ++k) acc = OpF<OP>::apply(val((f - k + n) % n), acc);
+        for (int q = 0; q < n; ++q) {
+            if (q == r) *reinterpret_cast<T*>(buf[q] + e) = acc;
+            else st_elem_wt<T>(buf[q] + e, acc);
+        }
+    };
+    const uint64_t mis16 = (uint64_t)(uintptr_t)buf[r] & 15;
+    uint64_t head = mis16 ? 16 - mis16 : 0;
+    if (head > tlen) head = tlen;
+    const uint64_t nvec = (tlen - head) >> 4;
+    const uint64_t tail = head + (nvec << 4);
+    {
+        const uint64_t nh = head / sizeof(T), nt = (tlen - tail) / sizeof(T);
+        if (tid < nh) fold_elem(tid * sizeof(T));
+        else if (tid >= 64 && tid - 64 < nt) fold_elem(tail + (tid - 64) * sizeof(T));
+    }
+    constexpr int U = NMAX <= 8 ? 2 : 1;
+    const uint64_t stride = kBlock;
+    for (uint64_t ib = 0; ib < nvec; ib += U * stride) {
+        const uint64_t i = ib + tid;
+        v4u v[U][NMAX];
+        bool live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) live[u] = i + u * stride < nvec;
+#pragma unroll
+        for (int k = 1; k <= NMAX; ++k) {
+            if (k <= n) {
+                const int q = (f - k + n) % n;  // x[f-1], x[f-2], ..., x[f]
+                if (q == r) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (live[u]) v[u][k - 1] = ld16_nt(buf[r] + head + (i + u * stride) * 16);
+                } else {
+                    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(buf[q] + head + ib * 16);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (live[u]) v[u][k - 1] = ld16_sys(rs, (uint32_t)((tid + u * stride) * 16));
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!live[u]) continue;
+            v4u acc = v[u][0];
+#pragma unroll
+            for (int k = 2; k <= NMAX; ++k)
+                if (k <= n) acc = reduce16<OP, T>(v[u][k - 1], acc);
+            v[u][0] = acc;
+        }
+#pragma unroll
+        for (int q = 0; q < NMAX; ++q) {
+            if (q >= n) continue;
+            if (q == r) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (live[u]) st16_nt(buf[r] + head + (i + u * stride) * 16, v[u][0]);
+            } else {
+                const __amdgpu_buffer_rsrc_t rs = wt_rsrc(buf[q] + head + ib * 16);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (live[u]) st16_wt(rs, (uint32_t)((tid + u * stride) * 16), v[u][0]);
+            }
+        }
+    }
+}
+
+template <int OP, typename T, int NMAX>
+__device__ __forceinline__ void direct_body(const CollArgs& a, uint64_t seq) {
+    const int n = a.n, r = a.rank;
+    Abort ab{a.err, wall_clock64() + a.timeout_ticks, a.poll_rmw};
+    __shared__ uint64_t* s_flags[RDC_MAX_RANKS];
+    __shared__ char* s_buf[RDC_MAX_RANKS];
+    // ready: this rank's buffer holds this launch's input (block 0, before any wait)
+    if (blockIdx.x == 0 && threadIdx.x < (unsigned)(n - 1))
+        flag_store(flag_word(a, (r + 1 + threadIdx.x) % n, (uint64_t)r * a.max_tiles), seq);
+    if (threadIdx.x < (unsigned)(n - 1))
+        s_flags[threadIdx.x] = flag_word(a, r, (uint64_t)((r + 1 + threadIdx.x) % n) * a.max_tiles);
+    if (threadIdx.x < (unsigned)n) s_buf[threadIdx.x] = a.cbuf[threadIdx.x] + a.off[r];
+    __syncthreads();
+    if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return;
+    __shared__ char* s_tile[RDC_MAX_RANKS];
+    for (int t = blockIdx.x; t < a.tiles[r]; t += gridDim.x) {
+        const uint64_t toff = (uint64_t)t * a.tile_bytes;
+        uint64_t tlen = a.len[r] - toff;
+        if (tlen > a.tile_bytes) tlen = a.tile_bytes;
+        if (threadIdx.x < (unsigned)n) s_tile[threadIdx.x] = s_buf[threadIdx.x] + toff;
+        __syncthreads();
+        direct_fold_range<OP, T, NMAX>(a, s_tile, tlen);
+        __syncthreads();  // s_tile is rewritten for the next tile
+    }
+}
+
 // ======================================================= ring allreduce ===
 // own[i] = OP(own[i], recv[i]) — reducer(src=reducebuf, dst=sendrecvbuf)
 // (communicator_collective.cc:174-176), element-wise head/tail + 16-B body.
@@ -1080,6 +1197,29 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint64_t seq) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int p = 0; p < a.n; ++p)
                 if (p != a.rank) flag_store(done_word(a, p, a.rank), seq);
+            if (a.kind == RDC_KIND_DIRECT) {
+                // registered buffers: every owner finished writing into this
+                // rank's buffer before its stream moves on (done words of this
+                // launch from every peer; bounded like every wait)
+                const uint64_t deadline = wall_clock64() + a.timeout_ticks;
+                bool gave_up = false;
+                for (int p = 0; p < a.n && !gave_up; ++p) {
+                    if (p == a.rank) continue;
+                    const uint64_t* w = done_word(a, a.rank, p);
+                    while (!seq_reached(flag_load(w), seq)) {
+                        if (wall_clock64() > deadline ||
+                            __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                            uint32_t expected = 0;
+                            __hip_atomic_compare_exchange_strong(a.err, &expected, (uint32_t)RDC_KERR_TIMEOUT_AG,
+                                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                            gave_up = true;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+            }
             __hip_atomic_store(a.launch_kind, (uint32_t)a.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.launch_ctr, seq_counter(seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the host reads the (sticky) error word here after a stream sync: no
@@ -1141,6 +1281,13 @@ __global__ __launch_bounds__(kBlock) void k_ring(CollArgs a) {
     launch_done(a, seq);
 }
 
+
+template <int OP, typename T, int NMAX>
+__global__ __launch_bounds__(kBlock) void k_direct(CollArgs a) {
+    uint64_t seq;
+    if (!launch_begin(a, &seq)) direct_body<OP, T, NMAX>(a, seq);
+    launch_done(a, seq);
+}
 
 // ================================================ small-allreduce service ===
 // One block per rank, resident while requests keep coming (rdc_service.h).
@@ -1563,6 +1710,13 @@ struct Kernels {
             hipLaunchKernelGGL((k_oneshot<OP, T, 16>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
         return hipGetLastError();
     }
+    static hipError_t direct(const CollArgs& a, int grid, hipStream_t s) {
+        if (a.n <= 8)
+            hipLaunchKernelGGL((k_direct<OP, T, 8>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
+        else
+            hipLaunchKernelGGL((k_direct<OP, T, 16>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
+        return hipGetLastError();
+    }
     static hipError_t ring(const CollArgs& a, int grid, hipStream_t s) {
         hipLaunchKernelGGL((k_ring<OP, T>), dim3(grid), dim3(kBlock), debug_lds_pad(), s, a);
         return hipGetLastError();
@@ -1587,12 +1741,13 @@ struct Kernels {
         return hipGetLastError();
     }
     static int occupancy(int kind, int n) {
-        // [mesh 8, mesh 16, oneshot 8, oneshot 16, ring, tree 8, tree 16]; 0 = not queried yet
-        static int cache[7] = {0, 0, 0, 0, 0, 0, 0};
+        // [mesh 8, mesh 16, oneshot 8, oneshot 16, ring, tree 8, tree 16, direct 8, direct 16]; 0 = not queried yet
+        static int cache[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         const int wide = n > 8 ? 1 : 0;
         const int slot = kind == RDC_KIND_RING      ? 4
                          : kind == RDC_KIND_TREE    ? 5 + wide
                          : kind == RDC_KIND_ONESHOT ? 2 + wide
+                         : kind == RDC_KIND_DIRECT  ? 7 + wide
                                                     : wide;
         if (cache[slot] > 0) return cache[slot];
         int b = 0;
@@ -1604,6 +1759,8 @@ struct Kernels {
             case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_oneshot<OP, T, 16>, kBlock, debug_lds_pad()); break;
             case 5: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_tree<OP, T, 8>, kBlock, debug_lds_pad()); break;
             case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_tree<OP, T, 16>, kBlock, debug_lds_pad()); break;
+            case 7: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_direct<OP, T, 8>, kBlock, debug_lds_pad()); break;
+            case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_direct<OP, T, 16>, kBlock, debug_lds_pad()); break;
             default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_ring<OP, T>, kBlock, debug_lds_pad()); break;
         }
         if (e != hipSuccess || b <= 0) {
@@ -1620,6 +1777,7 @@ struct Kernels {
     ks->reduce = &Kernels<OP, T>::reduce; \
     ks->mesh = &Kernels<OP, T>::mesh;     \
     ks->ring = &Kernels<OP, T>::ring;     \
+    ks->direct = &Kernels<OP, T>::direct; \
     ks->oneshot = &Kernels<OP, T>::oneshot; \
     ks->tree = &Kernels<OP, T>::tree;       \
     ks->svc = &Kernels<OP, T>::svc;         \

@@ -427,6 +427,12 @@ HbmBytes ModelHbmBytes(int n, uint64_t count, size_t esz, int algo) {
             rd += others + (uint64_t)n * len[r] + others;
             wr += others + 2 * len[r] + others;
             eg += others + (uint64_t)(n - 1) * len[r];  // what peers load from this rank's memory
+        } else if (algo == RDC_ALGO_DIRECT) {
+            // owner r loads chunk r of all n user buffers (n-1 of them remote)
+            // and stores the result into all n; no scratch
+            rd += (uint64_t)n * len[r];
+            wr += (uint64_t)n * len[r];
+            eg += (uint64_t)(n - 1) * len[r] + (S - len[r]);  // pushed results + what peers load from here
         } else {  // one-shot / tree order
             rd += (uint64_t)(n - 1) * S + (uint64_t)n * S;
             wr += (uint64_t)(n - 1) * S + S;

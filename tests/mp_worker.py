@@ -52,6 +52,9 @@ def main():
         nbytes = count * esz[dtype]
         if kind == "allgather":
             nbytes = 0
+        if c.get("empty_cache"):  # the freed blocks go back to HIP: a new allocation may reuse their addresses
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
         buf = torch.zeros(nbytes + pad + 64, dtype=torch.uint8, device="cuda")
         p = buf.data_ptr() + pad
         check_call(_LIB.RdcFill(ctypes.c_void_p(p), count, dtype, c.get("seed", 0x5EED0000), rank, sp))

@@ -1000,9 +1000,9 @@ def test_mp_full_grid_beside_resident_service():
 def test_mp_autotune_agrees_and_stays_bit_exact(world):
     """RdcCommAutotune (bench.py runs it before the timed region at N > 1):
     every rank keeps the same winner (times agreed by a MAX allreduce), the
-    stages cover the schedules (ring, mesh, pull-mode mesh, one-shot where it fits) and then
-    the winner's shape (mesh split / grid / tiles per reduce block, or ring
-    grid / tiles per block),
+    stages cover the schedules (ring, mesh, pull-mode mesh, one-shot where it fits, direct) and
+    then the winner's shape (mesh split / grid / tiles per reduce block, ring
+    grid / tiles per block, or direct grid),
     and the allreduces on the chosen shape stay bit-exact."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -1024,12 +1024,12 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
     small = [json.load(open(os.path.join(tmp, "case0_rank%d.tune" % r))) for r in range(world)]
     assert all(t == small[0] for t in small), small
-    # a one-shot size: the rule's schedule (the one-shot) first, then ring, mesh and the
-    # pull-mode mesh; the winner's shape if it has one
-    sched = [c["schedule"] for c in small[0]["candidates"][:4]]
-    assert sched[0] == "oneshot" and sorted(sched) == ["mesh", "mesh_pull", "oneshot", "ring"], small[0]
+    # a one-shot size: the rule's schedule (the one-shot) first, then ring, mesh, the
+    # pull-mode mesh and the direct schedule; the winner's shape if it has one
+    sched = [c["schedule"] for c in small[0]["candidates"][:5]]
+    assert sched[0] == "oneshot" and sorted(sched) == ["direct", "mesh", "mesh_pull", "oneshot", "ring"], small[0]
     if small[0]["chosen"]["schedule"] == "oneshot":
-        assert len(small[0]["candidates"]) == 4, small[0]
+        assert len(small[0]["candidates"]) == 5, small[0]
     tunes = [json.load(open(os.path.join(tmp, "case1_rank%d.tune" % r))) for r in range(world)]
     assert all(t == tunes[0] for t in tunes), tunes  # identical bits on every rank
     t = tunes[0]
@@ -1038,16 +1038,17 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
     # every candidate timed in 3 rounds: median inside its spread
     assert all(c["spread_ms"][0] <= c["ms"] <= c["spread_ms"][1] for c in cands), t
     # stage 0: the rule's schedule first (ring at n = 2, mesh from n = 3), the other two of
-    # ring / mesh / pull-mode mesh, the one-shot where it fits; then (either mesh) 7 splits,
-    # 4 grids, 4 tilings or (ring) 2 grids, 5 tilings, each later stage re-timing its
-    # predecessor's winner first
+    # ring / mesh / pull-mode mesh, the one-shot where it fits, the direct schedule; then
+    # (either mesh) 7 splits, 4 grids, 4 tilings, (ring) 2 grids, 5 tilings or (direct)
+    # 4 grids, each later stage re-timing its predecessor's winner first
     rule = "ring" if world == 2 else "mesh"
-    s0 = 4 if cands[3]["schedule"] == "oneshot" else 3
+    s0 = 5 if cands[3]["schedule"] == "oneshot" else 4
     assert cands[0]["schedule"] == rule and {c["schedule"] for c in cands[:3]} == {"ring", "mesh", "mesh_pull"}, t
+    assert cands[s0 - 1]["schedule"] == "direct", t
     if t["chosen"]["schedule"] != "oneshot":
-        mesh_like = t["chosen"]["schedule"] in ("mesh", "mesh_pull")
-        last = 4 if mesh_like else 5
-        assert len(cands) == s0 + (15 if mesh_like else 7), t
+        chosen = t["chosen"]["schedule"]
+        last = 4 if chosen != "ring" else 5
+        assert len(cands) == s0 + {"mesh": 15, "mesh_pull": 15, "ring": 7, "direct": 4}[chosen], t
         assert all(c["schedule"] == t["chosen"]["schedule"] for c in cands[s0:]), t
         # the last stage's incumbent stays unless another beats it by more than 3 %
         fin = cands[-last:]
@@ -1075,7 +1076,7 @@ def test_mp_tune_file_persists_autotune():
         a = json.load(open(os.path.join(first, "case0_rank%d.launch" % r)))
         b = json.load(open(os.path.join(second, "case0_rank%d.launch" % r)))
         assert a == b, (a, b, tuned)
-        assert {1: "ring", 2: "mesh", 3: "oneshot"}[b[5]] == tuned["chosen"]["schedule"], (b, tuned)
+        assert {1: "ring", 2: "mesh", 3: "oneshot", 5: "mesh_pull", 6: "direct"}[b[5]] == tuned["chosen"]["schedule"], (b, tuned)
     for tmp, cases in ((first, [{"count": big, "dtype": 6, "op": 2}]),
                        (second, [{"count": big, "dtype": 6, "op": 2}, {"count": big + 3, "dtype": 10, "op": 2}])):
         for i, c in enumerate(cases):
@@ -1370,3 +1371,73 @@ def test_mp_plan_disagreement_is_refused(key, value):
     outs = [p.communicate(timeout=120)[0].decode(errors="replace") for p in procs]
     for r, o in enumerate(outs):
         assert "ERR:" in o and ("disagree on " + key) in o, "rank %d:\n%s" % (r, o[-2000:])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mp_direct_after_free(world):
+    """The direct schedule across freed and re-allocated buffers (each case
+    allocates after torch.cuda.empty_cache, so HIP may hand the same
+    addresses to new allocations, of the same or another size).  A HIP IPC
+    handle names (process, base address): a peer still mapping the freed
+    allocation would get that stale mapping back for the new one, and closing
+    it first faulted the GPU at n = 3 (round 5, profiles/r05/direct/).  So an
+    address exported before for another allocation is not exported again:
+    such calls take the scratch schedules on every rank.  Every result
+    bit-exact against the oracle's ring, whichever path ran; the first call
+    (nothing freed yet) takes the direct schedule."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = []
+    for k, (mib, dt) in enumerate(((16, 6), (16, 6), (16, 10), (64, 10), (64, 6), (16, 6), (128, 10), (64, 6))):
+        esz = 4 if dt == 6 else 2
+        cases.append({"count": (mib << 20) // esz, "dtype": dt, "op": 2, "algo": 6, "empty_cache": k > 0,
+                      "seed": 0x5EEDE000 + k, "last_launch": True})
+    tmp = run_mp(world, cases, timeout=300)
+    for i, c in enumerate(cases):
+        want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, c, r)
+    ll = [json.load(open(os.path.join(tmp, "case%d_rank0.launch" % i))) for i in range(len(cases))]
+    assert ll[0][5] == 6, ll
+    assert all(x[5] in (6, 1, 2, 5) for x in ll), ll  # direct, or the automatic scratch schedule
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_mp_direct_registered_buffers(world):
+    """RDC_ALGO_DIRECT (k_direct): every rank's user buffer is mapped into
+    every peer (HIP IPC, once per allocation, agreed by a per-call host
+    rendezvous), owner r folds chunk r straight out of the n buffers in chunk
+    r's ring order and writes the result back into all of them.  Every
+    (dtype, op) family, sizes from one element to 16 Mi + 5, repeated calls on
+    one buffer (the mapping cache), chains mixing the direct schedule with the
+    scratch schedules on one buffer, and buffers whose addresses differ mod 16
+    between ranks (the rendezvous then falls back to the scratch schedules on
+    every rank) — every byte against the oracle's ring."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = []
+    for dt, op in ((6, 2), (0, 2), (10, 2), (7, 0), (1, 3), (11, 2), (4, 1)):
+        for count in (1, 1001, 70001):
+            cases.append({"count": count, "dtype": dt, "op": op, "algo": 6, "last_launch": True})
+    cases.append({"count": (16 << 20) + 5, "dtype": 6, "op": 2, "algo": 6, "reps": 3, "last_launch": True})
+    cases.append({"count": (3 << 20) + 1, "dtype": 6, "op": 2, "kind": "algo_chain", "algos": [6, 2, 6, 5, 1, 6, 3, 6]})
+    cases.append({"count": 70001, "dtype": 6, "op": 2, "algo": 6, "pad_per_rank": 4, "last_launch": True})
+    tmp = run_mp(world, cases, timeout=300)
+    for i, c in enumerate(cases):
+        if c.get("kind") == "algo_chain":  # every schedule gives the ring's bits
+            want = [O.fill(c["count"], 6, 0x5EED0000, r) for r in range(world)]
+            for _ in c["algos"]:
+                O.allreduce_ring(want, 6, 2)
+        else:
+            want = expected_for(c, world)
+        for r in range(world):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, c, r)
+        if c.get("last_launch"):
+            ll = json.load(open(os.path.join(tmp, "case%d_rank0.launch" % i)))
+            # aligned buffers take the direct schedule (LastLaunch algo 6);
+            # buffers 4 B apart per rank fall back (every rank alike); a
+            # buffer of at most rdc_reduce_ring_mincount (1 B) takes the tree
+            esz = np.dtype(O.NP_DTYPE[c["dtype"]]).itemsize
+            assert (ll[5] == 6) == ("pad_per_rank" not in c and c["count"] * esz > 1), (i, c, ll)

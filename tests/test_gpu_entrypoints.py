@@ -82,12 +82,13 @@ def test_bench_torchrun_two_ranks():
     assert ex["host_64MiB_registered"]["algbw_GBps_pcie_inclusive"] > 0, ex.get("host_64MiB_registered")
     chk = out["oracle_check"]
     assert all(chk.get(k) is True for k in PARITY_KEYS), chk
+    assert chk["schedule"]["cfg3_direct"] == "direct", chk  # a fresh buffer: the registered-buffer schedule ran
     assert out["extras_skipped"] == [] and "parity_checks" in out["extras_wall_s"], out["extras_wall_s"]
 
 
 # every hand-off kind the timed lines use, verified bit-exact in bench.py's
 # parity_checks
-PARITY_KEYS = ("cfg3_mesh", "cfg3_ring", "cfg3_mesh_pull", "cfg4_fp16", "cfg5_buckets", "oneshot_512KiB", "service_host_4KiB",
+PARITY_KEYS = ("cfg3_direct", "cfg3_mesh", "cfg3_ring", "cfg3_mesh_pull", "cfg4_fp16", "cfg5_buckets", "oneshot_512KiB", "service_host_4KiB",
                "tree_order", "broadcast_nonzero_root", "allgather_varsize")
 
 

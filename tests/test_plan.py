@@ -332,7 +332,8 @@ def test_hbm_byte_model_closed_forms(n):
     (3n-2)/n S each way; one-shot (2n-1) S loaded + n S stored; egress
     2(n-1)/n S for ring and mesh (what the link roofline counts) and (n-1) S
     for the one-shot; the pull-mode mesh loads what the mesh loads and
-    stores 2n S over the ranks.  Ragged Split chunks: the rank sums keep the
+    stores 2n S over the ranks; the direct schedule loads and stores S per
+    rank with the mesh's egress.  Ragged Split chunks: the rank sums keep the
     closed forms exactly."""
     for count in (n * 4096, n * 4096 + n - 1, 1001):
         S = 4 * count
@@ -344,6 +345,10 @@ def test_hbm_byte_model_closed_forms(n):
         pull = hbm(n, count, 6, 5)   # pull-mode mesh: same loads, one local result copy instead of n-1 remote
         assert pull["read_sum"] == mesh["read_sum"] and pull["write_sum"] == 2 * n * S
         assert pull["egress"] == mesh["egress"]
+        direct = hbm(n, count, 6, 6)  # registered buffers: each buffer read once and written once
+        assert direct["read_sum"] == direct["write_sum"] == n * S
+        if count % n == 0:
+            assert direct["read"] == direct["write"] == S and direct["egress"] == mesh["egress"]
         if count % n == 0:
             assert ring["read"] * n == 5 * (n - 1) * S and ring["write"] * n == 4 * (n - 1) * S
             assert mesh["read"] * n == (3 * n - 2) * S

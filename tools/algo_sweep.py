@@ -1,8 +1,10 @@
 #!/usr/bin/env python
 """Per-launch time of each allreduce schedule over a range of sizes, on the
 communicator's own stream, max over ranks (the schedule-choice data for
-RDC_ONESHOT_BYTES).  fp32 sum; algo 1 = ring (reference schedule), 2 = mesh,
-3 = one-shot (skipped where it does not fit the slot half).
+RDC_ONESHOT_BYTES / RDC_DIRECT_BYTES).  fp32 sum; algo 1 = ring (reference
+schedule), 2 = mesh, 3 = one-shot (skipped where it does not fit the slot
+half), 5 = pull-mode mesh, 6 = direct (registered buffers).  SWEEP_ALGOS
+(e.g. "0/1/6") picks the schedules.
 
     python -m torch.distributed.run --nproc-per-node N tools/algo_sweep.py [sizes_MiB] [steps]
 """
@@ -17,7 +19,7 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    sizes = [float(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,4,16,64,256").split(",")]
+    sizes = [float(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,4,16,64,256").replace("/", ",").split(",")]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     import torch
     import torch.distributed as dist
@@ -38,7 +40,9 @@ def main():
     for mib in sizes:
         nb = int(mib * (1 << 20))
         row = {}
-        for algo, name in ((0, "auto"), (1, "ring"), (2, "mesh"), (3, "oneshot")):
+        for algo, name in ((0, "auto"), (1, "ring"), (2, "mesh"), (3, "oneshot"), (5, "mesh_pull"), (6, "direct")):
+            if str(algo) not in os.environ.get("SWEEP_ALGOS", "0/1/2/3").replace(",", "/").split("/"):
+                continue
             if algo == 3 and nb > half.value // 2:
                 continue
 
