@@ -297,6 +297,7 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
                                        "tuned": {k: t["chosen"][k] for k in ("schedule", "split", "grid",
                                                                              "tiles_per_block")}})
         if nb == (256 << 20):
+            e.update({k: v for k, v in sizes[str(nb)].items() if k.startswith("tuned")})
             out["cfg2_256MiB"] = e
     del f
     return out
@@ -871,8 +872,11 @@ def main():
                                                                 budget),
                          partial=part_c, need_s=30)
     if multi:
-        del buf  # room for the other configs' buffers
-        torch.cuda.empty_cache()
+        # back to torch's caching allocator, NOT to HIP (no empty_cache): the
+        # later configs' buffers come out of the same allocations, which the
+        # direct schedule has mapped already; a freed allocation's address
+        # handed out again would not be exported (AllreduceDirect)
+        del buf
     if multi and args.ring_steps > 0:
         # the reference's own schedule on a buffer of the same size (same
         # bits, one link direction per GPU).  Grids are clamped to what stays
@@ -882,7 +886,6 @@ def main():
             rdc_amd.fill_(rbuf, 0x5EED0000, rank)
             ms = time_ring(_LIB, comm, rbuf, count, dt_enum, sp, dist, torch, args.ring_steps)
             del rbuf
-            torch.cuda.empty_cache()
             return ms
         ring_cmp = guarded("ring_schedule", ring_leg, need_s=5)
     if multi and f32 and args.extra_steps > 0:

@@ -187,7 +187,11 @@ int RdcCommAllreduceEx(void* comm, void* dev_buf, size_t count, int dtype, int o
 /* device-resident coalesced allreduce (see RdcAllreduceCoalesced), stream-ordered.
  * The per-group unit table is cached by (buffers, counts): after a first
  * (warm-up) call with the same buckets, launches need no host->device copy
- * and can be captured in a hipGraph. */
+ * and can be captured in a hipGraph.  algo 6 (or an Autotune'd direct
+ * schedule for the list's total size) runs the whole list as ONE direct
+ * launch between the ranks' buffers (every buffer's allocation mapped into
+ * the peers, <= 4096 buffers in <= 64 allocations per call; else the
+ * scratch schedules). */
 int RdcCommAllreduceCoalesced(void* comm, void* const* dev_bufs, const size_t* counts, int nbuf, int dtype, int op,
                               int algo, void* stream);
 int RdcCommBroadcast(void* comm, void* dev_buf, size_t bytes, int root, void* stream);

@@ -521,7 +521,7 @@ int RdcAllreduceCoalescedOn(void* comm, void** bufs, const size_t* counts, int n
 int RdcCommAllreduceCoalesced(void* comm, void* const* dev_bufs, const size_t* counts, int nbuf, int dtype, int op,
                               int algo, void* stream) {
     return guard([&] {
-        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_MESH_PULL) throw std::invalid_argument("rdc: bad algo");
+        if (algo < RDC_ALGO_AUTO || algo > RDC_ALGO_DIRECT) throw std::invalid_argument("rdc: bad algo");
         as_comm(comm)->AllreduceCoalesced(dev_bufs, counts, nbuf, dtype, op, static_cast<hipStream_t>(stream), algo);
     });
 }

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <unordered_map>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -833,9 +834,12 @@ Communicator::~Communicator() {
     }
     for (auto& kv : pack_cache_)
         if (kv.second.dtable) (void)hipFreeAsync(kv.second.dtable, nullptr);
+    for (auto& kv : direct_tables_)
+        if (kv.second.dtable) (void)hipFreeAsync(kv.second.dtable, nullptr);
     if (image_) (void)hipFreeAsync(image_, nullptr);
     (void)hipStreamSynchronize(nullptr);
     for (auto& r : retired_) (void)hipEventDestroy(r.first);
+    for (auto& r : direct_retired_) (void)hipEventDestroy(r.first);
     if (p2p_) (void)hipFree(p2p_);
     if (ch_) {
         {
@@ -986,9 +990,11 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
         LaunchTree(ks, static_cast<char*>(buf), (uint64_t)count * esz, stream);
         return;
     }
-    if (DirectEligible(algo, (uint64_t)count * esz, stream) &&
-        AllreduceDirect(ks, static_cast<char*>(buf), (uint64_t)count * esz, esz, stream))
-        return;
+    if (DirectEligible(algo, (uint64_t)count * esz, stream)) {
+        char* b0 = static_cast<char*>(buf);
+        const uint64_t nb = (uint64_t)count * esz;
+        if (AllreduceDirect(ks, &b0, &nb, 1, esz, stream)) return;
+    }
     if (algo == RDC_ALGO_DIRECT) algo = RDC_ALGO_AUTO;  // not registrable here: the scratch schedules
     int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
     SplitRanges((int64_t)count, n_, cb, ce);  // utils::Split (include/utils/utils.h:59-70)
@@ -1025,7 +1031,7 @@ namespace {
 // RDC_DIRECT_LOG=1: one stderr line per export and mapping of the direct
 // schedule, for debugging the mapping cache
 constexpr size_t kDirectExportsMax = 4096;  // allocations one rank exports over a channel's life
-constexpr size_t kDirectMapsMax = 4096;     // peer allocations one rank maps
+constexpr size_t kDirectMapsMax = 16384;    // peer allocations one rank maps
 
 bool direct_log() {
     static const bool on = [] {
@@ -1052,12 +1058,13 @@ bool rendezvous_wait(DirectDesc* slots, int n, uint64_t DirectDesc::*field, uint
 }
 }  // namespace
 
-bool Communicator::AllreduceDirect(const KernelSet& ks, char* buf, uint64_t bytes, size_t esz, hipStream_t stream) {
+bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const uint64_t* bytes, int nbuf,
+                                   size_t esz, hipStream_t stream) {
     Channel& ch = *ch_;
     const uint64_t call = ++ch.dcalls;  // the same on every rank (DirectEligible)
     DirectDesc* slots = reinterpret_cast<DirectDesc*>(ch.dreg.get()) + (call & 1) * (uint64_t)n_;
     DirectDesc& me = slots[rank_];
-    // 1) this rank's buffer: its allocation, offset and IPC handle.
+    // 1) this rank's buffers: their allocations, offsets and IPC handles.
     //
     // Mapping life cycle (measured round 5, tools/direct_check.py,
     // profiles/r05/direct/): a HIP IPC handle names an allocation by
@@ -1072,27 +1079,37 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* buf, uint64_t byte
     // call falls back to the scratch schedules on every rank.  The cost: a
     // freed allocation stays alive while peers keep its mapping.
     me.valid = 0;
-    me.bytes = bytes;
-    me.mis16 = (uint64_t)(uintptr_t)buf & 15;
-    if (!ch.direct_off) {
+    me.nalloc = 0;
+    me.nbuf = (uint32_t)nbuf;
+    bool valid = !ch.direct_off && nbuf >= 1 && nbuf <= kDirectBufsMax;
+    const auto t_export = std::chrono::steady_clock::now();
+    std::unordered_map<uint64_t, uint32_t> alloc_index;  // allocation id -> index in me.alloc
+    std::vector<char*> own_base;                          // index -> this rank's allocation base
+    for (int b = 0; b < nbuf && valid; ++b) {
+        char* buf = bufs[b];
         unsigned long long id = 0;
         hipDeviceptr_t base = nullptr;
         size_t size = 0;
         hipPointerAttribute_t at;
-        if (hipPointerGetAttributes(&at, buf) == hipSuccess && at.type == hipMemoryTypeDevice &&
-            hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)buf) == hipSuccess &&
-            hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)buf) == hipSuccess && base != nullptr &&
-            (char*)buf + bytes <= (char*)base + size) {
-            const uintptr_t b = (uintptr_t)base;
+        valid = hipPointerGetAttributes(&at, buf) == hipSuccess && at.type == hipMemoryTypeDevice &&
+                hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)buf) == hipSuccess &&
+                hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)buf) == hipSuccess && base != nullptr &&
+                buf + bytes[b] <= (char*)base + size;
+        (void)hipGetLastError();
+        if (!valid) break;
+        auto ix = alloc_index.find((uint64_t)id);
+        const uint32_t ai = ix != alloc_index.end() ? ix->second : me.nalloc;
+        if (ai == me.nalloc) {  // this call's first buffer in that allocation: export it
+            const uintptr_t bs = (uintptr_t)base;
             const char* why = nullptr;
-            auto it = ch.dexports.find(b);
+            auto it = ch.dexports.find(bs);
             if (it != ch.dexports.end()) {
                 if (it->second.id != (uint64_t)id) why = "address reused";
             } else {
-                // an earlier export overlapping [b, b + size) is a dead allocation
-                auto nx = ch.dexports.lower_bound(b);
-                if ((nx != ch.dexports.end() && nx->first < b + size) ||
-                    (nx != ch.dexports.begin() && std::prev(nx)->first + std::prev(nx)->second.size > b))
+                // an earlier export overlapping [bs, bs + size) is a dead allocation
+                auto nx = ch.dexports.lower_bound(bs);
+                if ((nx != ch.dexports.end() && nx->first < bs + size) ||
+                    (nx != ch.dexports.begin() && std::prev(nx)->first + std::prev(nx)->second.size > bs))
                     why = "range reused";
                 else if (ch.dexports.size() >= kDirectExportsMax)
                     why = "export table full";
@@ -1100,93 +1117,197 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* buf, uint64_t byte
                     Channel::DirectExport ex;
                     ex.id = (uint64_t)id;
                     ex.size = size;
-                    if (hipIpcGetMemHandle(&ex.handle, base) == hipSuccess) it = ch.dexports.emplace(b, ex).first;
+                    if (hipIpcGetMemHandle(&ex.handle, base) == hipSuccess) it = ch.dexports.emplace(bs, ex).first;
                     else why = "no IPC handle";
+                    (void)hipGetLastError();
                 }
             }
+            if (!why && me.nalloc >= (uint32_t)kDirectAllocsMax) why = "too many allocations in one call";
             if (direct_log())
-                fprintf(stderr, "rdc-direct r%d call %llu: buffer %p id %llu base %p size %zu%s%s\n", rank_,
-                        (unsigned long long)call, (void*)buf, id, (void*)base, size, why ? ": not exported, " : "",
-                        why ? why : "");
-            if (!why) {
-                me.buffer_id = (uint64_t)id;
-                me.offset = (uint64_t)((char*)buf - (char*)base);
-                me.handle = it->second.handle;
-                me.valid = 1;
+                fprintf(stderr, "rdc-direct r%d call %llu: buffer %d %p id %llu base %p size %zu%s%s\n", rank_,
+                        (unsigned long long)call, b, (void*)buf, id, (void*)base, size,
+                        why ? ": not exported, " : "", why ? why : "");
+            if (why) {
+                valid = false;
+                break;
             }
+            me.alloc[ai].id = (uint64_t)id;
+            me.alloc[ai].handle = it->second.handle;
+            alloc_index.emplace((uint64_t)id, ai);
+            own_base.push_back((char*)base);
+            ++me.nalloc;
         }
-        (void)hipGetLastError();
+        me.buf[b].alloc = ai;
+        me.buf[b].mis16 = (uint32_t)((uintptr_t)buf & 15);
+        me.buf[b].off = (uint64_t)(buf - (char*)base);
+        me.buf[b].bytes = bytes[b];
     }
+    me.valid = valid ? 1 : 0;
+    const double export_us =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_export).count();
     __atomic_store_n(&me.stamp0, call, __ATOMIC_RELEASE);
     if (!rendezvous_wait(slots, n_, &DirectDesc::stamp0, call, cfg_.timeout_s))
         throw std::runtime_error("rdc: registered-buffer rendezvous timed out (a peer did not join the allreduce)");
-    // 2) every buffer usable and alike?  Then map the peers' (cached per allocation)
+    // 2) every rank's list usable and alike (same buffers' sizes, each buffer
+    // congruent mod 16 on every rank)?  Then map the peers' allocations
     bool usable = true;
-    for (int p = 0; p < n_; ++p)
-        usable = usable && slots[p].valid && slots[p].bytes == bytes && slots[p].mis16 == me.mis16;
-    char* peer[RDC_MAX_RANKS] = {};
-    peer[rank_] = buf;
+    for (int p = 0; p < n_ && usable; ++p) {
+        usable = slots[p].valid && slots[p].nbuf == (uint32_t)nbuf;
+        for (int b = 0; b < nbuf && usable; ++b)
+            usable = slots[p].buf[b].bytes == bytes[b] && slots[p].buf[b].mis16 == me.buf[b].mis16;
+    }
+    std::vector<char*> amap_v((size_t)n_ * kDirectAllocsMax);  // rank q's allocation i as mapped here
+    auto amap = [&](int q, uint32_t i) -> char*& { return amap_v[(size_t)q * kDirectAllocsMax + i]; };
     int ok = usable ? 1 : 0;
     for (int p = 0; p < n_ && ok; ++p) {
-        if (p == rank_) continue;
-        auto key = std::make_pair(p, slots[p].buffer_id);
-        auto it = ch.dmaps.find(key);
-        if (it == ch.dmaps.end()) {
-            if (ch.dmaps.size() >= kDirectMapsMax) {  // full: no new mappings (fallback)
-                ok = 0;
-                break;
+        for (uint32_t i = 0; i < slots[p].nalloc && ok; ++i) {
+            if (p == rank_) {  // this rank's own allocation
+                amap(p, i) = own_base[i];
+                continue;
             }
-            void* m = nullptr;
-            if (hipIpcOpenMemHandle(&m, slots[p].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !m) {
-                (void)hipGetLastError();
-                ok = 0;
-                break;
+            auto key = std::make_pair(p, slots[p].alloc[i].id);
+            auto it = ch.dmaps.find(key);
+            if (it == ch.dmaps.end()) {
+                if (ch.dmaps.size() >= kDirectMapsMax) {  // full: no new mappings (fallback)
+                    ok = 0;
+                    break;
+                }
+                void* m = nullptr;
+                if (hipIpcOpenMemHandle(&m, slots[p].alloc[i].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+                    !m) {
+                    (void)hipGetLastError();
+                    ok = 0;
+                    break;
+                }
+                // a pointer this rank already holds for another allocation
+                // would be the stale mapping described above: never use it
+                bool dup = false;
+                for (auto& o : ch.dmaps) dup = dup || o.second == (char*)m;
+                if (direct_log())
+                    fprintf(stderr, "rdc-direct r%d call %llu: open peer %d id %llu -> %p%s\n", rank_,
+                            (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id, m,
+                            dup ? " (a mapping already held: not used)" : "");
+                if (dup) {
+                    ok = 0;
+                    break;
+                }
+                it = ch.dmaps.emplace(key, static_cast<char*>(m)).first;
             }
-            // a pointer this rank already holds for another allocation would
-            // be the stale mapping described above: never use it
-            bool dup = false;
-            for (auto& o : ch.dmaps) dup = dup || o.second == (char*)m;
-            if (direct_log())
-                fprintf(stderr, "rdc-direct r%d call %llu: open peer %d id %llu -> %p%s\n", rank_,
-                        (unsigned long long)call, p, (unsigned long long)slots[p].buffer_id, m,
-                        dup ? " (a mapping already held: not used)" : "");
-            if (dup) {
-                ok = 0;
-                break;
-            }
-            it = ch.dmaps.emplace(key, static_cast<char*>(m)).first;
+            amap(p, i) = it->second;
         }
-        peer[p] = it->second + slots[p].offset;
     }
     me.ok = ok;
     __atomic_store_n(&me.stamp1, call, __ATOMIC_RELEASE);
     if (!rendezvous_wait(slots, n_, &DirectDesc::stamp1, call, cfg_.timeout_s))
         throw std::runtime_error("rdc: registered-buffer rendezvous timed out (a peer did not join the allreduce)");
     for (int p = 0; p < n_; ++p) usable = usable && slots[p].ok;
+    if (direct_log())
+        fprintf(stderr, "rdc-direct r%d call %llu: %d buffers in %u allocations, export %.1f us, total %.1f us, %s\n",
+                rank_, (unsigned long long)call, nbuf, me.nalloc, export_us,
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_export).count(),
+                usable ? "direct" : "fallback");
     if (!usable) return false;  // every rank saw the same slots: all fall back together
     // 3) one launch: owner r folds chunk r of every buffer in place
-    int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
-    SplitRanges((int64_t)(bytes / esz), n_, cb, ce);
+    uint64_t total = 0;
+    for (int b = 0; b < nbuf; ++b) total += bytes[b];
     CollArgs a;
     FillArgsCommon(&a);
     a.kind = RDC_KIND_DIRECT;
-    a.user = buf;
-    for (int c = 0; c < n_; ++c) {
-        a.off[c] = (uint64_t)cb[c] * esz;
-        a.len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
-        a.cbuf[c] = peer[c];
-    }
-    const Shape sh = ShapeFor(bytes, RDC_ALGO_DIRECT);  // an Autotune'd grid, else the mesh's
+    const Shape sh = ShapeFor(total, RDC_ALGO_DIRECT);  // an Autotune'd grid, else the mesh's
     const int grid_cap = LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : mesh_blocks(),
                                     ks.occupancy(RDC_KIND_DIRECT, n_));
-    // ~2 tiles per block, 64 KiB .. 4 MiB, a multiple of 256 B
-    uint64_t tile = a.len[rank_] / (2 * (uint64_t)grid_cap) + 1;
+    // ~2 tiles (items) per block, 64 KiB .. 4 MiB, a multiple of 256 B
+    uint64_t tile = total / n_ / (2 * (uint64_t)grid_cap) + 1;
     tile = std::min<uint64_t>(std::max<uint64_t>(tile, 64 << 10), 4 << 20);
     tile = (tile + 255) & ~(uint64_t)255;
-    const int tiles = (int)std::max<uint64_t>(1, (a.len[rank_] + tile - 1) / tile);
-    a.tile_bytes = tile;
-    a.tiles[rank_] = a.len[rank_] ? tiles : 0;
-    const int grid = std::max(1, std::min(tiles, grid_cap));
+    int grid = 1;
+    if (nbuf == 1) {
+        char* buf = bufs[0];
+        int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+        SplitRanges((int64_t)(bytes[0] / esz), n_, cb, ce);
+        a.user = buf;
+        for (int c = 0; c < n_; ++c) {
+            a.off[c] = (uint64_t)cb[c] * esz;
+            a.len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
+            a.cbuf[c] = amap(c, slots[c].buf[0].alloc) + slots[c].buf[0].off;
+        }
+        const int tiles = (int)std::max<uint64_t>(1, (a.len[rank_] + tile - 1) / tile);
+        a.tile_bytes = tile;
+        a.tiles[rank_] = a.len[rank_] ? tiles : 0;
+        grid = std::max(1, std::min(tiles, grid_cap));
+    } else {
+        // items of this owner: chunk rank_ of every buffer in pieces of at
+        // most `tile`; then every rank's buffer addresses as mapped here.
+        // Cached by the layout (every rank's allocations and offsets).
+        std::vector<uint64_t> key;
+        key.reserve(2 + (size_t)nbuf * (1 + 2 * (size_t)n_));
+        key.push_back(esz);
+        key.push_back(tile);
+        for (int b = 0; b < nbuf; ++b) key.push_back(bytes[b]);
+        for (int p = 0; p < n_; ++p)
+            for (int b = 0; b < nbuf; ++b) {
+                key.push_back(slots[p].alloc[slots[p].buf[b].alloc].id);
+                key.push_back(slots[p].buf[b].off);
+            }
+        auto it = direct_tables_.find(key);
+        if (it == direct_tables_.end()) {
+            if (direct_tables_.size() >= 16) {  // evict the least recently used layout
+                auto lru = direct_tables_.begin();
+                for (auto j = direct_tables_.begin(); j != direct_tables_.end(); ++j)
+                    if (j->second.last_use < lru->second.last_use) lru = j;
+                if (lru->second.dtable) hip_check(hipFreeAsync(lru->second.dtable, stream), "release direct table");
+                hipEvent_t ev = nullptr;
+                hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+                hip_check(hipEventRecord(ev, stream), "record");
+                direct_retired_.emplace_back(ev, lru->second.host);
+                direct_tables_.erase(lru);
+            }
+            for (size_t i = 0; i < direct_retired_.size();) {  // host copies whose upload has surely finished
+                if (hipEventQuery(direct_retired_[i].first) == hipSuccess) {
+                    (void)hipEventDestroy(direct_retired_[i].first);
+                    direct_retired_[i] = direct_retired_.back();
+                    direct_retired_.pop_back();
+                } else {
+                    (void)hipGetLastError();
+                    ++i;
+                }
+            }
+            // DirectItem {buffer, byte offset in it, length} as 3 words, then
+            // ptr[q * nbuf + b]
+            auto host = std::make_shared<std::vector<uint64_t>>();
+            int nitems = 0;
+            for (int b = 0; b < nbuf; ++b) {
+                int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+                SplitRanges((int64_t)(bytes[b] / esz), n_, cb, ce);
+                const uint64_t so = (uint64_t)cb[rank_] * esz, sl = (uint64_t)(ce[rank_] - cb[rank_]) * esz;
+                for (uint64_t x = 0; x < sl; x += tile) {
+                    host->push_back((uint64_t)b);
+                    host->push_back(so + x);
+                    host->push_back(std::min<uint64_t>(tile, sl - x));
+                    ++nitems;
+                }
+            }
+            for (int p = 0; p < n_; ++p)
+                for (int b = 0; b < nbuf; ++b)
+                    host->push_back((uint64_t)(uintptr_t)(amap(p, slots[p].buf[b].alloc) + slots[p].buf[b].off));
+            DirectTable t;
+            t.nitems = nitems;
+            t.tile = tile;
+            t.host = host;
+            const size_t tb = host->size() * sizeof(uint64_t);
+            hip_check(hipMallocAsync(&t.dtable, tb, stream), "allocate direct table");
+            hip_check(hipMemcpyAsync(t.dtable, host->data(), tb, hipMemcpyHostToDevice, stream), "upload direct table");
+            it = direct_tables_.emplace(std::move(key), t).first;
+        }
+        it->second.last_use = ++direct_tick_;
+        a.user = bufs[0];
+        a.units = it->second.dtable;
+        a.nunits = it->second.nitems;
+        a.dnbuf = nbuf;
+        a.tile_bytes = tile;
+        grid = std::max(1, std::min(it->second.nitems, grid_cap));
+        if (it->second.nitems == 0) grid = 1;
+    }
     if (notify_) {
         a.notify = notify_;
         a.notify_val = notify_val_;
@@ -1197,7 +1318,7 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* buf, uint64_t byte
     last_launch_[4] = tile;
     last_launch_[5] = RDC_ALGO_DIRECT;
     ++seq_;
-    log_launch(this, seq_, RDC_ALGO_DIRECT, bytes, grid, tile);
+    log_launch(this, seq_, RDC_ALGO_DIRECT, total, grid, tile);
     hip_check(ks.direct(a, grid, stream), "launch direct allreduce");
     trace_ = nullptr;
     return true;
@@ -1501,6 +1622,23 @@ void Communicator::AllreduceCoalesced(void* const* bufs, const size_t* counts, i
         if (!sb.empty() && !lb.empty())
             AllreduceCoalesced(lb.data(), lc.data(), (int)lb.size(), dtype, op, stream, algo);
         if (!sb.empty()) return;
+    }
+    {
+        // registered buffers (k_direct over the list): every buffer mapped
+        // into every peer, one launch for the whole list, no scratch
+        std::vector<char*> db;
+        std::vector<uint64_t> dn;
+        uint64_t total = 0;
+        for (int b = 0; b < nbuf; ++b)
+            if (counts[b]) {
+                db.push_back(static_cast<char*>(bufs[b]));
+                dn.push_back((uint64_t)counts[b] * esz);
+                total += (uint64_t)counts[b] * esz;
+            }
+        if (!db.empty() && DirectEligible(algo, total, stream) &&
+            AllreduceDirect(ks, db.data(), dn.data(), (int)db.size(), esz, stream))
+            return;
+        if (algo == RDC_ALGO_DIRECT) algo = RDC_ALGO_AUTO;  // not registrable here: the scratch schedules
     }
     std::vector<uint64_t> cnt((size_t)nbuf);
     for (int b = 0; b < nbuf; ++b) cnt[(size_t)b] = counts[b];

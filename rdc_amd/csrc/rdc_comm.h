@@ -128,18 +128,29 @@ struct Channel {
     size_t tune_bytes = 0;
 };
 
-// One rank's slot of the registered-buffer rendezvous (shared host memory).
+// One rank's slot of the registered-buffer rendezvous (shared host memory):
+// the call's buffers (one, or a coalesced list), each as (allocation, offset),
+// and the allocations they live in with their IPC handles.
+constexpr int kDirectAllocsMax = 1024;  // allocations per call (torch's small pool: 2 MiB segments)
+constexpr int kDirectBufsMax = 4096;    // buffers per call (a longer list takes the scratch schedules)
+struct DirectAlloc {
+    uint64_t id;                        // HIP_POINTER_ATTRIBUTE_BUFFER_ID
+    hipIpcMemHandle_t handle;
+};
+struct DirectBuf {
+    uint32_t alloc;                     // index into alloc[]
+    uint32_t mis16;                     // address % 16 (every rank's must agree per buffer)
+    uint64_t off;                       // address - allocation base
+    uint64_t bytes;
+};
 struct DirectDesc {
     uint64_t stamp0;          // rendezvous number whose descriptor this slot holds (release-stored last)
-    uint64_t buffer_id;       // HIP_POINTER_ATTRIBUTE_BUFFER_ID of the buffer's allocation
-    uint64_t offset;          // buffer - allocation base
-    uint64_t bytes;
-    uint64_t mis16;           // buffer address % 16 (every rank's must agree)
-    int32_t valid;            // an exportable device allocation
-    int32_t ok;               // phase 1: every peer's buffer is mapped here
+    int32_t valid;            // every buffer in an exportable device allocation
+    int32_t ok;               // phase 1: every peer's buffers are mapped here
     uint64_t stamp1;          // rendezvous number of `ok` (release-stored last)
-    hipIpcMemHandle_t handle;
-    char pad[64];
+    uint32_t nalloc, nbuf;
+    DirectAlloc alloc[kDirectAllocsMax];
+    DirectBuf buf[kDirectBufsMax];
 };
 
 class Communicator {
@@ -328,7 +339,21 @@ private:
     // rank's buffer unusable (the caller takes the scratch schedules; every
     // rank decides alike)
     bool DirectEligible(int algo, uint64_t bytes, hipStream_t stream) const;
-    bool AllreduceDirect(const KernelSet& ks, char* buf, uint64_t bytes, size_t esz, hipStream_t stream);
+    // one buffer (nbuf = 1) or a coalesced list; bytes[b] > 0 for every b
+    bool AllreduceDirect(const KernelSet& ks, char* const* bufs, const uint64_t* bytes, int nbuf, size_t esz,
+                         hipStream_t stream);
+    // device tables of coalesced direct launches: owner items + every rank's
+    // buffer addresses, cached by the call's layout
+    struct DirectTable {
+        void* dtable = nullptr;
+        std::shared_ptr<std::vector<uint64_t>> host;  // the upload's source
+        int nitems = 0;
+        uint64_t tile = 0;
+        uint64_t last_use = 0;
+    };
+    std::map<std::vector<uint64_t>, DirectTable> direct_tables_;
+    std::vector<std::pair<hipEvent_t, std::shared_ptr<std::vector<uint64_t>>>> direct_retired_;
+    uint64_t direct_tick_ = 0;
     void CoalescedTree(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, size_t esz,
                        hipStream_t stream);
     void CoalescedStaged(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, int dtype, int op,

@@ -124,7 +124,10 @@ struct CollArgs {
     int8_t tree_dst[RDC_MAX_RANKS];      //   acc[tree_src[i]]), i < tree_len, over the n inputs indexed
     int8_t tree_src[RDC_MAX_RANKS];      //   by rank; the result is acc[0] (rdc_plan.h PlanTreeProgram)
     const void* units;                   // coalesced mesh: device PackUnit table (off/len are packed
-    int nunits;                          //   offsets; user bytes reached through the units), else null
+    int nunits;                          //   offsets; user bytes reached through the units), else null;
+                                         //   coalesced direct: nunits items {buffer, offset, length}
+                                         //   (3 words each), then every rank's dnbuf buffer addresses
+    int dnbuf;                           // coalesced direct: buffers in the list
     uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up
     int uc;                              // 1: every scratch region is uncached (hand-offs need no L2
                                          //   write-back, rdc_device.h block_publish)

@@ -717,6 +717,22 @@ __device__ __forceinline__ void direct_body(const CollArgs& a, uint64_t seq) {
     __syncthreads();
     if (!block_wait(s_flags, n - 1, seq, ab, RDC_KERR_TIMEOUT_RS, a.uc)) return;
     __shared__ char* s_tile[RDC_MAX_RANKS];
+    if (a.units) {
+        // coalesced list: item t = piece of chunk r of buffer it[0], at byte
+        // it[1], it[2] bytes; rank q's buffer b at ptr[q * dnbuf + b]
+        const uint64_t* items = static_cast<const uint64_t*>(a.units);
+        const uint64_t* ptr = items + 3 * (uint64_t)a.nunits;
+        for (int t = blockIdx.x; t < a.nunits; t += gridDim.x) {
+            const uint64_t b = items[3 * (uint64_t)t], so = items[3 * (uint64_t)t + 1];
+            const uint64_t tlen = items[3 * (uint64_t)t + 2];
+            if (threadIdx.x < (unsigned)n)
+                s_tile[threadIdx.x] = reinterpret_cast<char*>(ptr[(uint64_t)threadIdx.x * a.dnbuf + b]) + so;
+            __syncthreads();
+            direct_fold_range<OP, T, NMAX>(a, s_tile, tlen);
+            __syncthreads();  // s_tile is rewritten for the next item
+        }
+        return;
+    }
     for (int t = blockIdx.x; t < a.tiles[r]; t += gridDim.x) {
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[r] - toff;

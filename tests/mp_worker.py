@@ -172,7 +172,9 @@ def main():
         if kind == "coalesced":
             # bucketed allreduce: buffer b filled with seed + b, one fused call per rep
             counts = c["counts"]
-            pads = [(rank * 3 + b) % 5 * esz[dtype] for b in range(len(counts))]
+            # pads differ per rank unless "same_pads" (the direct schedule needs every
+            # buffer congruent mod 16 across ranks)
+            pads = [((0 if c.get("same_pads") else rank * 3) + b) % 5 * esz[dtype] for b in range(len(counts))]
             bufs = [torch.zeros(k * esz[dtype] + pd + 64, dtype=torch.uint8, device="cuda")
                     for k, pd in zip(counts, pads)]
             ptrs = [t.data_ptr() + pd for t, pd in zip(bufs, pads)]
@@ -192,6 +194,11 @@ def main():
                     check_call(_LIB.RdcCommAllreduceCoalesced(comm.handle, arr, cnt, len(counts), dtype, c["op"],
                                                               c.get("algo", 0), sp))
             comm.check(sp)
+            if c.get("last_launch"):
+                ll = (ctypes.c_uint64 * 6)()
+                check_call(_LIB.RdcCommLastLaunch(comm.handle, ll))
+                open(os.path.join(outdir, "case%d_rank%d.launch" % (i, rank)), "w").write(
+                    json.dumps([int(x) for x in ll]))
             if c.get("digest"):  # full-size lists: sha256 over the buckets in order
                 import hashlib
                 h = hashlib.sha256()

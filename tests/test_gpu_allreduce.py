@@ -1423,6 +1423,14 @@ def test_mp_direct_registered_buffers(world):
     cases.append({"count": (16 << 20) + 5, "dtype": 6, "op": 2, "algo": 6, "reps": 3, "last_launch": True})
     cases.append({"count": (3 << 20) + 1, "dtype": 6, "op": 2, "kind": "algo_chain", "algos": [6, 2, 6, 5, 1, 6, 3, 6]})
     cases.append({"count": 70001, "dtype": 6, "op": 2, "algo": 6, "pad_per_rank": 4, "last_launch": True})
+    # coalesced lists as ONE direct launch (buffers in separate allocations
+    # and sub-allocated, odd sizes, an empty bucket); a list whose buffers sit
+    # at rank-dependent offsets mod 16 falls back to the scratch schedules
+    for dt, counts in ((6, [1024, 7, 0, 100003, 1, 65536]), (10, [4099] * 9), (2, [(1 << 18) + 3] * 40)):
+        cases.append({"count": 0, "dtype": dt, "op": 2, "kind": "coalesced", "counts": counts, "algo": 6,
+                      "same_pads": True, "last_launch": True, "reps": 2})
+    cases.append({"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1024, 70001, 333], "algo": 6,
+                  "last_launch": True, "coalesced_fallback": True})
     tmp = run_mp(world, cases, timeout=300)
     for i, c in enumerate(cases):
         if c.get("kind") == "algo_chain":  # every schedule gives the ring's bits
@@ -1440,4 +1448,7 @@ def test_mp_direct_registered_buffers(world):
             # buffers 4 B apart per rank fall back (every rank alike); a
             # buffer of at most rdc_reduce_ring_mincount (1 B) takes the tree
             esz = np.dtype(O.NP_DTYPE[c["dtype"]]).itemsize
+            if c.get("kind") == "coalesced":
+                assert (ll[5] == 6) == (not c.get("coalesced_fallback")), (i, c, ll)
+                continue
             assert (ll[5] == 6) == ("pad_per_rank" not in c and c["count"] * esz > 1), (i, c, ll)
