@@ -798,6 +798,8 @@ def fuzz_cases(seed, world, n=40):
             c = {"count": count, "dtype": dt, "op": op, "algo": rng.choice([0, 1, 2, 3, 5]), "seed": 0x5EED0000 + sd}
             if rng.random() < 0.5:  # the ranks' buffers differ mod 16 (element-aligned)
                 c["pad_per_rank"] = esz[dt] * rng.choice([1, 2, 3])
+            if random.Random(sd ^ 0xD1EC7).random() < 0.3:  # the direct schedule (separate stream: the
+                c["algo"] = 6                                # other draws stay as they were)
             cases.append(c)
         elif kind == "broadcast":
             cases.append({"count": max(1, int(2 ** rng.uniform(0, 24))), "dtype": 0, "kind": "broadcast",
@@ -805,8 +807,11 @@ def fuzz_cases(seed, world, n=40):
         else:
             dt, op = rng.choice([(6, 2), (2, 0), (10, 2), (7, 1)])
             counts = [max(0, int(2 ** rng.uniform(-1, 19))) for _ in range(rng.randint(1, 12))]
-            cases.append({"count": 0, "dtype": dt, "op": op, "kind": "coalesced", "counts": counts,
-                          "algo": rng.choice([0, 1, 2, 3, 5]), "seed": 0x5EED0000 + sd})
+            c = {"count": 0, "dtype": dt, "op": op, "kind": "coalesced", "counts": counts,
+                 "algo": rng.choice([0, 1, 2, 3, 5]), "seed": 0x5EED0000 + sd}
+            if random.Random(sd ^ 0xD1EC7).random() < 0.3:  # one direct launch over the list
+                c.update({"algo": 6, "same_pads": True})
+            cases.append(c)
     return cases
 
 

@@ -18,7 +18,7 @@ first, runs = int(sys.argv[1]), int(sys.argv[2])
 envs = [{}, {"RDC_SCRATCH_BYTES": "8M", "RDC_TILE_BYTES": "16K"}, {"RDC_SCRATCH_BYTES": "4M", "RDC_NBLOCKS": "5"},
         {"RDC_ALGO": "ring"}, {"RDC_ALGO": "mesh", "RDC_SCRATCH_BYTES": "16M"}, {"RDC_HOST_SERVICE": "0"},
         {"rdc_reduce_ring_mincount": "64K"}, {"RDC_HOST_PIECE_BYTES": "1M", "RDC_HOST_INLINE_BYTES": "2M"}]
-extra = dict(kv.split("=", 1) for kv in os.environ.get("FUZZ_ENV", "").split(",") if "=" in kv)
+extra = dict(kv.split("=", 1) for kv in os.environ.get("FUZZ_ENV", "").replace(";", ",").split(",") if "=" in kv)
 fails = 0
 for k in range(runs):
     seed = first + k
