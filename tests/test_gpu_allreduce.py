@@ -852,8 +852,10 @@ def test_mp_across_devices(world):
     hand-offs after its timed region)."""
     if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
         pytest.skip("needs 2 or more GPUs")
-    cases = [{"count": 1001, "dtype": 6, "op": 2, "algo": a} for a in (0, 1, 2, 3, 5)]
-    cases += [{"count": (16 << 20) + 5, "dtype": 6, "op": 2, "algo": a} for a in (1, 2, 5)]
+    cases = [{"count": 1001, "dtype": 6, "op": 2, "algo": a} for a in (0, 1, 2, 3, 5, 6)]
+    cases += [{"count": (16 << 20) + 5, "dtype": 6, "op": 2, "algo": a} for a in (1, 2, 5, 6)]
+    cases += [{"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1024, 70001, 333] * 3, "algo": 6,
+               "same_pads": True}]
     cases += [{"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"},
               {"count": (40 << 20) + 3, "dtype": 1, "op": 0, "kind": "host_allreduce"},
               {"count": (3 << 20) + 5, "dtype": 0, "kind": "broadcast", "root": world - 1}]
@@ -875,11 +877,12 @@ def test_mp_full_size_cfg2():
     import hashlib
     count = (256 << 20) // 4
     cases = [{"count": count, "dtype": 6, "op": 2, "algo": 2, "digest": True},
-             {"count": count, "dtype": 6, "op": 2, "algo": 1, "digest": True}]
+             {"count": count, "dtype": 6, "op": 2, "algo": 1, "digest": True},
+             {"count": count, "dtype": 6, "op": 2, "algo": 6, "digest": True}]
     tmp = run_mp(2, cases, timeout=400, env_extra={"RDC_SCRATCH_BYTES": "4080M", "RDC_NBLOCKS": "64"})
     want = expected_for(cases[0], 2)
     h = hashlib.sha256(np.frombuffer(want[0].tobytes(), dtype=np.uint8).tobytes()).hexdigest()
-    for i in range(2):
+    for i in range(len(cases)):
         for r in range(2):
             assert open(os.path.join(tmp, "case%d_rank%d.sha" % (i, r))).read() == h, (i, r)
 
@@ -904,7 +907,10 @@ def test_mp_full_size_cfg3_cfg4_eight_ranks():
     cases = [{"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 2, "digest": True},
              {"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 1, "digest": True, "last_launch": True},
              {"count": (1 << 30) // 2, "dtype": 10, "op": 2, "algo": 2, "digest": True},
-             {"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 5, "digest": True}]
+             {"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 5, "digest": True},
+             # the direct schedule (registered user buffers) on both dtypes
+             {"count": (1 << 30) // 4, "dtype": 6, "op": 2, "algo": 6, "digest": True},
+             {"count": (1 << 30) // 2, "dtype": 10, "op": 2, "algo": 6, "digest": True, "last_launch": True}]
     tmp = run_mp(8, cases, timeout=600, env_extra={"RDC_SCRATCH_BYTES": "4080M"})
     want = {6: full_digest((1 << 30) // 4, 6, 8), 10: full_digest((1 << 30) // 2, 10, 8)}
     for i, c in enumerate(cases):
@@ -913,6 +919,7 @@ def test_mp_full_size_cfg3_cfg4_eight_ranks():
     # the ring ran as ONE launch per call with one tile per block
     grid = json.load(open(os.path.join(tmp, "case1_rank0.launch")))
     assert grid[5] == 1 and grid[0] >= 1, grid
+    assert json.load(open(os.path.join(tmp, "case5_rank0.launch")))[5] == 6  # the direct schedule ran
 
 
 def test_mp_cfg5_exact_shape_eight_ranks():
@@ -928,7 +935,10 @@ def test_mp_cfg5_exact_shape_eight_ranks():
     cases = [{"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [per] * K, "reps": 2,
               "digest": True},
              {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [per] * K, "reps": 2,
-              "digest": True, "algo": 5}]   # the pull-mode mesh over the same unit table
+              "digest": True, "algo": 5},   # the pull-mode mesh over the same unit table
+             # one direct launch over the list (buckets congruent mod 16 across ranks)
+             {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [per] * K, "reps": 2,
+              "digest": True, "algo": 6, "same_pads": True, "last_launch": True}]
     tmp = run_mp(8, cases, timeout=600, env_extra={"RDC_SCRATCH_BYTES": "4080M"})
     h = hashlib.sha256()
     for b in range(K):
@@ -936,9 +946,10 @@ def test_mp_cfg5_exact_shape_eight_ranks():
         for _ in range(2):
             O.allreduce_ring(xs, 6, 2)
         h.update(xs[0].tobytes())
-    for i in range(2):
+    for i in range(len(cases)):
         for r in range(8):
             assert open(os.path.join(tmp, "case%d_rank%d.sha" % (i, r))).read() == h.hexdigest(), (i, r)
+    assert json.load(open(os.path.join(tmp, "case2_rank0.launch")))[5] == 6  # the direct schedule ran
 
 
 def test_mp_forced_oversized_grid_four_ranks():
