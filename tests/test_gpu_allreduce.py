@@ -1439,6 +1439,11 @@ def test_mp_direct_registered_buffers(world):
     cases.append({"count": (16 << 20) + 5, "dtype": 6, "op": 2, "algo": 6, "reps": 3, "last_launch": True})
     cases.append({"count": (3 << 20) + 1, "dtype": 6, "op": 2, "kind": "algo_chain", "algos": [6, 2, 6, 5, 1, 6, 3, 6]})
     cases.append({"count": 70001, "dtype": 6, "op": 2, "algo": 6, "pad_per_rank": 4, "last_launch": True})
+    # results written by other processes' blocks into lines this rank's L2s
+    # hold (a read kernel before every call), read back by a copy kernel
+    for count in (16384, 262147, 1 << 20):
+        cases.append({"count": count, "dtype": 6, "op": 2, "algo": 6, "reps": 3, "warm_l2": True,
+                      "seed": 0x5EEDF000 + count, "last_launch": True})
     # coalesced lists as ONE direct launch (buffers in separate allocations
     # and sub-allocated, odd sizes, an empty bucket); a list whose buffers sit
     # at rank-dependent offsets mod 16 falls back to the scratch schedules
