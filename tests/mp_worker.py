@@ -217,6 +217,8 @@ def main():
             open(os.path.join(outdir, "case%d_rank%d.tune" % (i, rank)), "w").write(json.dumps(res))
         if c.get("last_launch"):  # record the launch shape the library chose (grid clamp checks)
             ll = (ctypes.c_uint64 * 6)()
+        if c.get("direct_release"):  # RdcCommDirectRelease: mappings closed, the direct schedule off
+            comm.direct_release()
         reps = c.get("reps", 1)
         for _ in range(reps):
             if c.get("warm_l2"):  # every XCD's L2 holds the buffer's lines before peers overwrite them

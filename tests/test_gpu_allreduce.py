@@ -1452,6 +1452,9 @@ def test_mp_direct_registered_buffers(world):
                       "same_pads": True, "last_launch": True, "reps": 2})
     cases.append({"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1024, 70001, 333], "algo": 6,
                   "last_launch": True, "coalesced_fallback": True})
+    # RdcCommDirectRelease on every rank: later algo-6 calls take the scratch schedules
+    cases.append({"count": 70001, "dtype": 6, "op": 2, "algo": 6, "direct_release": True, "reps": 2,
+                  "last_launch": True})
     tmp = run_mp(world, cases, timeout=300)
     for i, c in enumerate(cases):
         if c.get("kind") == "algo_chain":  # every schedule gives the ring's bits
@@ -1472,4 +1475,5 @@ def test_mp_direct_registered_buffers(world):
             if c.get("kind") == "coalesced":
                 assert (ll[5] == 6) == (not c.get("coalesced_fallback")), (i, c, ll)
                 continue
-            assert (ll[5] == 6) == ("pad_per_rank" not in c and c["count"] * esz > 1), (i, c, ll)
+            assert (ll[5] == 6) == ("pad_per_rank" not in c and "direct_release" not in c and c["count"] * esz > 1), \
+                (i, c, ll)
