@@ -1058,45 +1058,42 @@ bool rendezvous_wait(DirectDesc* slots, int n, uint64_t DirectDesc::*field, uint
 }
 }  // namespace
 
-bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const uint64_t* bytes, int nbuf,
-                                   size_t esz, hipStream_t stream) {
+// Step 1 of AllreduceDirect: this rank's buffers as (allocation, offset)
+// and the allocations' IPC handles, into its rendezvous slot `me`; false when
+// any buffer cannot be exported (the call then falls back on every rank).
+// own_base[i] = the base of me.alloc[i] in this process.
+//
+// Mapping life cycle (measured round 5, tools/direct_check.py,
+// profiles/r05/direct/): a HIP IPC handle names an allocation by (exporting
+// process, base address), and an importer that still holds a mapping from an
+// earlier allocation at the same base gets that old mapping back — stale
+// memory — when it opens the new handle.  Closing the old mapping first fixes
+// the data, but re-mapping into address ranges just unmapped faulted the GPU
+// at n = 3.  So mappings are never closed while the channel lives
+// (RdcCommDirectRelease / channel close), and an allocation whose base address
+// — or any byte of whose range — this rank exported before for ANOTHER
+// allocation is not exported.  The cost: a freed allocation stays alive while
+// peers keep its mapping.
+bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_t* bytes, int nbuf, uint64_t call,
+                                std::vector<char*>* own_base) {
     Channel& ch = *ch_;
-    const uint64_t call = ++ch.dcalls;  // the same on every rank (DirectEligible)
-    DirectDesc* slots = reinterpret_cast<DirectDesc*>(ch.dreg.get()) + (call & 1) * (uint64_t)n_;
-    DirectDesc& me = slots[rank_];
-    // 1) this rank's buffers: their allocations, offsets and IPC handles.
-    //
-    // Mapping life cycle (measured round 5, tools/direct_check.py,
-    // profiles/r05/direct/): a HIP IPC handle names an allocation by
-    // (exporting process, base address), and an importer that still holds a
-    // mapping from an earlier allocation at the same base gets that old
-    // mapping back — stale memory — when it opens the new handle.  Closing
-    // the old mapping first fixes the data, but re-mapping into address
-    // ranges just unmapped faulted the GPU at n = 3.  So mappings are never
-    // closed while the channel lives (RdcCommDirectRelease / channel close),
-    // and an allocation whose base address — or any byte of whose range —
-    // this rank exported before for ANOTHER allocation is not exported: the
-    // call falls back to the scratch schedules on every rank.  The cost: a
-    // freed allocation stays alive while peers keep its mapping.
-    me.valid = 0;
     me.nalloc = 0;
     me.nbuf = (uint32_t)nbuf;
-    bool valid = !ch.direct_off && nbuf >= 1 && nbuf <= kDirectBufsMax;
-    const auto t_export = std::chrono::steady_clock::now();
+    if (ch.direct_off || nbuf < 1 || nbuf > kDirectBufsMax) return false;
     std::unordered_map<uint64_t, uint32_t> alloc_index;  // allocation id -> index in me.alloc
-    std::vector<char*> own_base;                          // index -> this rank's allocation base
-    for (int b = 0; b < nbuf && valid; ++b) {
+    for (int b = 0; b < nbuf; ++b) {
         char* buf = bufs[b];
         unsigned long long id = 0;
         hipDeviceptr_t base = nullptr;
         size_t size = 0;
         hipPointerAttribute_t at;
-        valid = hipPointerGetAttributes(&at, buf) == hipSuccess && at.type == hipMemoryTypeDevice &&
-                hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)buf) == hipSuccess &&
-                hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)buf) == hipSuccess && base != nullptr &&
-                buf + bytes[b] <= (char*)base + size;
+        const bool dev = hipPointerGetAttributes(&at, buf) == hipSuccess && at.type == hipMemoryTypeDevice &&
+                         hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)buf) ==
+                             hipSuccess &&
+                         hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)buf) == hipSuccess && base != nullptr &&
+                         buf + bytes[b] <= (char*)base + size;
         (void)hipGetLastError();
-        if (!valid) break;
+        if (!dev) return false;
         auto ix = alloc_index.find((uint64_t)id);
         const uint32_t ai = ix != alloc_index.end() ? ix->second : me.nalloc;
         if (ai == me.nalloc) {  // this call's first buffer in that allocation: export it
@@ -1127,14 +1124,11 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
                 fprintf(stderr, "rdc-direct r%d call %llu: buffer %d %p id %llu base %p size %zu%s%s\n", rank_,
                         (unsigned long long)call, b, (void*)buf, id, (void*)base, size,
                         why ? ": not exported, " : "", why ? why : "");
-            if (why) {
-                valid = false;
-                break;
-            }
+            if (why) return false;
             me.alloc[ai].id = (uint64_t)id;
             me.alloc[ai].handle = it->second.handle;
             alloc_index.emplace((uint64_t)id, ai);
-            own_base.push_back((char*)base);
+            own_base->push_back((char*)base);
             ++me.nalloc;
         }
         me.buf[b].alloc = ai;
@@ -1142,9 +1136,132 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
         me.buf[b].off = (uint64_t)(buf - (char*)base);
         me.buf[b].bytes = bytes[b];
     }
-    me.valid = valid ? 1 : 0;
-    const double export_us =
-        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_export).count();
+    return true;
+}
+
+// Step 2: every rank's allocations as mapped in this process (*amap, indexed
+// q * kDirectAllocsMax + i; this rank's own from own_base), opening the ones
+// not mapped yet; false when one cannot be mapped.
+bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,
+                                  std::vector<char*>* amap) {
+    Channel& ch = *ch_;
+    amap->assign((size_t)n_ * kDirectAllocsMax, nullptr);
+    for (int p = 0; p < n_; ++p)
+        for (uint32_t i = 0; i < slots[p].nalloc; ++i) {
+            char*& dst = (*amap)[(size_t)p * kDirectAllocsMax + i];
+            if (p == rank_) {
+                dst = own_base[i];
+                continue;
+            }
+            auto key = std::make_pair(p, slots[p].alloc[i].id);
+            auto it = ch.dmaps.find(key);
+            if (it == ch.dmaps.end()) {
+                if (ch.dmaps.size() >= kDirectMapsMax) return false;  // full: no new mappings
+                void* m = nullptr;
+                if (hipIpcOpenMemHandle(&m, slots[p].alloc[i].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+                    !m) {
+                    (void)hipGetLastError();
+                    return false;
+                }
+                // a pointer this rank already holds for another allocation
+                // would be the stale mapping described above: never use it
+                bool dup = false;
+                for (auto& o : ch.dmaps) dup = dup || o.second == (char*)m;
+                if (direct_log())
+                    fprintf(stderr, "rdc-direct r%d call %llu: open peer %d id %llu -> %p%s\n", rank_,
+                            (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id, m,
+                            dup ? " (a mapping already held: not used)" : "");
+                if (dup) return false;
+                it = ch.dmaps.emplace(key, static_cast<char*>(m)).first;
+            }
+            dst = it->second;
+        }
+    return true;
+}
+
+// The device table of a coalesced direct launch: this owner's items (chunk
+// rank_ of every buffer in pieces of at most `tile`: {buffer, byte offset,
+// length} as 3 words), then every rank's buffer addresses as mapped here
+// (ptr[q * nbuf + b]).  Cached by the layout (every rank's allocations and
+// offsets), so a repeated bucket list uploads nothing; evicted tables are
+// freed stream-ordered and their host copies kept until the upload is done.
+const Communicator::DirectTable& Communicator::DirectTableFor(const DirectDesc* slots, const uint64_t* bytes,
+                                                              int nbuf, size_t esz, uint64_t tile,
+                                                              const std::vector<char*>& amap, hipStream_t stream) {
+    std::vector<uint64_t> key;
+    key.reserve(2 + (size_t)nbuf * (1 + 2 * (size_t)n_));
+    key.push_back(esz);
+    key.push_back(tile);
+    for (int b = 0; b < nbuf; ++b) key.push_back(bytes[b]);
+    for (int p = 0; p < n_; ++p)
+        for (int b = 0; b < nbuf; ++b) {
+            key.push_back(slots[p].alloc[slots[p].buf[b].alloc].id);
+            key.push_back(slots[p].buf[b].off);
+        }
+    auto it = direct_tables_.find(key);
+    if (it == direct_tables_.end()) {
+        if (direct_tables_.size() >= 16) {  // evict the least recently used layout
+            auto lru = direct_tables_.begin();
+            for (auto j = direct_tables_.begin(); j != direct_tables_.end(); ++j)
+                if (j->second.last_use < lru->second.last_use) lru = j;
+            if (lru->second.dtable) hip_check(hipFreeAsync(lru->second.dtable, stream), "release direct table");
+            hipEvent_t ev = nullptr;
+            hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+            hip_check(hipEventRecord(ev, stream), "record");
+            direct_retired_.emplace_back(ev, lru->second.host);
+            direct_tables_.erase(lru);
+        }
+        for (size_t i = 0; i < direct_retired_.size();) {  // host copies whose upload has surely finished
+            if (hipEventQuery(direct_retired_[i].first) == hipSuccess) {
+                (void)hipEventDestroy(direct_retired_[i].first);
+                direct_retired_[i] = direct_retired_.back();
+                direct_retired_.pop_back();
+            } else {
+                (void)hipGetLastError();
+                ++i;
+            }
+        }
+        auto host = std::make_shared<std::vector<uint64_t>>();
+        int nitems = 0;
+        for (int b = 0; b < nbuf; ++b) {
+            int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+            SplitRanges((int64_t)(bytes[b] / esz), n_, cb, ce);
+            const uint64_t so = (uint64_t)cb[rank_] * esz, sl = (uint64_t)(ce[rank_] - cb[rank_]) * esz;
+            for (uint64_t x = 0; x < sl; x += tile) {
+                host->push_back((uint64_t)b);
+                host->push_back(so + x);
+                host->push_back(std::min<uint64_t>(tile, sl - x));
+                ++nitems;
+            }
+        }
+        for (int p = 0; p < n_; ++p)
+            for (int b = 0; b < nbuf; ++b)
+                host->push_back((uint64_t)(uintptr_t)(amap[(size_t)p * kDirectAllocsMax + slots[p].buf[b].alloc] +
+                                                      slots[p].buf[b].off));
+        DirectTable t;
+        t.nitems = nitems;
+        t.tile = tile;
+        t.host = host;
+        const size_t tb = host->size() * sizeof(uint64_t);
+        hip_check(hipMallocAsync(&t.dtable, tb, stream), "allocate direct table");
+        hip_check(hipMemcpyAsync(t.dtable, host->data(), tb, hipMemcpyHostToDevice, stream), "upload direct table");
+        it = direct_tables_.emplace(std::move(key), t).first;
+    }
+    it->second.last_use = ++direct_tick_;
+    return it->second;
+}
+
+bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const uint64_t* bytes, int nbuf,
+                                   size_t esz, hipStream_t stream) {
+    Channel& ch = *ch_;
+    const uint64_t call = ++ch.dcalls;  // the same on every rank (DirectEligible)
+    DirectDesc* slots = reinterpret_cast<DirectDesc*>(ch.dreg.get()) + (call & 1) * (uint64_t)n_;
+    DirectDesc& me = slots[rank_];
+    const auto t0 = std::chrono::steady_clock::now();
+    // 1) publish this rank's buffers
+    std::vector<char*> own_base;
+    me.valid = DirectExport(me, bufs, bytes, nbuf, call, &own_base) ? 1 : 0;
+    const double export_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     __atomic_store_n(&me.stamp0, call, __ATOMIC_RELEASE);
     if (!rendezvous_wait(slots, n_, &DirectDesc::stamp0, call, cfg_.timeout_s))
         throw std::runtime_error("rdc: registered-buffer rendezvous timed out (a peer did not join the allreduce)");
@@ -1156,47 +1273,8 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
         for (int b = 0; b < nbuf && usable; ++b)
             usable = slots[p].buf[b].bytes == bytes[b] && slots[p].buf[b].mis16 == me.buf[b].mis16;
     }
-    std::vector<char*> amap_v((size_t)n_ * kDirectAllocsMax);  // rank q's allocation i as mapped here
-    auto amap = [&](int q, uint32_t i) -> char*& { return amap_v[(size_t)q * kDirectAllocsMax + i]; };
-    int ok = usable ? 1 : 0;
-    for (int p = 0; p < n_ && ok; ++p) {
-        for (uint32_t i = 0; i < slots[p].nalloc && ok; ++i) {
-            if (p == rank_) {  // this rank's own allocation
-                amap(p, i) = own_base[i];
-                continue;
-            }
-            auto key = std::make_pair(p, slots[p].alloc[i].id);
-            auto it = ch.dmaps.find(key);
-            if (it == ch.dmaps.end()) {
-                if (ch.dmaps.size() >= kDirectMapsMax) {  // full: no new mappings (fallback)
-                    ok = 0;
-                    break;
-                }
-                void* m = nullptr;
-                if (hipIpcOpenMemHandle(&m, slots[p].alloc[i].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
-                    !m) {
-                    (void)hipGetLastError();
-                    ok = 0;
-                    break;
-                }
-                // a pointer this rank already holds for another allocation
-                // would be the stale mapping described above: never use it
-                bool dup = false;
-                for (auto& o : ch.dmaps) dup = dup || o.second == (char*)m;
-                if (direct_log())
-                    fprintf(stderr, "rdc-direct r%d call %llu: open peer %d id %llu -> %p%s\n", rank_,
-                            (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id, m,
-                            dup ? " (a mapping already held: not used)" : "");
-                if (dup) {
-                    ok = 0;
-                    break;
-                }
-                it = ch.dmaps.emplace(key, static_cast<char*>(m)).first;
-            }
-            amap(p, i) = it->second;
-        }
-    }
-    me.ok = ok;
+    std::vector<char*> amap;  // rank q's allocation i as mapped here, at q * kDirectAllocsMax + i
+    me.ok = usable && DirectMapPeers(slots, own_base, call, &amap) ? 1 : 0;
     __atomic_store_n(&me.stamp1, call, __ATOMIC_RELEASE);
     if (!rendezvous_wait(slots, n_, &DirectDesc::stamp1, call, cfg_.timeout_s))
         throw std::runtime_error("rdc: registered-buffer rendezvous timed out (a peer did not join the allreduce)");
@@ -1204,7 +1282,7 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     if (direct_log())
         fprintf(stderr, "rdc-direct r%d call %llu: %d buffers in %u allocations, export %.1f us, total %.1f us, %s\n",
                 rank_, (unsigned long long)call, nbuf, me.nalloc, export_us,
-                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_export).count(),
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(),
                 usable ? "direct" : "fallback");
     if (!usable) return false;  // every rank saw the same slots: all fall back together
     // 3) one launch: owner r folds chunk r of every buffer in place
@@ -1222,91 +1300,26 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     tile = (tile + 255) & ~(uint64_t)255;
     int grid = 1;
     if (nbuf == 1) {
-        char* buf = bufs[0];
         int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
         SplitRanges((int64_t)(bytes[0] / esz), n_, cb, ce);
-        a.user = buf;
+        a.user = bufs[0];
         for (int c = 0; c < n_; ++c) {
             a.off[c] = (uint64_t)cb[c] * esz;
             a.len[c] = (uint64_t)(ce[c] - cb[c]) * esz;
-            a.cbuf[c] = amap(c, slots[c].buf[0].alloc) + slots[c].buf[0].off;
+            a.cbuf[c] = amap[(size_t)c * kDirectAllocsMax + slots[c].buf[0].alloc] + slots[c].buf[0].off;
         }
         const int tiles = (int)std::max<uint64_t>(1, (a.len[rank_] + tile - 1) / tile);
         a.tile_bytes = tile;
         a.tiles[rank_] = a.len[rank_] ? tiles : 0;
         grid = std::max(1, std::min(tiles, grid_cap));
     } else {
-        // items of this owner: chunk rank_ of every buffer in pieces of at
-        // most `tile`; then every rank's buffer addresses as mapped here.
-        // Cached by the layout (every rank's allocations and offsets).
-        std::vector<uint64_t> key;
-        key.reserve(2 + (size_t)nbuf * (1 + 2 * (size_t)n_));
-        key.push_back(esz);
-        key.push_back(tile);
-        for (int b = 0; b < nbuf; ++b) key.push_back(bytes[b]);
-        for (int p = 0; p < n_; ++p)
-            for (int b = 0; b < nbuf; ++b) {
-                key.push_back(slots[p].alloc[slots[p].buf[b].alloc].id);
-                key.push_back(slots[p].buf[b].off);
-            }
-        auto it = direct_tables_.find(key);
-        if (it == direct_tables_.end()) {
-            if (direct_tables_.size() >= 16) {  // evict the least recently used layout
-                auto lru = direct_tables_.begin();
-                for (auto j = direct_tables_.begin(); j != direct_tables_.end(); ++j)
-                    if (j->second.last_use < lru->second.last_use) lru = j;
-                if (lru->second.dtable) hip_check(hipFreeAsync(lru->second.dtable, stream), "release direct table");
-                hipEvent_t ev = nullptr;
-                hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
-                hip_check(hipEventRecord(ev, stream), "record");
-                direct_retired_.emplace_back(ev, lru->second.host);
-                direct_tables_.erase(lru);
-            }
-            for (size_t i = 0; i < direct_retired_.size();) {  // host copies whose upload has surely finished
-                if (hipEventQuery(direct_retired_[i].first) == hipSuccess) {
-                    (void)hipEventDestroy(direct_retired_[i].first);
-                    direct_retired_[i] = direct_retired_.back();
-                    direct_retired_.pop_back();
-                } else {
-                    (void)hipGetLastError();
-                    ++i;
-                }
-            }
-            // DirectItem {buffer, byte offset in it, length} as 3 words, then
-            // ptr[q * nbuf + b]
-            auto host = std::make_shared<std::vector<uint64_t>>();
-            int nitems = 0;
-            for (int b = 0; b < nbuf; ++b) {
-                int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
-                SplitRanges((int64_t)(bytes[b] / esz), n_, cb, ce);
-                const uint64_t so = (uint64_t)cb[rank_] * esz, sl = (uint64_t)(ce[rank_] - cb[rank_]) * esz;
-                for (uint64_t x = 0; x < sl; x += tile) {
-                    host->push_back((uint64_t)b);
-                    host->push_back(so + x);
-                    host->push_back(std::min<uint64_t>(tile, sl - x));
-                    ++nitems;
-                }
-            }
-            for (int p = 0; p < n_; ++p)
-                for (int b = 0; b < nbuf; ++b)
-                    host->push_back((uint64_t)(uintptr_t)(amap(p, slots[p].buf[b].alloc) + slots[p].buf[b].off));
-            DirectTable t;
-            t.nitems = nitems;
-            t.tile = tile;
-            t.host = host;
-            const size_t tb = host->size() * sizeof(uint64_t);
-            hip_check(hipMallocAsync(&t.dtable, tb, stream), "allocate direct table");
-            hip_check(hipMemcpyAsync(t.dtable, host->data(), tb, hipMemcpyHostToDevice, stream), "upload direct table");
-            it = direct_tables_.emplace(std::move(key), t).first;
-        }
-        it->second.last_use = ++direct_tick_;
+        const DirectTable& t = DirectTableFor(slots, bytes, nbuf, esz, tile, amap, stream);
         a.user = bufs[0];
-        a.units = it->second.dtable;
-        a.nunits = it->second.nitems;
+        a.units = t.dtable;
+        a.nunits = t.nitems;
         a.dnbuf = nbuf;
         a.tile_bytes = tile;
-        grid = std::max(1, std::min(it->second.nitems, grid_cap));
-        if (it->second.nitems == 0) grid = 1;
+        grid = std::max(1, std::min(t.nitems, grid_cap));
     }
     if (notify_) {
         a.notify = notify_;

@@ -342,6 +342,10 @@ private:
     // one buffer (nbuf = 1) or a coalesced list; bytes[b] > 0 for every b
     bool AllreduceDirect(const KernelSet& ks, char* const* bufs, const uint64_t* bytes, int nbuf, size_t esz,
                          hipStream_t stream);
+    bool DirectExport(DirectDesc& me, char* const* bufs, const uint64_t* bytes, int nbuf, uint64_t call,
+                      std::vector<char*>* own_base);
+    bool DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,
+                        std::vector<char*>* amap);
     // device tables of coalesced direct launches: owner items + every rank's
     // buffer addresses, cached by the call's layout
     struct DirectTable {
@@ -352,6 +356,8 @@ private:
         uint64_t last_use = 0;
     };
     std::map<std::vector<uint64_t>, DirectTable> direct_tables_;
+    const DirectTable& DirectTableFor(const DirectDesc* slots, const uint64_t* bytes, int nbuf, size_t esz,
+                                      uint64_t tile, const std::vector<char*>& amap, hipStream_t stream);
     std::vector<std::pair<hipEvent_t, std::shared_ptr<std::vector<uint64_t>>>> direct_retired_;
     uint64_t direct_tick_ = 0;
     void CoalescedTree(const KernelSet& ks, void* const* bufs, const size_t* counts, int nbuf, size_t esz,
