@@ -193,10 +193,15 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
     def timed(one, nsteps=steps):
         return timed_ms(one, comm, sp, dist, torch, nsteps)
 
-    def entry(ms, nbytes, what, nsteps=steps):
+    def entry(ms, nbytes, what, nsteps=steps, device=True):
         bb = nbytes / (ms * 1e-3) / 1e9 * 2 * (world - 1) / world
-        return {"workload": what, "bytes_per_gpu": nbytes, "ms_per_step": round(ms, 4), "busbw_GBps": round(bb, 2),
-                "steps": nsteps}
+        e = {"workload": what, "bytes_per_gpu": nbytes, "ms_per_step": round(ms, 4), "busbw_GBps": round(bb, 2),
+             "steps": nsteps}
+        if device:  # the schedule the last timed call launched (RdcCommLastLaunch)
+            ll = (ctypes.c_uint64 * 6)()
+            check_call(lib.RdcCommLastLaunch(comm.handle, ll))
+            e["schedule"] = {1: "ring", 2: "mesh", 3: "oneshot", 4: "tree", 5: "mesh_pull", 6: "direct"}.get(int(ll[5]))
+        return e
 
     h = torch.empty(S // 2, dtype=torch.float16, device="cuda")
     rdc_amd.fill_(h, 0x5EED0000, rank)
@@ -223,7 +228,7 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
     ms = timed_ms(lambda: check_call(lib.RdcAllreduce(pa, 1024, 6, 2, None, None)), comm, sp, dist, torch,
                   max(steps, 2000), warm=20, synchronous=True)
     e = entry(ms, 4096, "4 KiB float32 allreduce of HOST memory via RdcAllreduce (cfg1 shape, synchronous; "
-              "clock stops when the last call returns, max over ranks)", max(steps, 2000))
+              "clock stops when the last call returns, max over ranks)", max(steps, 2000), device=False)
     e["us_per_call"] = round(ms * 1e3, 2)
     out["cfg1_host_4KiB"] = e
     # the PCIe-inclusive rate (north star: rdc buffers begin and end in host
@@ -236,7 +241,7 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
         ms = timed_ms(lambda: check_call(lib.RdcAllreduce(ph, hb.size, 6, 2, None, None)), comm, sp, dist, torch, 5,
                       warm=2, synchronous=True)
         e = entry(ms, hb.nbytes, "64 MiB float32 allreduce of HOST (pageable) memory via RdcAllreduce: copy in, "
-                  "H2D, allreduce, D2H, pipelined (PCIe-inclusive; synchronous, max over ranks)", 5)
+                  "H2D, allreduce, D2H, pipelined (PCIe-inclusive; synchronous, max over ranks)", 5, device=False)
         e["algbw_GBps_pcie_inclusive"] = round(hb.nbytes / (ms * 1e-3) / 1e9, 2)
         out["host_64MiB"] = e
         del hb
@@ -259,7 +264,7 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
             check_call(lib.RdcDelBuffer(reg))
         e = entry(ms, hb.nbytes, "64 MiB float32 allreduce of HOST memory registered with RdcNewBuffer(pinned=1) "
                   "via RdcAllreduce: H2D, allreduce, D2H in place, pipelined (PCIe-inclusive; synchronous, max "
-                  "over ranks)", 5)
+                  "over ranks)", 5, device=False)
         e["algbw_GBps_pcie_inclusive"] = round(hb.nbytes / (ms * 1e-3) / 1e9, 2)
         out["host_64MiB_registered"] = e
         del hb
@@ -286,7 +291,7 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
             check_call(lib.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(f.data_ptr()), nb // 4, 6, 2, 0, sp))
         ms = timed(one, ns)
         e = entry(ms, nb, "in-place allreduce(sum) of %d KiB float32" % (nb >> 10), ns)
-        sizes[str(nb)] = {k: e[k] for k in ("ms_per_step", "busbw_GBps", "steps")}
+        sizes[str(nb)] = {k: e[k] for k in ("ms_per_step", "busbw_GBps", "steps", "schedule")}
         if autotune_reps > 0 and nb < S:
             t = comm.autotune(nb, 6, reps=autotune_reps, stream=sp)
             if t["chosen"] is not None:
