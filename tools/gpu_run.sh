@@ -13,6 +13,7 @@
 #     benchN:<n>[:args]     N-rank line, ranks sharing the GPU (bench_n<n>.txt); args: bench.py flags, ',' = ' '
 #     pmc1                  N=1 k_reduce HBM counters (FETCH_SIZE, WRITE_SIZE passes) -> traffic.json
 #     pmc0:<algo>:<n>:<B>   rank 0 of an n-rank allreduce under --pmc, the others unprofiled
+#     ktrace0:<algo>:<n>:<B> rank 0 of an n-rank bench under --kernel-trace --stats, the others unprofiled
 #     ab:<name>:<envA>:<envB>[:args]
 #                           bench.py N=2 alternated A B A B with two env settings (',' separates
 #                           VAR=value pairs; '-' = none), e.g. ab:tile:RDC_TILE_BYTES=256K:-
@@ -87,6 +88,8 @@ for step in "$@"; do
             "k_reduce<2, float" reduce_sum_f32_1073741824 $P/traffic.json ;;
     pmc0)
         bash tools/pmc_rank0.sh $a1 $a2 $a3 $OUT/pmc_rank0_${a1}_n${a2} || exit 1 ;;
+    ktrace0)
+        bash tools/ktrace_rank0.sh $a1 $a2 $a3 $OUT/ktrace_rank0_${a1}_n${a2} || exit 1 ;;
     ab)
         extra=$(echo "${a4:-}" | tr ',' ' ')
         for v in A B A B; do
