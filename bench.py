@@ -763,6 +763,11 @@ def main():
             if os.environ.get("RDC_BENCH_FAIL_AUTOTUNE") == str(rank):  # test hook: this rank fails
                 raise RuntimeError("injected autotune failure (RDC_BENCH_FAIL_AUTOTUNE)")
             tuned = comm.autotune(S, dt_enum, reps=args.autotune_reps, stream=sp)
+            # the direct schedule's self-check (run by Autotune before it times
+            # that schedule): 1 passed, 2 failed (then not a candidate), 0 not run
+            dc = ctypes.c_uint64()
+            check_call(_LIB.RdcCommGetParam(comm.handle, b"direct_check", ctypes.byref(dc)))
+            tuned["direct_selfcheck"] = {0: "not run", 1: "passed", 2: "failed"}.get(int(dc.value), int(dc.value))
             failed = 0.0
         except Exception as e:  # noqa: BLE001 - recorded in the line
             tuned, failed = {"error": str(e)[:300]}, 1.0

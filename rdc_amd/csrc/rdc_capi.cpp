@@ -641,6 +641,7 @@ int RdcCommGetParam(void* comm, const char* key, uint64_t* value) {
         else if (k == "coalesced_misaligned") *value = (uint64_t)c->coalesced_misaligned_;
         else if (k == "shares_scratch") *value = c->shares_channel() ? 1 : 0;
         else if (k == "host_registered_calls") *value = HostRegisteredCalls();
+        else if (k == "direct_check") *value = (uint64_t)c->DirectCheckResult();
         else throw std::invalid_argument("rdc: unknown parameter " + k);
     });
 }

@@ -335,6 +335,7 @@ Channel::~Channel() {
     }
     if (last_ev) (void)hipEventDestroy(last_ev);
     if (tune_buf) (void)hipFree(tune_buf);
+    for (void* p : tune_old) (void)hipFree(p);
     if (scratch) (void)hipFree(scratch);
     if (scratch_ag) (void)hipFree(scratch_ag);
     if (flags) (void)hipFree(flags);
@@ -1337,6 +1338,61 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     return true;
 }
 
+// The channel's own hipMalloc buffer of at least `bytes` (Autotune, the
+// direct self-check): peers map it, so an outgrown one is kept, not freed.
+void Communicator::TuneBuffer(size_t bytes) {
+    Channel& ch = *ch_;
+    if (ch.tune_bytes >= bytes) return;
+    if (ch.tune_buf) ch.tune_old.push_back(ch.tune_buf);
+    ch.tune_buf = nullptr;
+    ch.tune_bytes = 0;
+    hip_check(hipMalloc(&ch.tune_buf, bytes), "autotune buffer");
+    ch.tune_bytes = bytes;
+}
+
+// One int32 BitOR allreduce of 4 MiB by the direct schedule and one by the
+// ring on the same input (the ring's result is the reference: every schedule
+// gives the same bits).  The direct result is then read by a KERNEL
+// (k_reduce: 0 | x) so that it comes through the caches of this GPU, where a
+// line written by another GPU could be stale, not through a DMA engine.  Both
+// land on the host, every rank compares, and the ranks agree (MAX) before
+// anyone uses the answer.  A failure is reported on stderr and the direct
+// schedule is left out of every Autotune on this channel.
+int Communicator::DirectSelfCheck(hipStream_t stream) {
+    Channel& ch = *ch_;
+    if (ch.direct_check) return ch.direct_check;
+    KernelSet ks;
+    if (!get_kernels(RDC_DT_INT32, RDC_OP_BITOR, &ks)) throw std::logic_error("rdc: no int32 BitOR kernels");
+    const size_t count = (size_t)1 << 20, nb = count * sizeof(int32_t);
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    TuneBuffer(3 * nb);
+    char* x = static_cast<char*>(ch.tune_buf);
+    char* y = x + nb;
+    char* z = y + nb;
+    DeviceFill(x, count, RDC_DT_INT32, 0x5EEDC4ECull, rank_, stream);
+    hip_check(hipMemcpyAsync(y, x, nb, hipMemcpyDeviceToDevice, stream), "self-check copy");
+    hip_check(hipMemsetAsync(z, 0, nb, stream), "self-check zero");
+    Allreduce(y, count, RDC_DT_INT32, RDC_OP_BITOR, stream, RDC_ALGO_RING);
+    Allreduce(x, count, RDC_DT_INT32, RDC_OP_BITOR, stream, RDC_ALGO_DIRECT);
+    const bool took = last_launch_[5] == RDC_ALGO_DIRECT;
+    hip_check(ks.reduce(z, x, nb, 2 * cus_min_, stream), "self-check read-back");
+    std::vector<char> hy(nb), hz(nb);
+    hip_check(hipMemcpyAsync(hy.data(), y, nb, hipMemcpyDeviceToHost, stream), "D2H");
+    hip_check(hipMemcpyAsync(hz.data(), z, nb, hipMemcpyDeviceToHost, stream), "D2H");
+    Check(stream);
+    int32_t bad = (!took || memcmp(hy.data(), hz.data(), nb) != 0) ? 1 : 0;
+    // agree: every rank's flag, MAX over ranks (a scratch schedule: 4 bytes)
+    hip_check(hipMemcpyAsync(z, &bad, sizeof(bad), hipMemcpyHostToDevice, stream), "H2D");
+    Allreduce(z, 1, RDC_DT_INT32, RDC_OP_MAX, stream, RDC_ALGO_AUTO);
+    hip_check(hipMemcpyAsync(&bad, z, sizeof(bad), hipMemcpyDeviceToHost, stream), "D2H");
+    Check(stream);
+    ch.direct_check = bad ? 2 : 1;
+    if (bad && rank_ == 0)
+        fprintf(stderr, "rdc: the direct schedule failed its self-check on this node (%s); Autotune leaves it out\n",
+                took ? "results differ from the ring's" : "it did not run");
+    return ch.direct_check;
+}
+
 // Closes every peer-buffer mapping of the direct schedule and turns the
 // schedule off for the channel (re-mapping into just-unmapped address ranges
 // faulted the GPU in round 5's tests, so nothing is mapped again).  A mapping
@@ -1819,6 +1875,8 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     // stay alive in the peers' mappings and its address could not be
     // exported again (AllreduceDirect)
     const bool direct_cand = ch_ && ch_->dreg && !ch_->direct_off;
+    // the direct schedule is a candidate only where it passed its self-check
+    const bool direct_ok = direct_cand && DirectSelfCheck(stream) == 1;
     auto release = [&] {
         if (buf && !direct_cand) (void)hipFreeAsync(buf, stream);
         if (dms) (void)hipFreeAsync(dms, stream);
@@ -1828,14 +1886,7 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     };
     try {
         if (direct_cand) {
-            if (ch_->tune_bytes < count * esz) {
-                hip_check(hipStreamSynchronize(stream), "sync");
-                if (ch_->tune_buf) hip_check(hipFree(ch_->tune_buf), "autotune buffer");
-                ch_->tune_buf = nullptr;
-                ch_->tune_bytes = 0;
-                hip_check(hipMalloc(&ch_->tune_buf, count * esz), "autotune buffer");
-                ch_->tune_bytes = count * esz;
-            }
+            TuneBuffer(count * esz);
             buf = ch_->tune_buf;
         } else {
             hip_check(hipMallocAsync(&buf, count * esz, stream), "autotune buffer");
@@ -1920,7 +1971,7 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
         // (and the direct schedule on registered buffers where the ranks are
         // processes: no scratch, each buffer read and written once)
         for (int a : {RDC_ALGO_RING, RDC_ALGO_MESH, RDC_ALGO_MESH_PULL, RDC_ALGO_ONESHOT, RDC_ALGO_DIRECT})
-            if (a != rule && (a != RDC_ALGO_ONESHOT || oneshot_fits) && (a != RDC_ALGO_DIRECT || direct_cand))
+            if (a != rule && (a != RDC_ALGO_ONESHOT || oneshot_fits) && (a != RDC_ALGO_DIRECT || direct_ok))
                 add(a, s0, r0, g0, t0);
         int w = stage(lo);
         if (cand[w].algo == RDC_ALGO_ONESHOT) {

@@ -126,6 +126,9 @@ struct Channel {
     bool direct_off = false;  // RdcCommDirectRelease ran: the direct schedule stays off
     void* tune_buf = nullptr;  // Autotune's buffer, kept (peers map it) until the channel closes
     size_t tune_bytes = 0;
+    std::vector<void*> tune_old;  // outgrown tune buffers: never freed before the channel closes (a
+                                  // freed address handed out again could not be exported)
+    int direct_check = 0;         // DirectSelfCheck: 0 not run, 1 passed, 2 failed
 };
 
 // One rank's slot of the registered-buffer rendezvous (shared host memory):
@@ -224,6 +227,11 @@ public:
     // closes this rank's mappings of peer buffers and turns the direct
     // schedule off for this communicator's channel (RdcCommDirectRelease)
     void DirectUnmapAll();
+    // collective: one direct allreduce against the ring on the same input,
+    // read back through the caches; 1 passed, 2 failed (cached per channel);
+    // Autotune only times the direct schedule on a node where it passed
+    int DirectSelfCheck(hipStream_t stream);
+    int DirectCheckResult() const { return ch_ ? ch_->direct_check : 0; }
 
     // Collective (every rank, same arguments, no collective in flight): time
     // the schedules (ring, mesh, one-shot where it fits) and then the launch
@@ -342,6 +350,7 @@ private:
     // one buffer (nbuf = 1) or a coalesced list; bytes[b] > 0 for every b
     bool AllreduceDirect(const KernelSet& ks, char* const* bufs, const uint64_t* bytes, int nbuf, size_t esz,
                          hipStream_t stream);
+    void TuneBuffer(size_t bytes);
     bool DirectExport(DirectDesc& me, char* const* bufs, const uint64_t* bytes, int nbuf, uint64_t call,
                       std::vector<char*>* own_base);
     bool DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,

@@ -214,6 +214,9 @@ def main():
             continue
         if c.get("autotune"):  # RdcCommAutotune for this many bytes, then the case runs on the chosen shape
             res = comm.autotune(c["autotune"], dtype, reps=2, stream=sp)
+            dc = ctypes.c_uint64()
+            check_call(_LIB.RdcCommGetParam(comm.handle, b"direct_check", ctypes.byref(dc)))
+            res["direct_check"] = int(dc.value)  # the direct schedule's self-check (1 = passed)
             open(os.path.join(outdir, "case%d_rank%d.tune" % (i, rank)), "w").write(json.dumps(res))
         if c.get("last_launch"):  # record the launch shape the library chose (grid clamp checks)
             ll = (ctypes.c_uint64 * 6)()

@@ -1040,6 +1040,8 @@ def test_mp_autotune_agrees_and_stays_bit_exact(world):
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
     small = [json.load(open(os.path.join(tmp, "case0_rank%d.tune" % r))) for r in range(world)]
     assert all(t == small[0] for t in small), small
+    # the direct schedule passed its self-check (direct vs ring, read back by a kernel) before it was timed
+    assert small[0]["direct_check"] == 1, small[0]
     # a one-shot size: the rule's schedule (the one-shot) first, then ring, mesh, the
     # pull-mode mesh and the direct schedule; the winner's shape if it has one
     sched = [c["schedule"] for c in small[0]["candidates"][:5]]
