@@ -389,6 +389,11 @@ int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int a
  * buffers [bounds[g], bounds[g+1])); fuse_bytes 0 = default. */
 int RdcPlanCoalesced(int n, const size_t* counts, int nbuf, int dtype, uint64_t* chunk_out, uint64_t* units_out,
                      int max_units, int* out_units);
+/* RdcPlanDirectItems: owner `rank`'s items of a coalesced direct launch
+ * (algo 6 over a list): Split chunk `rank` of every buffer in pieces of at
+ * most `tile` bytes, 3 words each {buffer, byte offset, bytes}. */
+int RdcPlanDirectItems(int n, int rank, const size_t* counts, int nbuf, int dtype, uint64_t tile, uint64_t* out,
+                       int max_items, int* out_items);
 int RdcPlanFuseGroups(const size_t* counts, int nbuf, int dtype, size_t fuse_bytes, int* bounds_out, int max_bounds,
                       int* out_n);
 

@@ -80,6 +80,7 @@ def _load():
         "RdcMemcpy": (i, [vp, vp, sz]),
         "RdcPlanLayout": (i, [i, sz, ctypes.POINTER(u64)]),
         "RdcPlanHbmBytes": (i, [i, sz, i, i, ctypes.POINTER(u64)]),
+        "RdcPlanDirectItems": (i, [i, i, ctypes.POINTER(sz), i, i, u64, ctypes.POINTER(u64), i, ctypes.POINTER(i)]),
         "RdcPlanHostPieceRanges": (i, [i, sz, i, u64, u64, i, ctypes.POINTER(u64), ctypes.POINTER(u64),
                                        ctypes.POINTER(ctypes.c_int)]),
         "RdcPlanAutoAlgo": (i, [i, sz, sz, sz]),

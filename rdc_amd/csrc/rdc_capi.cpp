@@ -817,6 +817,21 @@ int RdcPlanAllreduce(int n, size_t count, int dtype, size_t scratch_bytes, int a
     });
 }
 
+int RdcPlanDirectItems(int n, int rank, const size_t* counts, int nbuf, int dtype, uint64_t tile, uint64_t* out,
+                       int max_items, int* out_items) {
+    return guard([&] {
+        const size_t esz = rdc_dtype_size(dtype);
+        if (n < 1 || n > RDC_MAX_RANKS || rank < 0 || rank >= n || esz == 0 || nbuf < 0 || (nbuf && !counts) ||
+            tile == 0 || !out_items)
+            throw std::invalid_argument("rdc: bad argument");
+        std::vector<uint64_t> bytes((size_t)nbuf);
+        for (int b = 0; b < nbuf; ++b) bytes[(size_t)b] = (uint64_t)counts[b] * esz;
+        const std::vector<uint64_t> items = PlanDirectItems(n, rank, bytes.data(), nbuf, esz, tile);
+        *out_items = (int)(items.size() / 3);
+        for (size_t i = 0; i < items.size() && out && (int)(i / 3) < max_items; ++i) out[i] = items[i];
+    });
+}
+
 int RdcPlanCoalesced(int n, const size_t* counts, int nbuf, int dtype, uint64_t* chunk_out, uint64_t* units_out,
                      int max_units, int* out_units) {
     return guard([&] {

@@ -1222,19 +1222,8 @@ const Communicator::DirectTable& Communicator::DirectTableFor(const DirectDesc* 
                 ++i;
             }
         }
-        auto host = std::make_shared<std::vector<uint64_t>>();
-        int nitems = 0;
-        for (int b = 0; b < nbuf; ++b) {
-            int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
-            SplitRanges((int64_t)(bytes[b] / esz), n_, cb, ce);
-            const uint64_t so = (uint64_t)cb[rank_] * esz, sl = (uint64_t)(ce[rank_] - cb[rank_]) * esz;
-            for (uint64_t x = 0; x < sl; x += tile) {
-                host->push_back((uint64_t)b);
-                host->push_back(so + x);
-                host->push_back(std::min<uint64_t>(tile, sl - x));
-                ++nitems;
-            }
-        }
+        auto host = std::make_shared<std::vector<uint64_t>>(PlanDirectItems(n_, rank_, bytes, nbuf, esz, tile));
+        const int nitems = (int)(host->size() / 3);
         for (int p = 0; p < n_; ++p)
             for (int b = 0; b < nbuf; ++b)
                 host->push_back((uint64_t)(uintptr_t)(amap[(size_t)p * kDirectAllocsMax + slots[p].buf[b].alloc] +

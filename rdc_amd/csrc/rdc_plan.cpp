@@ -287,6 +287,21 @@ CoalescedPlan PlanCoalesced(int n, const uint64_t* counts, int nbuf, size_t esz,
     return P;
 }
 
+std::vector<uint64_t> PlanDirectItems(int n, int rank, const uint64_t* bytes, int nbuf, size_t esz, uint64_t tile) {
+    std::vector<uint64_t> items;
+    for (int b = 0; b < nbuf; ++b) {
+        int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
+        SplitRanges((int64_t)(bytes[b] / esz), n, cb, ce);
+        const uint64_t so = (uint64_t)cb[rank] * esz, sl = (uint64_t)(ce[rank] - cb[rank]) * esz;
+        for (uint64_t x = 0; x < sl; x += tile) {
+            items.push_back((uint64_t)b);
+            items.push_back(so + x);
+            items.push_back(std::min<uint64_t>(tile, sl - x));
+        }
+    }
+    return items;
+}
+
 // The reference derives the tree in three hash-container passes whose
 // iteration order decides who folds first (topo.cc:20-115, communicator_base.cc:
 // 136-149, graph.h:70-83, communicator_collective.cc:16-27).  The same

@@ -145,6 +145,11 @@ struct CoalescedPlan {
 };
 constexpr uint64_t kPackUnitMax = 128 << 10;
 CoalescedPlan PlanCoalesced(int n, const uint64_t* counts, int nbuf, size_t esz, uint64_t unit_max = kPackUnitMax);
+
+// Owner `rank`'s items of a coalesced direct launch (k_direct over a list):
+// Split chunk `rank` of every buffer (bytes[b] / esz elements) in pieces of
+// at most `tile` bytes, as {buffer, byte offset in it, bytes} triples.
+std::vector<uint64_t> PlanDirectItems(int n, int rank, const uint64_t* bytes, int nbuf, size_t esz, uint64_t tile);
 // Cut the buffer list (in order) into fusion groups of at most fuse_bytes of
 // data each; a buffer larger than fuse_bytes forms a group of its own.
 // Returns group boundaries: group g = buffers [bounds[g], bounds[g+1]).

@@ -463,3 +463,34 @@ def test_resident_grid_per_xcd_never_oversubscribes_an_xcd():
         assert 1 <= g <= max(1, want)
         room = per_cu * (cus // xcds) - per_cu * reserve
         assert g == 1 or max(_xcd_loads(g, xcds)) * ranks <= room, (want, per_cu, cus, ranks, xcds, reserve, g)
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_plan_direct_items_cover_each_owner_chunk(n):
+    """The coalesced direct launch's owner items (RdcPlanDirectItems, the
+    table k_direct walks): for every owner r, the items are exactly Split
+    chunk r of every buffer (oracle split), in order, cut into pieces of at
+    most `tile` bytes; every element of every buffer belongs to exactly one
+    owner's items."""
+    from rdc_amd._lib import _LIB
+    counts = [1024, 7, 0, 100003, 1, 65536, 3, (1 << 18) + 3]
+    for dt, esz in ((6, 4), (10, 2), (0, 1)):
+        for tile in (256, 64 << 10):
+            covered = [np.zeros(c, dtype=np.int32) for c in counts]
+            for r in range(n):
+                arr = (ctypes.c_size_t * len(counts))(*counts)
+                cap = 1 << 14
+                out = (ctypes.c_uint64 * (3 * cap))()
+                k = ctypes.c_int()
+                assert _LIB.RdcPlanDirectItems(n, r, arr, len(counts), dt, tile, out, cap, ctypes.byref(k)) == 0
+                items = [tuple(out[3 * i: 3 * i + 3]) for i in range(k.value)]
+                want = []
+                for b, c in enumerate(counts):
+                    lo, hi = O.split(c, n)[r]
+                    so, sl = lo * esz, (hi - lo) * esz
+                    want += [(b, so + x, min(tile, sl - x)) for x in range(0, sl, tile)]
+                assert items == want, (n, r, dt, tile)
+                for b, so, ln in items:
+                    covered[b][so // esz: (so + ln) // esz] += 1
+            assert all((cv == 1).all() for cv in covered), (n, dt, tile)
+    assert _LIB.RdcPlanDirectItems(n, n, (ctypes.c_size_t * 1)(4), 1, 6, 256, None, 0, ctypes.byref(ctypes.c_int())) != 0
