@@ -1376,7 +1376,7 @@ int Communicator::DirectSelfCheck(hipStream_t stream) {
     hip_check(hipMemcpyAsync(&bad, z, sizeof(bad), hipMemcpyDeviceToHost, stream), "D2H");
     Check(stream);
     ch.direct_check = bad ? 2 : 1;
-    if (bad && rank_ == 0)
+    if (bad && rank_ == 0 && !ch.direct_off)
         fprintf(stderr, "rdc: the direct schedule failed its self-check on this node (%s); Autotune leaves it out\n",
                 took ? "results differ from the ring's" : "it did not run");
     return ch.direct_check;
@@ -1394,6 +1394,7 @@ void Communicator::DirectUnmapAll() {
     for (auto& m : ch_->dmaps) (void)hipIpcCloseMemHandle(m.second);
     ch_->dmaps.clear();
     ch_->direct_off = true;
+    ch_->direct_check = 2;  // Autotune leaves it out from now on (every rank calls this)
     (void)hipGetLastError();
 }
 
@@ -1863,7 +1864,9 @@ int Communicator::Autotune(size_t bytes, int dtype, int reps, hipStream_t stream
     // memory has no IPC handle), kept for later autotunes — freed, it would
     // stay alive in the peers' mappings and its address could not be
     // exported again (AllreduceDirect)
-    const bool direct_cand = ch_ && ch_->dreg && !ch_->direct_off;
+    // (the same on every rank: not direct_off, which RdcCommDirectRelease
+    // sets per rank — the self-check then fails on every rank alike)
+    const bool direct_cand = ch_ && ch_->dreg;
     // the direct schedule is a candidate only where it passed its self-check
     const bool direct_ok = direct_cand && DirectSelfCheck(stream) == 1;
     auto release = [&] {
