@@ -1031,6 +1031,15 @@ bool Communicator::DirectEligible(int algo, uint64_t bytes, hipStream_t stream) 
 namespace {
 // RDC_DIRECT_LOG=1: one stderr line per export and mapping of the direct
 // schedule, for debugging the mapping cache
+// RDC_DIRECT_ROTATE=0: every owner walks its chunk from tile 0 (A/B knob)
+bool direct_rotate() {
+    static const bool on = [] {
+        const char* e = getenv("RDC_DIRECT_ROTATE");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 constexpr size_t kDirectExportsMax = 4096;  // allocations one rank exports over a channel's life
 constexpr size_t kDirectMapsMax = 16384;    // peer allocations one rank maps
 
@@ -1281,6 +1290,7 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     CollArgs a;
     FillArgsCommon(&a);
     a.kind = RDC_KIND_DIRECT;
+    a.rotate = direct_rotate() ? 1 : 0;
     const Shape sh = ShapeFor(total, RDC_ALGO_DIRECT);  // an Autotune'd grid, else the mesh's
     const int grid_cap = LaunchGrid(sh.max_blocks > 0 ? sh.max_blocks : mesh_blocks(),
                                     ks.occupancy(RDC_KIND_DIRECT, n_));

@@ -128,6 +128,7 @@ struct CollArgs {
                                          //   coalesced direct: nunits items {buffer, offset, length}
                                          //   (3 words each), then every rank's dnbuf buffer addresses
     int dnbuf;                           // coalesced direct: buffers in the list
+    int rotate;                          // direct: owner r starts its tile (item) walk r/n of the way in
     uint64_t timeout_ticks;              // wall_clock64 ticks (100 MHz) before giving up
     int uc;                              // 1: every scratch region is uncached (hand-offs need no L2
                                          //   write-back, rdc_device.h block_publish)

@@ -722,7 +722,9 @@ __device__ __forceinline__ void direct_body(const CollArgs& a, uint64_t seq) {
         // it[1], it[2] bytes; rank q's buffer b at ptr[q * dnbuf + b]
         const uint64_t* items = static_cast<const uint64_t*>(a.units);
         const uint64_t* ptr = items + 3 * (uint64_t)a.nunits;
-        for (int t = blockIdx.x; t < a.nunits; t += gridDim.x) {
+        const int rot = a.rotate ? (int)((int64_t)a.nunits * r / n) : 0;
+        for (int i = blockIdx.x; i < a.nunits; i += gridDim.x) {
+            const int t = i + rot < a.nunits ? i + rot : i + rot - a.nunits;
             const uint64_t b = items[3 * (uint64_t)t], so = items[3 * (uint64_t)t + 1];
             const uint64_t tlen = items[3 * (uint64_t)t + 2];
             if (threadIdx.x < (unsigned)n)
@@ -733,7 +735,15 @@ __device__ __forceinline__ void direct_body(const CollArgs& a, uint64_t seq) {
         }
         return;
     }
-    for (int t = blockIdx.x; t < a.tiles[r]; t += gridDim.x) {
+    // owners walk their chunks from staggered points (rotate): at any moment
+    // the n owners touch offsets that are not all exactly S/n apart in every
+    // buffer.  tools/placement_probe.py (profiles/r05/direct/placement/): one
+    // buffer placement in three runs ~20 % slower at n = 4 with or without
+    // it; the stagger gains 1-3 % at n = 4 and up to 8 % at n = 8, never loses
+    const int ntiles = a.tiles[r];
+    const int rot = a.rotate ? (int)((int64_t)ntiles * r / n) : 0;
+    for (int i = blockIdx.x; i < ntiles; i += gridDim.x) {
+        const int t = i + rot < ntiles ? i + rot : i + rot - ntiles;
         const uint64_t toff = (uint64_t)t * a.tile_bytes;
         uint64_t tlen = a.len[r] - toff;
         if (tlen > a.tile_bytes) tlen = a.tile_bytes;
