@@ -270,6 +270,22 @@ def time_extra_configs(lib, comm, S, world, rank, sp, dist, torch, steps, out, a
         del hb
     else:
         out.setdefault("skipped", []).append("host_64MiB_registered")
+    # the north star's host-inclusive rate at cfg3's size: 1 GiB of fp32 in
+    # pageable host memory through RdcAllreduce (copy in, H2D, allreduce, D2H,
+    # pipelined in 16 MiB pieces), one warm-up and two timed calls
+    if budget is None or budget.left() >= 40:
+        hb = np.ones(S // 4, dtype=np.float32)
+        ph = ctypes.c_void_p(hb.ctypes.data)
+        ms = timed_ms(lambda: check_call(lib.RdcAllreduce(ph, hb.size, 6, 2, None, None)), comm, sp, dist, torch, 2,
+                      warm=1, synchronous=True)
+        e = entry(ms, hb.nbytes, "%d MiB float32 allreduce of HOST (pageable) memory via RdcAllreduce: copy in, "
+                  "H2D, allreduce, D2H, pipelined (PCIe-inclusive; synchronous, max over ranks)" % (S >> 20), 2,
+                  device=False)
+        e["algbw_GBps_pcie_inclusive"] = round(hb.nbytes / (ms * 1e-3) / 1e9, 2)
+        out["host_1GiB"] = e
+        del hb
+    else:
+        out.setdefault("skipped", []).append("host_1GiB")
     # cfg2's 256 MiB fp32 buffer and the sizes below it (prefixes of one
     # buffer): where the mesh's per-launch fill / drain and the one-shot
     # hand-off decide the rate, for the size thresholds at this rank count
@@ -632,6 +648,128 @@ def xgmi_probe(lib, comm, sp, dist, torch, nbytes=256 << 20, reps=5):
     return out
 
 
+# Keys every N > 1 line carries, null where ranks share a
+# GPU (no link timed) but always present, so an 8-GPU run is decisive:
+REQUIRED_MULTI_KEYS = (
+    "direct_selfcheck",                      # the channel's self-check at creation (passed / failed / not run)
+    "cfg3_schedule.untuned.schedule",        # what a drop-in call gets with no tuning ...
+    "cfg3_schedule.untuned.ms_per_step",
+    "cfg3_schedule.tuned.schedule",          # ... and what the timed region ran after Autotune
+    "cfg3_schedule.tuned.ms_per_step",
+    "roofline.frac_of_bidir_ring_roofline",  # north star: >= 0.70 at n = 8
+    "roofline.frac_of_measured",             # against this line's own link probe
+    "xgmi_link_rates.one_link_one_direction_GBps",
+    "xgmi_link_rates.all_links_egress_GBps",
+    "host_inclusive_1GiB.algbw_GBps_pcie_inclusive",  # H2D + allreduce + D2H of 1 GiB of host memory
+)
+
+
+def missing_multi_keys(line, need_values=False):
+    """REQUIRED_MULTI_KEYS absent from `line` (dotted paths); need_values: also
+    the ones whose value is null (a line measured with one rank per GPU)."""
+    miss = []
+    for path in REQUIRED_MULTI_KEYS:
+        cur, ok = line, True
+        for part in path.split("."):
+            if not isinstance(cur, dict) or part not in cur:
+                ok = False
+                break
+            cur = cur[part]
+        if not ok or (need_values and cur is None):
+            miss.append(path)
+    return miss
+
+
+def compose_multi(lib, ctx):
+    """The N > 1 line's roofline and decisive keys from the run's measurements
+    (ctx: world, S, count, esz, dtype, dt_enum, buckets, unfused, algo, steps,
+    wall, kern_ms, timed_algo, gpus_here, probe, tuned, direct_selfcheck,
+    untuned = {schedule, ms_per_step} or None, host_1g = extra_configs'
+    host_1GiB entry or None).  Pure function of ctx (lib only for the HBM
+    byte model), so tests/test_bench_line.py checks a mocked 8-GPU line."""
+    world, S = ctx["world"], ctx["S"]
+    steps, wall, kern_ms = ctx["steps"], ctx["wall"], ctx["kern_ms"]
+    gpus_here = ctx["gpus_here"]
+    shared = gpus_here < world
+    algbw = S / (kern_ms * 1e-3) / 1e9
+    busbw = algbw * 2 * (world - 1) / world
+    algo_name = ctx["algo"]
+    if algo_name == "auto":  # the schedule the library launched in the timed region (RdcCommLastLaunch)
+        algo_name = ctx["timed_algo"] or "mesh"
+    peak = XGMI_LINK_DIR_GBPS * (1 if algo_name == "ring" else (world - 1))  # mesh / mesh_pull / direct: every link
+    probe = ctx["probe"]
+    roof = {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 1), "unit": "GB/s",
+            "frac": round(busbw / peak, 4), "traffic": None,
+            "kernel": "k_%s<Sum,%s>" % (algo_name, ctx["dtype"]),
+            "algorithmic_bytes_per_launch": int(2 * (world - 1) * S // world), "kernel_avg_ms": round(kern_ms, 4),
+            "frac_of_bidir_ring_roofline": round(busbw / BIDIR_RING_GBPS, 4),
+            "peak_measured": None, "frac_of_measured": None,
+            "xgmi_probe": probe}
+    if isinstance(probe, dict) and probe.get("all_links_egress_GBps"):
+        meas = probe["one_link_one_direction_GBps"] if algo_name == "ring" else probe["all_links_egress_GBps"]
+        roof["peak_measured"] = meas
+        roof["frac_of_measured"] = round(busbw / meas, 4)
+    # HBM side of the same launches: the committed byte model of the
+    # schedule (RdcPlanHbmBytes = rdc_plan.cpp ModelHbmBytes: bytes the
+    # kernels load and store, per rank) over the kernel time
+    count = ctx["count"] if ctx["buckets"] == 1 else S // ctx["esz"]
+    hm = hbm_model(lib, world, count, ctx["dt_enum"], algo_name)
+    if hm is not None:
+        per_gpu = -(-world // max(1, gpus_here)) if shared else 1   # ranks on one GPU
+        moved = hm["read_sum"] + hm["write_sum"] if (shared and gpus_here == 1) else \
+            per_gpu * (hm["read"] + hm["write"])
+        ach = moved / (kern_ms * 1e-3) / 1e9
+        hb = {"model": "rdc_plan.cpp ModelHbmBytes (RdcPlanHbmBytes): loads + stores the schedule's kernels "
+                       "issue, remote stores counted at the issuing rank",
+              "read_bytes_per_rank": hm["read"], "write_bytes_per_rank": hm["write"], "ranks_on_gpu": per_gpu,
+              "bytes_per_step": int(moved), "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+              "frac": round(ach / HBM_PEAK_GBPS, 4)}
+        # rank 0's own L2-to-memory bytes (rocprofv3 PMC, FETCH_SIZE x 2 +
+        # WRITE_SIZE, the other ranks unprofiled: tools/pmc_rank0.sh),
+        # committed per (schedule, dtype, n, S) in traffic.json
+        tr = load_traffic("%s_%s_n%d_%d" % (algo_name, DT_SHORT[ctx["dtype"]], world, S))
+        hb["traffic_per_rank"] = tr
+        hb["traffic_over_model"] = round(tr / (hm["read"] + hm["write"]), 4) if tr else None
+        roof["shared_hbm" if shared else "hbm"] = hb
+    if shared:
+        # every rank's bytes move through ONE HBM: no xGMI link is timed,
+        # so no xGMI fraction is meaningful (round 1 printed 7.996 here)
+        roof.update({"bound": "shared-hbm", "peak": None, "frac": None, "frac_of_bidir_ring_roofline": None,
+                     "frac_of_measured": None,
+                     "note": "%d ranks share %d GPU(s): rehearsal of the protocol, not an xGMI measurement; "
+                             "roofline.shared_hbm is the one HBM all ranks' bytes move through"
+                             % (world, gpus_here)})
+    keys = {}
+    keys["direct_selfcheck"] = ctx["direct_selfcheck"]
+    unt = ctx.get("untuned")
+    tuned = ctx.get("tuned")
+    tuned_ok = isinstance(tuned, dict) and tuned.get("chosen") is not None
+    keys["cfg3_schedule"] = {
+        "untuned": {"schedule": unt.get("schedule") if unt else None,
+                    "ms_per_step": unt.get("ms_per_step") if unt else None,
+                    "busbw_GBps": round(S / (unt["ms_per_step"] * 1e-3) / 1e9 * 2 * (world - 1) / world, 2)
+                    if unt and unt.get("ms_per_step") else None,
+                    "note": "the library's default for this buffer with no RdcCommAutotune (what rdc::Allreduce / "
+                            "rdc.allreduce get), timed before the autotune"},
+        "tuned": {"schedule": algo_name, "ms_per_step": round(wall / steps * 1e3, 4),
+                  "busbw_GBps": round(S / (wall / steps) / 1e9 * 2 * (world - 1) / world, 2),
+                  "source": "RdcCommAutotune on this node" if tuned_ok else "library defaults (no autotune)"},
+    }
+    rates = probe if isinstance(probe, dict) else {}
+    keys["xgmi_link_rates"] = {k: rates.get(k) for k in ("one_link_one_direction_GBps", "all_links_egress_GBps",
+                                                          "pull_one_link_GBps", "pull_all_links_GBps")}
+    keys["xgmi_link_rates"]["note"] = ("slowest rank, k_push copy kernel, %s" % (
+        "ranks share one GPU: HBM, not xGMI" if shared else "one rank per GPU")) if rates else \
+        (probe.get("error") if isinstance(probe, dict) else "not measured")
+    h1 = ctx.get("host_1g")
+    keys["host_inclusive_1GiB"] = {
+        "algbw_GBps_pcie_inclusive": h1.get("algbw_GBps_pcie_inclusive") if isinstance(h1, dict) else None,
+        "ms_per_step": h1.get("ms_per_step") if isinstance(h1, dict) else None,
+        "workload": "1 GiB float32 of pageable HOST memory through RdcAllreduce (copy in, H2D, allreduce, D2H); "
+                    "never the headline value (DESIGN.md 7.5)"}
+    return roof, algo_name, keys
+
+
 def free_port():
     import socket
     s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
@@ -753,7 +891,21 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         sync_check(comm, sp, dist, torch)
-    tuned = None
+    tuned = untuned = direct_selfcheck = None
+    if world > 1:
+        # the direct schedule's self-check, run by the library when the channel
+        # was created (round 6): 1 passed, 2 failed, 0 not run
+        dc = ctypes.c_uint64()
+        check_call(_LIB.RdcCommGetParam(comm.handle, b"direct_check", ctypes.byref(dc)))
+        direct_selfcheck = {0: "not run", 1: "passed", 2: "failed"}.get(int(dc.value), int(dc.value))
+    if world > 1 and args.autotune_reps > 0 and args.algo == "auto" and args.buckets == 1:
+        # what a drop-in caller gets: the untuned default for this buffer,
+        # timed (a few steps, max over ranks) before the autotune replaces it
+        ms_u = timed_ms(step, comm, sp, dist, torch, max(3, min(args.steps, 10)), warm=1)
+        llu = (ctypes.c_uint64 * 6)()
+        check_call(_LIB.RdcCommLastLaunch(comm.handle, llu))
+        untuned = {"schedule": {1: "ring", 2: "mesh", 3: "oneshot", 4: "tree", 5: "mesh_pull", 6: "direct"}.get(
+            int(llu[5])), "ms_per_step": round(ms_u, 4)}
     if world > 1 and args.autotune_reps > 0:
         # launch-shape autotuning on THIS node (outside the timed region; the
         # defaults were tuned where every rank shares one HBM).  Every rank
@@ -945,50 +1097,12 @@ def main():
         # busbw of the whole job: S / t x 2(n-1)/n, t = the
         # wall time per step (max over ranks, barrier-bracketed)
         value = S / (wall / args.steps) / 1e9 * 2 * (world - 1) / world
-        busbw = algbw * 2 * (world - 1) / world
-        algo_name = args.algo
-        if algo_name == "auto":  # the schedule the library launched in the timed region (RdcCommLastLaunch)
-            algo_name = timed_algo or "mesh"
-        peak = XGMI_LINK_DIR_GBPS * (1 if algo_name == "ring" else (world - 1))  # mesh / mesh_pull: every link
-        roof = {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 1), "unit": "GB/s",
-                "frac": round(busbw / peak, 4), "traffic": None,
-                "kernel": "k_%s<Sum,%s>" % (algo_name, args.dtype),
-                "algorithmic_bytes_per_launch": int(2 * (world - 1) * S // world), "kernel_avg_ms": round(kern_ms, 4),
-                "frac_of_bidir_ring_roofline": round(busbw / BIDIR_RING_GBPS, 4),
-                "xgmi_probe": probe}
-        if isinstance(probe, dict) and probe.get("all_links_egress_GBps"):
-            meas = probe["one_link_one_direction_GBps"] if algo_name == "ring" else probe["all_links_egress_GBps"]
-            roof["peak_measured"] = meas
-            roof["frac_of_measured"] = round(busbw / meas, 4)
-        # HBM side of the same launches: the committed byte model of the
-        # schedule (RdcPlanHbmBytes = rdc_plan.cpp ModelHbmBytes: bytes the
-        # kernels load and store, per rank) over the kernel time
-        hm = hbm_model(_LIB, world, count if args.buckets == 1 else S // esz, dt_enum, algo_name)
-        if hm is not None:
-            per_gpu = -(-world // max(1, gpus_here)) if shared else 1   # ranks on one GPU
-            moved = hm["read_sum"] + hm["write_sum"] if (shared and gpus_here == 1) else \
-                per_gpu * (hm["read"] + hm["write"])
-            ach = moved / (kern_ms * 1e-3) / 1e9
-            hb = {"model": "rdc_plan.cpp ModelHbmBytes (RdcPlanHbmBytes): loads + stores the schedule's kernels "
-                           "issue, remote stores counted at the issuing rank",
-                  "read_bytes_per_rank": hm["read"], "write_bytes_per_rank": hm["write"], "ranks_on_gpu": per_gpu,
-                  "bytes_per_step": int(moved), "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                  "frac": round(ach / HBM_PEAK_GBPS, 4)}
-            # rank 0's own L2-to-memory bytes (rocprofv3 PMC, FETCH_SIZE x 2 +
-            # WRITE_SIZE, the other ranks unprofiled: tools/pmc_rank0.sh),
-            # committed per (schedule, dtype, n, S) in traffic.json
-            tr = load_traffic("%s_%s_n%d_%d" % (algo_name, DT_SHORT[args.dtype], world, S))
-            hb["traffic_per_rank"] = tr
-            hb["traffic_over_model"] = round(tr / (hm["read"] + hm["write"]), 4) if tr else None
-            roof["shared_hbm" if shared else "hbm"] = hb
-        if shared:
-            # every rank's bytes move through ONE HBM: no xGMI link is timed,
-            # so no xGMI fraction is meaningful (round 1 printed 7.996 here)
-            roof.update({"bound": "shared-hbm", "peak": None, "frac": None, "frac_of_bidir_ring_roofline": None,
-                         "frac_of_measured": None,
-                         "note": "%d ranks share %d GPU(s): rehearsal of the protocol, not an xGMI measurement; "
-                                 "roofline.shared_hbm is the one HBM all ranks' bytes move through"
-                                 % (world, gpus_here)})
+        ctx = {"world": world, "S": S, "count": count, "esz": esz, "dtype": args.dtype, "dt_enum": dt_enum,
+               "buckets": args.buckets, "unfused": args.unfused, "algo": args.algo, "steps": args.steps,
+               "wall": wall, "kern_ms": kern_ms, "timed_algo": timed_algo, "gpus_here": gpus_here, "probe": probe,
+               "tuned": tuned, "direct_selfcheck": direct_selfcheck, "untuned": untuned,
+               "host_1g": extra.get("host_1GiB") if isinstance(extra, dict) else None}
+        roof, algo_name, multi_keys = compose_multi(_LIB, ctx)
         workload = "in-place allreduce(sum) of a %d MiB %s buffer per GPU, %s schedule" % (S >> 20, args.dtype,
                                                                                         algo_name)
         if args.buckets > 1:
@@ -1023,6 +1137,7 @@ def main():
         "cpu_baseline": cpu_baseline(S, args.cpu_seconds) if world == 1 else None,
     }
     if world > 1:
+        out.update(multi_keys)
         out["busbw_GBps"] = round(value, 2)
         out["ranks_share_gpu"] = shared
         out["gpu_max_hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")  # None: HIP's default (4)

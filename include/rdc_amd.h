@@ -371,6 +371,15 @@ int RdcPlanHostPieceRanges(int n, size_t count, int dtype, uint64_t lo, uint64_t
  * RDC_ALGO_MESH (2) (negative on bad arguments).
  * oneshot_bytes = RDC_ONESHOT_BYTES (0 = the default size / rank-aware rule). */
 int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_bytes);
+/* Whether an untuned automatic allreduce of `bytes` over n processes takes the
+ * registered-buffer schedule (RDC_ALGO_DIRECT) when every rank's buffer can be
+ * mapped and the channel's direct self-check passed: 1 / 0 (negative on bad
+ * arguments).  direct_min = RDC_DIRECT_BYTES: RDC_DIRECT_MIN_AUTO (the
+ * default) = beyond the one-shot sizes and from 1 MiB; 0 = never; N = from N
+ * bytes.  Replaces nothing in the reference (its one schedule is the ring);
+ * the drop-in rdc::Allreduce / rdc.allreduce calls get it without tuning. */
+#define RDC_DIRECT_MIN_AUTO (~(uint64_t)0)
+int RdcPlanDirectAuto(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_bytes, uint64_t direct_min);
 /* HBM byte model of one allreduce of `count` elements over n ranks with
  * schedule `algo` (1 ring, 2 mesh, 3 one-shot, 4 tree, 5 pull-mode mesh, 6 direct): the
  * bytes the kernels load and store, counted per access as their loops issue

@@ -84,6 +84,7 @@ def _load():
         "RdcPlanHostPieceRanges": (i, [i, sz, i, u64, u64, i, ctypes.POINTER(u64), ctypes.POINTER(u64),
                                        ctypes.POINTER(ctypes.c_int)]),
         "RdcPlanAutoAlgo": (i, [i, sz, sz, sz]),
+        "RdcPlanDirectAuto": (i, [i, sz, sz, sz, u64]),
         "RdcPlanHostPieces": (i, [sz, ctypes.POINTER(ctypes.c_uint64), i, ctypes.POINTER(i)]),
         "RdcPlanAllreduce": (i, [i, sz, i, sz, i, sz, i, ctypes.POINTER(u64), i, ctypes.POINTER(ctypes.c_int)]),
         "RdcAllreduceCoalesced": (i, [pvp, ctypes.POINTER(sz), i, i, i]),

@@ -105,7 +105,7 @@ void set_param(Manager& m, const char* name, const char* val) {
     }
     else if (k == "RDC_FUSE_BYTES_DIRECT") m.cfg.fuse_bytes_direct = std::max<size_t>(parse_unit(val), 1);
     else if (k == "RDC_POISON_SCRATCH") m.cfg.poison = atoi(val) != 0 ? 1 : 0;
-    else if (k == "RDC_DIRECT_BYTES") m.cfg.direct_min = parse_unit(val);
+    else if (k == "RDC_DIRECT_BYTES") m.cfg.direct_min = strcmp(val, "auto") == 0 ? kDirectMinAuto : parse_unit(val);
     else if (k == "RDC_P2P_SLOT_BYTES") m.cfg.p2p_slot_bytes = std::max<size_t>(parse_unit(val) / 4096 * 4096, 4096);
     // other reference keys (RDC_HEARTBEAT_INTERVAL, RDC_RESTART, ...) belong
     // to subsystems outside the device path and are accepted silently
@@ -642,6 +642,8 @@ int RdcCommGetParam(void* comm, const char* key, uint64_t* value) {
         else if (k == "shares_scratch") *value = c->shares_channel() ? 1 : 0;
         else if (k == "host_registered_calls") *value = HostRegisteredCalls();
         else if (k == "direct_check") *value = (uint64_t)c->DirectCheckResult();
+        else if (k.compare(0, 7, "direct_") == 0) *value = c->DirectStat(k);
+        else if (k == "RDC_DIRECT_BYTES") *value = g.direct_min;
         else throw std::invalid_argument("rdc: unknown parameter " + k);
     });
 }
@@ -749,6 +751,16 @@ int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_by
         algo = AutoAlgo(n, bytes, L, oneshot_bytes);
     });
     return rc != 0 ? rc : algo;
+}
+
+int RdcPlanDirectAuto(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_bytes, uint64_t direct_min) {
+    int on = -1;
+    const int rc = guard([&] {
+        if (n < 1 || n > RDC_MAX_RANKS) throw std::invalid_argument("rdc: bad argument");
+        const Layout L = MakeLayout(n, scratch_bytes ? scratch_bytes : CommConfig().scratch_bytes);
+        on = DirectAuto(n, bytes, L, oneshot_bytes, direct_min) ? 1 : 0;
+    });
+    return rc != 0 ? rc : on;
 }
 
 int RdcPlanHbmBytes(int n, size_t count, int dtype, int algo, uint64_t* out5) {

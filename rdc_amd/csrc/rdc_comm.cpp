@@ -326,13 +326,16 @@ Channel::~Channel() {
                 if (peer_flags[p]) (void)hipIpcCloseMemHandle(peer_flags[p]);
                 if (peer_svc_region[p]) (void)hipIpcCloseMemHandle(peer_svc_region[p]);
             }
-        for (auto& m : dmaps) (void)hipIpcCloseMemHandle(m.second);  // registered peers' buffers
+        for (auto& m : dmaps) (void)hipIpcCloseMemHandle(m.second.ptr);  // registered peers' buffers
         dmaps.clear();
         try {
             bs->barrier();  // every importer closed its mapping
         } catch (...) {
         }
     }
+    for (auto& q : dquarantine) (void)hipMemAddressFree(q.first, q.second);
+    dquarantine.clear();
+    if (dlast) (void)hipEventDestroy(dlast);
     if (last_ev) (void)hipEventDestroy(last_ev);
     if (tune_buf) (void)hipFree(tune_buf);
     for (void* p : tune_old) (void)hipFree(p);
@@ -621,16 +624,21 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     {   // more than 16 hardware queues on one GPU are time-sliced by its
         // scheduler (~10 ms slices): a collective spinning on a peer whose
         // queue is not mapped waits a slice (DESIGN.md §4, round 3 session 3)
+        // The advice is rdc_amd.launcher's budget (hw_queues_per_process): the
+        // share of 16 rounded down to a power of two — 3 queues per process
+        // at 5-6 ranks per GPU lost hand-offs in round 5 (profiles/r05/queues/)
         const char* q = getenv("GPU_MAX_HW_QUEUES");
         const int per = q && *q ? atoi(q) : 4;
         static bool warned = false;
-        const int want = std::max(1, 16 / c->share_max_);
-        if (c->rank_ == 0 && !warned && c->share_max_ * per > 16) {
+        int want = 1;
+        while (want * 2 <= std::max(1, 16 / c->share_max_)) want *= 2;
+        const bool pow2 = per > 0 && (per & (per - 1)) == 0;
+        if (c->rank_ == 0 && !warned && c->share_max_ > 1 && (c->share_max_ * per > 16 || !pow2)) {
             warned = true;
             fprintf(stderr,
-                    "rdc: %d ranks share one GPU with GPU_MAX_HW_QUEUES=%d each; the GPU time-slices that many "
-                    "queues and collectives wait ~10 ms per slice. Set GPU_MAX_HW_QUEUES=%d (rdc_amd.launcher "
-                    "does)\n",
+                    "rdc: %d ranks share one GPU with GPU_MAX_HW_QUEUES=%d each; set GPU_MAX_HW_QUEUES=%d "
+                    "(rdc_amd.launcher does): more than 16 queues are time-sliced (~10 ms per slice) and a "
+                    "budget that is not a power of two lost hand-offs at 5-6 ranks per GPU\n",
                     c->share_max_, per, want);
         }
     }
@@ -725,6 +733,23 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     dbg("[rdc %d] %s\n", c->rank_, "peers mapped");
     c->owns_peers_ipc_ = true;
     bs->barrier();
+    // Round 6: the direct schedule's self-check runs once
+    // per channel here, not only before Autotune, so that untuned automatic
+    // calls may take the schedule (DirectEligible).  Collective: share, dreg,
+    // RDC_ALGO and RDC_DIRECT_BYTES are the same on every rank (plan keys).
+    if (!share && ch->dreg && cfg.algo == RDC_ALGO_AUTO && cfg.direct_min != 0) {
+        hipStream_t s = nullptr;
+        hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "self-check stream");
+        try {
+            c->DirectSelfCheck(s);
+        } catch (...) {
+            (void)hipStreamDestroy(s);
+            throw;
+        }
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+        dbg("[rdc %d] %s\n", c->rank_, ch->direct_check == 1 ? "direct self-check passed" : "direct self-check failed");
+    }
     return c.release();
 }
 
@@ -1011,13 +1036,22 @@ void Communicator::Allreduce(void* buf, size_t count, int dtype, int op, hipStre
 // Every check here uses values identical on every rank (the schedule asked
 // for, the byte count, the channel kind, whether the stream is being
 // captured — ranks capture alike), so either all ranks rendezvous or none.
+//
+// An automatic call (algo and RDC_ALGO auto) takes the schedule only on a
+// channel whose self-check passed (DirectSelfCheck, run at channel creation:
+// direct_check is agreed by a MAX allreduce, so it is rank-uniform), and then
+// where Autotune / RDC_TUNE_FILE chose it for the size class, or — untuned —
+// by the rule DirectAuto (RDC_DIRECT_BYTES; rdc_plan.h).  A tune file written
+// on a node where the check passed therefore never turns it on where it did
+// not.  An explicit algo 6 or RDC_ALGO=direct is taken as asked.
 bool Communicator::DirectEligible(int algo, uint64_t bytes, hipStream_t stream) const {
     if (!ch_ || !ch_->dreg || n_ < 2) return false;  // multi-process channels only
     bool want = algo == RDC_ALGO_DIRECT || (algo == RDC_ALGO_AUTO && cfg_.algo == RDC_ALGO_DIRECT);
     if (algo == RDC_ALGO_AUTO && cfg_.algo == RDC_ALGO_AUTO) {
+        if (ch_->direct_check != 1) return false;
         const auto it = tuned_algo_.find(SizeClass(bytes));
         want = it != tuned_algo_.end() ? it->second == RDC_ALGO_DIRECT
-                                       : cfg_.direct_min > 0 && bytes >= cfg_.direct_min;
+                                       : DirectAuto(n_, bytes, layout(), cfg_.oneshot_push_max, cfg_.direct_min);
     }
     if (!want) return false;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1035,6 +1069,16 @@ namespace {
 bool direct_rotate() {
     static const bool on = [] {
         const char* e = getenv("RDC_DIRECT_ROTATE");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
+// RDC_DIRECT_QUARANTINE=0: closed peer mappings' address ranges are not
+// reserved afterwards (A/B knob for the remap fault)
+bool direct_quarantine() {
+    static const bool on = [] {
+        const char* e = getenv("RDC_DIRECT_QUARANTINE");
         return !(e && *e == '0');
     }();
     return on;
@@ -1073,23 +1117,51 @@ bool rendezvous_wait(DirectDesc* slots, int n, uint64_t DirectDesc::*field, uint
 // any buffer cannot be exported (the call then falls back on every rank).
 // own_base[i] = the base of me.alloc[i] in this process.
 //
-// Mapping life cycle (measured round 5, tools/direct_check.py,
-// profiles/r05/direct/): a HIP IPC handle names an allocation by (exporting
-// process, base address), and an importer that still holds a mapping from an
+// Mapping life cycle (round 6; round 5's rule kept every mapping for the
+// channel's life).  A HIP IPC handle names an allocation by (exporting
+// process, base address), and an importer that still holds a mapping of an
 // earlier allocation at the same base gets that old mapping back — stale
-// memory — when it opens the new handle.  Closing the old mapping first fixes
-// the data, but re-mapping into address ranges just unmapped faulted the GPU
-// at n = 3.  So mappings are never closed while the channel lives
-// (RdcCommDirectRelease / channel close), and an allocation whose base address
-// — or any byte of whose range — this rank exported before for ANOTHER
-// allocation is not exported.  The cost: a freed allocation stays alive while
-// peers keep its mapping.
+// memory — when it opens the new handle (round 5, profiles/r05/direct/).  So
+// this rank RETIRES every allocation it exported that is gone (its buffer id
+// at the base changed or the base is no longer allocated): the ones that
+// overlap a buffer of this call always (before that buffer's allocation is
+// exported, possibly at the same base), and up to kRetireScan others per call
+// round-robin.  The retired ids ride in this rank's slot; every peer closes
+// its mapping of them (DirectMapPeers) BEFORE it opens anything in the same
+// rendezvous, so the old mapping is never handed back, and the exporter's
+// freed memory is released once every peer closed.
+namespace {
+constexpr size_t kRetireScan = 16;  // exports checked per call beyond this call's own ranges
+
+// the allocation that now holds `base` in this process, if any
+uint64_t live_buffer_id(uintptr_t base) {
+    unsigned long long id = 0;
+    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)base) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return (uint64_t)id;
+}
+}  // namespace
+
 bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_t* bytes, int nbuf, uint64_t call,
                                 std::vector<char*>* own_base) {
     Channel& ch = *ch_;
     me.nalloc = 0;
+    me.nretired = 0;
     me.nbuf = (uint32_t)nbuf;
     if (ch.direct_off || nbuf < 1 || nbuf > kDirectBufsMax) return false;
+    auto retire = [&](std::map<uintptr_t, Channel::DirectExport>::iterator it) -> bool {
+        if (me.nretired >= (uint32_t)kDirectRetireMax) return false;
+        me.retired[me.nretired++] = it->second.id;
+        if (direct_log())
+            fprintf(stderr, "rdc-direct r%d call %llu: retire id %llu (base %p)\n", rank_, (unsigned long long)call,
+                    (unsigned long long)it->second.id, (void*)it->first);
+        if (ch.dscan == it->first) ch.dscan = it->first + 1;
+        ch.dexports.erase(it);
+        ++ch.dstat_retired;
+        return true;
+    };
     std::unordered_map<uint64_t, uint32_t> alloc_index;  // allocation id -> index in me.alloc
     for (int b = 0; b < nbuf; ++b) {
         char* buf = bufs[b];
@@ -1109,16 +1181,18 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
         if (ai == me.nalloc) {  // this call's first buffer in that allocation: export it
             const uintptr_t bs = (uintptr_t)base;
             const char* why = nullptr;
+            // every earlier export overlapping [bs, bs + size) under another id
+            // belongs to a dead allocation (live ones do not overlap): retire it
+            auto nx = ch.dexports.upper_bound(bs);
+            if (nx != ch.dexports.begin()) --nx;
+            while (!why && nx != ch.dexports.end() && nx->first < bs + size) {
+                auto cur = nx++;
+                if (cur->first + cur->second.size <= bs || cur->second.id == (uint64_t)id) continue;
+                if (!retire(cur)) why = "retire list full";
+            }
             auto it = ch.dexports.find(bs);
-            if (it != ch.dexports.end()) {
-                if (it->second.id != (uint64_t)id) why = "address reused";
-            } else {
-                // an earlier export overlapping [bs, bs + size) is a dead allocation
-                auto nx = ch.dexports.lower_bound(bs);
-                if ((nx != ch.dexports.end() && nx->first < bs + size) ||
-                    (nx != ch.dexports.begin() && std::prev(nx)->first + std::prev(nx)->second.size > bs))
-                    why = "range reused";
-                else if (ch.dexports.size() >= kDirectExportsMax)
+            if (!why && it == ch.dexports.end()) {
+                if (ch.dexports.size() >= kDirectExportsMax)
                     why = "export table full";
                 else {
                     Channel::DirectExport ex;
@@ -1146,15 +1220,70 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
         me.buf[b].off = (uint64_t)(buf - (char*)base);
         me.buf[b].bytes = bytes[b];
     }
+    // round-robin check of the other exports: allocations freed since
+    if (!ch.dexports.empty()) {
+        auto it = ch.dexports.lower_bound(ch.dscan);
+        for (size_t k = 0; k < std::min(kRetireScan, ch.dexports.size()) && me.nretired < (uint32_t)kDirectRetireMax;
+             ++k) {
+            if (it == ch.dexports.end()) it = ch.dexports.begin();
+            auto cur = it++;
+            if (alloc_index.count(cur->second.id)) continue;  // in use by this call
+            if (live_buffer_id(cur->first) != cur->second.id) retire(cur);
+        }
+        ch.dscan = it == ch.dexports.end() ? 0 : it->first;
+    }
     return true;
 }
 
 // Step 2: every rank's allocations as mapped in this process (*amap, indexed
 // q * kDirectAllocsMax + i; this rank's own from own_base), opening the ones
-// not mapped yet; false when one cannot be mapped.
+// not mapped yet; false when one cannot be mapped.  First, the mappings of
+// allocations the peers retired are closed — after this rank's previous
+// direct launch (the last one that may read through them) has completed,
+// and then (RDC_DIRECT_QUARANTINE, on) their address ranges are reserved so
+// that no later mapping lands on a range this process unmapped
+// (tools/ipc_remap_probe.hip).
 bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,
                                   std::vector<char*>* amap) {
     Channel& ch = *ch_;
+    bool waited = false;
+    for (int p = 0; p < n_; ++p) {
+        if (p == rank_) continue;
+        const uint32_t nr = std::min<uint32_t>(slots[p].nretired, (uint32_t)kDirectRetireMax);
+        for (uint32_t k = 0; k < nr; ++k) {
+            auto it = ch.dmaps.find(std::make_pair(p, slots[p].retired[k]));
+            if (it == ch.dmaps.end()) continue;
+            if (!waited && ch.dlast) {
+                const auto t0 = std::chrono::steady_clock::now();
+                hip_check(hipEventSynchronize(ch.dlast), "wait for the previous direct launch");
+                ch.dstat_close_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                              std::chrono::steady_clock::now() - t0)
+                                              .count();
+                waited = true;
+            }
+            const Channel::DirectMap m = it->second;
+            ch.dmaps.erase(it);
+            const hipError_t e = hipIpcCloseMemHandle(m.ptr);
+            (void)hipGetLastError();
+            ++ch.dstat_closed;
+            if (direct_log())
+                fprintf(stderr, "rdc-direct r%d call %llu: close peer %d id %llu at %p (%zu B)%s\n", rank_,
+                        (unsigned long long)call, p, (unsigned long long)slots[p].retired[k], (void*)m.ptr, m.size,
+                        e == hipSuccess ? "" : " FAILED");
+            if (e == hipSuccess && direct_quarantine() && m.size) {
+                void* r = nullptr;
+                if (hipMemAddressReserve(&r, m.size, 0, m.ptr, 0) == hipSuccess && r == m.ptr) {
+                    ch.dquarantine.emplace_back(m.ptr, m.size);
+                    ++ch.dstat_quarantined;
+                } else {
+                    if (r) (void)hipMemAddressFree(r, m.size);
+                    (void)hipGetLastError();
+                }
+            }
+            // device tables naming that allocation can never match a later call
+            // (buffer ids are not reused); they age out of the LRU
+        }
+    }
     amap->assign((size_t)n_ * kDirectAllocsMax, nullptr);
     for (int p = 0; p < n_; ++p)
         for (uint32_t i = 0; i < slots[p].nalloc; ++i) {
@@ -1176,15 +1305,20 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
                 // a pointer this rank already holds for another allocation
                 // would be the stale mapping described above: never use it
                 bool dup = false;
-                for (auto& o : ch.dmaps) dup = dup || o.second == (char*)m;
+                for (auto& o : ch.dmaps) dup = dup || o.second.ptr == (char*)m;
+                Channel::DirectMap dm;
+                dm.ptr = static_cast<char*>(m);
+                hipDeviceptr_t mb = nullptr;
+                if (hipMemGetAddressRange(&mb, &dm.size, (hipDeviceptr_t)m) != hipSuccess || mb != m) dm.size = 0;
+                (void)hipGetLastError();
                 if (direct_log())
-                    fprintf(stderr, "rdc-direct r%d call %llu: open peer %d id %llu -> %p%s\n", rank_,
-                            (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id, m,
+                    fprintf(stderr, "rdc-direct r%d call %llu: open peer %d id %llu -> %p (%zu B)%s\n", rank_,
+                            (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id, m, dm.size,
                             dup ? " (a mapping already held: not used)" : "");
                 if (dup) return false;
-                it = ch.dmaps.emplace(key, static_cast<char*>(m)).first;
+                it = ch.dmaps.emplace(key, dm).first;
             }
-            dst = it->second;
+            dst = it->second.ptr;
         }
     return true;
 }
@@ -1278,6 +1412,11 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     if (!rendezvous_wait(slots, n_, &DirectDesc::stamp1, call, cfg_.timeout_s))
         throw std::runtime_error("rdc: registered-buffer rendezvous timed out (a peer did not join the allreduce)");
     for (int p = 0; p < n_; ++p) usable = usable && slots[p].ok;
+    ++ch.dstat_calls;
+    ch.dstat_export_ns += (uint64_t)(export_us * 1e3);
+    ch.dstat_rdv_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           std::chrono::steady_clock::now() - t0)
+                           .count();
     if (direct_log())
         fprintf(stderr, "rdc-direct r%d call %llu: %d buffers in %u allocations, export %.1f us, total %.1f us, %s\n",
                 rank_, (unsigned long long)call, nbuf, me.nalloc, export_us,
@@ -1333,6 +1472,10 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     ++seq_;
     log_launch(this, seq_, RDC_ALGO_DIRECT, total, grid, tile);
     hip_check(ks.direct(a, grid, stream), "launch direct allreduce");
+    // the last launch that may read through this rank's peer mappings: a
+    // later rendezvous that closes one of them waits for it first
+    if (!ch.dlast) hip_check(hipEventCreateWithFlags(&ch.dlast, hipEventDisableTiming), "direct event");
+    hip_check(hipEventRecord(ch.dlast, stream), "record direct launch");
     trace_ = nullptr;
     return true;
 }
@@ -1392,19 +1535,37 @@ int Communicator::DirectSelfCheck(hipStream_t stream) {
     return ch.direct_check;
 }
 
+uint64_t Communicator::DirectStat(const std::string& k) const {
+    if (!ch_) return 0;
+    const Channel& ch = *ch_;
+    if (k == "direct_calls") return ch.dstat_calls;
+    if (k == "direct_rendezvous_ns") return ch.dstat_rdv_ns;
+    if (k == "direct_export_ns") return ch.dstat_export_ns;
+    if (k == "direct_retired") return ch.dstat_retired;
+    if (k == "direct_closed") return ch.dstat_closed;
+    if (k == "direct_quarantined") return ch.dstat_quarantined;
+    if (k == "direct_close_wait_ns") return ch.dstat_close_wait_ns;
+    if (k == "direct_maps") return ch.dmaps.size();
+    if (k == "direct_exports") return ch.dexports.size();
+    throw std::invalid_argument("rdc: unknown parameter " + k);
+}
+
 // Closes every peer-buffer mapping of the direct schedule and turns the
 // schedule off for the channel (re-mapping into just-unmapped address ranges
 // faulted the GPU in round 5's tests, so nothing is mapped again).  A mapping
 // keeps the peer's allocation alive after the peer frees it: this releases
 // them.  Every rank should call it (a rank that has it off makes every call
 // fall back anyway).
+// direct_check stays as agreed (a release on a subset of ranks
+// must not make the ranks' Autotune candidate lists or self-check collectives
+// differ); direct_off alone makes this rank publish valid = 0 at every later
+// rendezvous, so every rank falls back together.
 void Communicator::DirectUnmapAll() {
     if (!ch_) return;
     if (!ch_->dmaps.empty()) (void)hipDeviceSynchronize();  // no launch still reads through them
-    for (auto& m : ch_->dmaps) (void)hipIpcCloseMemHandle(m.second);
+    for (auto& m : ch_->dmaps) (void)hipIpcCloseMemHandle(m.second.ptr);
     ch_->dmaps.clear();
     ch_->direct_off = true;
-    ch_->direct_check = 2;  // Autotune leaves it out from now on (every rank calls this)
     (void)hipGetLastError();
 }
 

@@ -42,10 +42,12 @@ struct CommConfig {
     // byte): allreduces of at most this many bytes take the reference's tree
     // order instead of the ring's (communicator_collective.cc:6-13)
     size_t ring_mincount = 1;
-    // RDC_DIRECT_BYTES: allreduces of at least this many bytes on multi-process
-    // channels use the registered-buffer schedule (RDC_ALGO_DIRECT) when every
-    // rank's buffer can be mapped (0 = only when asked for or autotuned)
-    size_t direct_min = 0;
+    // RDC_DIRECT_BYTES: which untuned automatic allreduces on multi-process
+    // channels take the registered-buffer schedule (RDC_ALGO_DIRECT) when every
+    // rank's buffer can be mapped and the channel's self-check passed: "auto"
+    // (kDirectMinAuto, the default: rdc_plan.h DirectAuto), 0 = only when
+    // asked for (algo 6, RDC_ALGO=direct) or autotuned, N = from N bytes
+    uint64_t direct_min = kDirectMinAuto;
     // RDC_POISON_SCRATCH=1: consumers overwrite every scratch range they
     // finished reading with 0xFF bytes (debug mode, rdc_device.h block_poison)
     int poison = 0;
@@ -116,13 +118,23 @@ struct Channel {
     // address (kept for the channel's life: see AllreduceDirect)
     std::shared_ptr<char> dreg;
     uint64_t dcalls = 0;
-    std::map<std::pair<int, uint64_t>, char*> dmaps;
+    struct DirectMap {
+        char* ptr = nullptr;
+        size_t size = 0;
+    };
+    std::map<std::pair<int, uint64_t>, DirectMap> dmaps;
     struct DirectExport {
         hipIpcMemHandle_t handle;
         uint64_t id = 0;
         size_t size = 0;
     };
     std::map<uintptr_t, DirectExport> dexports;
+    uintptr_t dscan = 0;              // retirement scan cursor (a base address in dexports)
+    hipEvent_t dlast = nullptr;       // recorded after this rank's latest direct launch
+    std::vector<std::pair<char*, size_t>> dquarantine;  // closed mappings' address ranges, held reserved
+    // host cost of the per-call rendezvous (RdcCommGetParam "direct_*")
+    uint64_t dstat_calls = 0, dstat_rdv_ns = 0, dstat_export_ns = 0, dstat_closed = 0, dstat_retired = 0;
+    uint64_t dstat_close_wait_ns = 0, dstat_quarantined = 0;
     bool direct_off = false;  // RdcCommDirectRelease ran: the direct schedule stays off
     void* tune_buf = nullptr;  // Autotune's buffer, kept (peers map it) until the channel closes
     size_t tune_bytes = 0;
@@ -146,12 +158,15 @@ struct DirectBuf {
     uint64_t off;                       // address - allocation base
     uint64_t bytes;
 };
+constexpr int kDirectRetireMax = 256;  // retired allocations one rank announces per call
 struct DirectDesc {
     uint64_t stamp0;          // rendezvous number whose descriptor this slot holds (release-stored last)
     int32_t valid;            // every buffer in an exportable device allocation
     int32_t ok;               // phase 1: every peer's buffers are mapped here
     uint64_t stamp1;          // rendezvous number of `ok` (release-stored last)
     uint32_t nalloc, nbuf;
+    uint32_t nretired, pad_;
+    uint64_t retired[kDirectRetireMax];  // ids of this rank's exported allocations that are gone: peers close them
     DirectAlloc alloc[kDirectAllocsMax];
     DirectBuf buf[kDirectBufsMax];
 };
@@ -232,6 +247,11 @@ public:
     // Autotune only times the direct schedule on a node where it passed
     int DirectSelfCheck(hipStream_t stream);
     int DirectCheckResult() const { return ch_ ? ch_->direct_check : 0; }
+    // the channel's direct-schedule counters: "direct_calls" (rendezvous),
+    // "direct_rendezvous_ns" / "direct_export_ns" (host time, summed),
+    // "direct_retired" / "direct_closed" / "direct_quarantined" (mapping life
+    // cycle), "direct_close_wait_ns", "direct_maps" / "direct_exports" (held now)
+    uint64_t DirectStat(const std::string& key) const;
 
     // Collective (every rank, same arguments, no collective in flight): time
     // the schedules (ring, mesh, one-shot where it fits) and then the launch

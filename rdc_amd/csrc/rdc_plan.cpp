@@ -156,6 +156,14 @@ int AutoAlgo(int n, uint64_t bytes, const Layout& L, uint64_t push_max) {
     return n == 2 ? RDC_ALGO_RING : RDC_ALGO_MESH;
 }
 
+bool DirectAuto(int n, uint64_t bytes, const Layout& L, uint64_t push_max, uint64_t direct_min) {
+    if (n < 2 || direct_min == 0) return false;
+    if (direct_min != kDirectMinAuto) return bytes >= direct_min;
+    if (bytes < kDirectAutoMinBytes) return false;
+    const int a = AutoAlgo(n, bytes, L, push_max);
+    return a == RDC_ALGO_RING || a == RDC_ALGO_MESH;
+}
+
 Piece PlanOneshot(int n, uint64_t count, size_t esz, const Layout& L, size_t cfg_tile, int max_blocks) {
     int64_t cb[RDC_MAX_RANKS], ce[RDC_MAX_RANKS];
     SplitRanges((int64_t)count, n, cb, ce);

@@ -87,6 +87,19 @@ bool OneshotAuto(int n, uint64_t bytes, const Layout& L, uint64_t push_max);
 // either way; measured 16 MiB 0.028 vs 0.036 ms, 1 GiB 1.71 vs 1.74 ms with 2
 // ranks on one GPU) and the mesh from n = 3 (all n-1 links)
 int AutoAlgo(int n, uint64_t bytes, const Layout& L, uint64_t push_max);
+// Round 6: the registered-buffer schedule (RDC_ALGO_DIRECT) for an untuned
+// RDC_ALGO=auto call on a multi-process channel whose direct self-check
+// passed.  direct_min (RDC_DIRECT_BYTES): kDirectMinAuto (the default) = where
+// AutoAlgo picks a two-hand-off schedule (ring or mesh, i.e. above the
+// one-shot sizes) and the buffer is at least kDirectAutoMinBytes; 0 = never;
+// otherwise from direct_min bytes.  Why there: the direct schedule moves 2 S
+// of HBM per rank where the ring moves 9(n-1)/n S and the pull mesh
+// (5n-2)/n S (ModelHbmBytes), the same link bytes as the mesh, and pays one
+// host rendezvous per call (two shared-memory stamps, measured in
+// profiles/r06/direct_default/), which the one-shot sizes do not amortise.
+constexpr uint64_t kDirectMinAuto = ~(uint64_t)0;
+constexpr uint64_t kDirectAutoMinBytes = (uint64_t)1 << 20;
+bool DirectAuto(int n, uint64_t bytes, const Layout& L, uint64_t push_max, uint64_t direct_min);
 uint64_t OneshotHalfBytes(const Layout& L);
 Piece PlanOneshot(int n, uint64_t count, size_t esz, const Layout& L, size_t cfg_tile, int max_blocks);
 

@@ -155,6 +155,57 @@ def main():
             print("rank %d case %d ok" % (rank, i), flush=True)
             # the channel is unusable now: leave without finalizing collectives
             os._exit(0)
+        if kind == "mem_return":
+            # the direct schedule's mapping life cycle (round 6): a big buffer
+            # goes through the direct schedule, is freed back to HIP, and the
+            # next direct call (a small new buffer) makes every peer close its
+            # mapping of it — the freed memory must come back to the device
+            # (round 5 kept peer mappings, so a freed allocation stayed alive)
+            def stat(k):
+                v = ctypes.c_uint64()
+                check_call(_LIB.RdcCommGetParam(comm.handle, k.encode(), ctypes.byref(v)))
+                return int(v.value)
+            def vram_used():  # device-wide bytes in use (driver sysfs), -1 if unreadable
+                try:
+                    hip = ctypes.CDLL("libamdhip64.so")
+                    b = ctypes.create_string_buffer(64)
+                    hip.hipDeviceGetPCIBusId(b, 63, device)
+                    with open("/sys/bus/pci/devices/%s/mem_info_vram_used" % b.value.decode().lower()) as f:
+                        return int(f.read().split()[0])
+                except Exception:  # noqa: BLE001
+                    return -1
+            big = torch.empty(count, dtype=torch.float32, device="cuda")
+            check_call(_LIB.RdcFill(ctypes.c_void_p(big.data_ptr()), count, 6, c.get("seed", 0x5EED0000), rank, sp))
+            check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(big.data_ptr()), count, 6, 2, 6, sp))
+            comm.check(sp)
+            ll = (ctypes.c_uint64 * 6)()
+            check_call(_LIB.RdcCommLastLaunch(comm.handle, ll))
+            first_algo = int(ll[5])
+            got = big[:4096].cpu().numpy().view(np.uint8).copy()
+            del big
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            free0 = torch.cuda.mem_get_info()[0]
+            used0 = vram_used()
+            closed0 = stat("direct_closed")
+            small = torch.empty(c["small"], dtype=torch.float32, device="cuda")
+            check_call(_LIB.RdcFill(ctypes.c_void_p(small.data_ptr()), c["small"], 6, 0x5EEDB000, rank, sp))
+            check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(small.data_ptr()), c["small"], 6, 2, 6, sp))
+            comm.check(sp)
+            check_call(_LIB.RdcCommLastLaunch(comm.handle, ll))
+            torch.cuda.synchronize()
+            free1 = torch.cuda.mem_get_info()[0]
+            used1 = vram_used()
+            info = {"first_algo": first_algo, "second_algo": int(ll[5]), "free_before": free0, "free_after": free1,
+                    "vram_used_before": used0, "vram_used_after": used1,
+                    "closed": stat("direct_closed") - closed0, "retired": stat("direct_retired"),
+                    "maps": stat("direct_maps"), "quarantined": stat("direct_quarantined")}
+            open(os.path.join(outdir, "case%d_rank%d.json" % (i, rank)), "w").write(json.dumps(info))
+            out = np.concatenate([got, small.cpu().numpy().view(np.uint8)])
+            np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
+            del small
+            print("rank %d case %d ok" % (rank, i), flush=True)
+            continue
         if kind == "bcast_chain":
             # stream-ordered chain without host syncs: refill, broadcast from a
             # rotating root, accumulate — exposes a root overwriting a peer's
@@ -270,6 +321,14 @@ def main():
         if c.get("last_launch"):
             check_call(_LIB.RdcCommLastLaunch(comm.handle, ll))
             open(os.path.join(outdir, "case%d_rank%d.launch" % (i, rank)), "w").write(json.dumps([int(x) for x in ll]))
+        if c.get("direct_stats"):  # the direct schedule's rendezvous / mapping counters after this case
+            st = {}
+            for k in ("direct_check", "direct_calls", "direct_retired", "direct_closed", "direct_maps",
+                      "direct_exports", "direct_quarantined", "direct_rendezvous_ns", "direct_export_ns"):
+                v = ctypes.c_uint64()
+                check_call(_LIB.RdcCommGetParam(comm.handle, k.encode(), ctypes.byref(v)))
+                st[k] = int(v.value)
+            open(os.path.join(outdir, "case%d_rank%d.stats" % (i, rank)), "w").write(json.dumps(st))
         log("rank", rank, "case", i, "done")
         # warm_l2: the result read back by a copy KERNEL (through the L2s), not by a DMA copy
         out = (buf[pad: pad + nbytes].clone() if c.get("warm_l2") else buf[pad: pad + nbytes]).cpu().numpy()

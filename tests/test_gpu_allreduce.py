@@ -1394,31 +1394,104 @@ def test_mp_plan_disagreement_is_refused(key, value):
 @pytest.mark.parametrize("world", [2, 3])
 def test_mp_direct_after_free(world):
     """The direct schedule across freed and re-allocated buffers (each case
-    allocates after torch.cuda.empty_cache, so HIP may hand the same
-    addresses to new allocations, of the same or another size).  A HIP IPC
-    handle names (process, base address): a peer still mapping the freed
-    allocation would get that stale mapping back for the new one, and closing
-    it first faulted the GPU at n = 3 (round 5, profiles/r05/direct/).  So an
-    address exported before for another allocation is not exported again:
-    such calls take the scratch schedules on every rank.  Every result
-    bit-exact against the oracle's ring, whichever path ran; the first call
-    (nothing freed yet) takes the direct schedule."""
+    allocates after torch.cuda.empty_cache, so HIP hands the same or
+    overlapping address ranges to new allocations, of the same or another
+    size — round 5's fault pattern: a 64 MiB mapping over two closed 16 MiB
+    ones).  A HIP IPC handle names (process, base address), so a peer still
+    mapping the freed allocation would get that stale mapping back for the
+    new one: the exporter retires the dead allocation in its rendezvous slot
+    and every peer closes its mapping (after its previous direct launch
+    finished) before opening the new handle, then holds the closed range
+    reserved.  Round 6: EVERY call takes the direct schedule
+    (round 5's rule made these fall back), every result bit-exact against the
+    oracle's ring, and mappings are closed as allocations die."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cases = []
-    for k, (mib, dt) in enumerate(((16, 6), (16, 6), (16, 10), (64, 10), (64, 6), (16, 6), (128, 10), (64, 6))):
+    for k, (mib, dt) in enumerate(((16, 6), (16, 6), (16, 10), (64, 10), (64, 6), (16, 6), (128, 10), (64, 6),
+                                   (16, 6), (16, 6), (256, 6), (16, 10))):
         esz = 4 if dt == 6 else 2
         cases.append({"count": (mib << 20) // esz, "dtype": dt, "op": 2, "algo": 6, "empty_cache": k > 0,
-                      "seed": 0x5EEDE000 + k, "last_launch": True})
+                      "seed": 0x5EEDE000 + k, "last_launch": True, "direct_stats": True})
     tmp = run_mp(world, cases, timeout=300)
     for i, c in enumerate(cases):
         want = expected_for(c, world)
         for r in range(world):
             got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, c, r)
-    ll = [json.load(open(os.path.join(tmp, "case%d_rank0.launch" % i))) for i in range(len(cases))]
-    assert ll[0][5] == 6, ll
-    assert all(x[5] in (6, 1, 2, 5) for x in ll), ll  # direct, or the automatic scratch schedule
+    for r in range(world):
+        ll = [json.load(open(os.path.join(tmp, "case%d_rank%d.launch" % (i, r)))) for i in range(len(cases))]
+        assert all(x[5] == 6 for x in ll), (r, ll)  # the direct schedule on every call
+        st = [json.load(open(os.path.join(tmp, "case%d_rank%d.stats" % (i, r)))) for i in range(len(cases))]
+        # dead allocations are retired and their peer mappings closed as the run goes
+        assert st[-1]["direct_retired"] >= 1 and st[-1]["direct_closed"] >= 1, (r, st[-1])
+        assert st[-1]["direct_maps"] <= 4 * (world - 1), (r, st[-1])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mp_direct_is_the_untuned_default(world):
+    """Round 6: without RdcCommAutotune, an automatic
+    allreduce (algo 0, what rdc::Allreduce / rdc.allreduce issue) of a device
+    buffer above the one-shot sizes takes the direct schedule, because the
+    channel ran its self-check at creation (direct_check 1); smaller buffers
+    keep the one-shot; a coalesced list above the threshold is one direct
+    launch; RDC_DIRECT_BYTES=0 restores the scratch schedules.  Every result
+    bit-exact against the oracle's ring."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    big = (16 << 20) + 5
+    cases = [{"count": big, "dtype": 6, "op": 2, "last_launch": True, "direct_stats": True},
+             {"count": big, "dtype": 10, "op": 2, "last_launch": True, "reps": 2},
+             {"count": 70001, "dtype": 6, "op": 2, "last_launch": True},
+             {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1 << 20] * 8 + [12345],
+              "same_pads": True, "last_launch": True}]
+    for env, want_direct in (({}, True), ({"RDC_DIRECT_BYTES": "0"}, False)):
+        tmp = run_mp(world, cases, timeout=300, env_extra=env)
+        for i, c in enumerate(cases):
+            want = expected_for(c, world)
+            for r in range(world):
+                got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+                assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (env, i, r)
+        ll = [json.load(open(os.path.join(tmp, "case%d_rank0.launch" % i))) for i in range(len(cases))]
+        st = json.load(open(os.path.join(tmp, "case0_rank0.stats")))
+        if want_direct:
+            assert st["direct_check"] == 1, st  # checked at creation, no autotune ran
+            assert ll[0][5] == 6 and ll[1][5] == 6 and ll[3][5] == 6, ll
+            assert ll[2][5] == 3, ll  # 280 KB: the one-shot
+        else:
+            assert st["direct_check"] == 0 and st["direct_calls"] == 0, st  # no self-check, no rendezvous
+            assert all(x[5] != 6 for x in ll), ll
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mp_direct_freed_memory_returned(world):
+    """A 512 MiB buffer through the direct schedule, freed back to HIP: the
+    next direct call makes every peer close its mapping, and the device's
+    free memory grows by at least this rank's 512 MiB (round 5 never closed a
+    peer mapping, so every freed allocation stayed alive in n-1 processes)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    count = (512 << 20) // 4
+    cases = [{"count": count, "dtype": 6, "op": 2, "kind": "mem_return", "small": (4 << 20) + 3,
+              "seed": 0x5EEDA000}]
+    tmp = run_mp(world, cases, timeout=300)
+    second = expected_for({"count": (4 << 20) + 3, "dtype": 6, "op": 2, "seed": 0x5EEDB000}, world)
+    for r in range(world):
+        got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
+        info = json.load(open(os.path.join(tmp, "case0_rank%d.json" % r)))
+        assert info["first_algo"] == 6 and info["second_algo"] == 6, info
+        assert info["closed"] >= world - 1, info
+        # device-wide VRAM in use (the driver's counter; hipMemGetInfo where it is unreadable)
+        if info["vram_used_before"] >= 0 and info["vram_used_after"] >= 0:
+            assert info["vram_used_before"] - info["vram_used_after"] >= (512 << 20) - (64 << 20), info
+        else:
+            assert info["free_after"] - info["free_before"] >= (512 << 20) - (64 << 20), info
+        assert got[4096:].tobytes() == np.frombuffer(second[r].tobytes(), dtype=np.uint8).tobytes(), r
+    # the big buffer's head (its first 4 KiB) against the full-size oracle
+    want_big = expected_for({"count": count, "dtype": 6, "op": 2, "seed": 0x5EEDA000}, world)
+    for r in range(world):
+        got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
+        assert got[:4096].tobytes() == np.frombuffer(want_big[r].tobytes(), dtype=np.uint8).tobytes()[:4096], r
 
 
 @pytest.mark.parametrize("world", [2, 3, 5])
