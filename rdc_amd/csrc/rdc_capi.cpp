@@ -642,6 +642,8 @@ int RdcCommGetParam(void* comm, const char* key, uint64_t* value) {
         else if (k == "shares_scratch") *value = c->shares_channel() ? 1 : 0;
         else if (k == "host_registered_calls") *value = HostRegisteredCalls();
         else if (k == "direct_check") *value = (uint64_t)c->DirectCheckResult();
+        else if (k == "flags_kind") *value = (uint64_t)c->region_kind(2);    // 3 = HSA-uncached (MTYPE UC)
+        else if (k == "scratch_kind") *value = (uint64_t)c->region_kind(0);
         else if (k.compare(0, 7, "direct_") == 0) *value = c->DirectStat(k);
         else if (k == "RDC_DIRECT_BYTES") *value = g.direct_min;
         else throw std::invalid_argument("rdc: unknown parameter " + k);

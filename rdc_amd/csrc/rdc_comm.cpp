@@ -17,6 +17,9 @@
 #include <stdexcept>
 #include <string>
 
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
 #include "rdc_kernels.h"
 #include "rdc_p2p.h"
 #include "rdc_plan.h"
@@ -31,20 +34,117 @@ void hip_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string("rdc: ") + what + ": " + hipGetErrorString(e));
 }
 
+// Region kinds of a channel (Channel::region_kind): 0 hipExtMallocWithFlags(
+// hipDeviceMallocUncached), 1 fine-grained, 2 coarse (hipMalloc), 3 the GPU's
+// coarse HSA pool allocated with HSA_AMD_MEMORY_POOL_UNCACHED_FLAG and shared
+// through HSA IPC (kKindHsaUC).
+//
+// What the L2s make of them (round 6, tools/ipc_mtype_probe.hip, per-request
+// MTYPE counters TCP_TCC_{UC,NC,RW,CC}_READ_REQ, profiles/r06/mtype/): kind 0
+// is NOT uncached on gfx950 — every request is MTYPE CC (cached in the
+// reader XCD's L2, kept coherent by the hardware's invalidations), in the
+// allocating process and in every hipIpcOpenMemHandle importer alike; kinds 1
+// and 2 are RW; kind 3 is UC in both (every access goes to memory).  With CC,
+// every device read kind — plain, sc1, nt, atomic, after a system acquire —
+// of a line is served by that XCD's L2, so a line whose invalidation was lost
+// stays stale for all of them while memory (and the host) hold the new value:
+// the record of round 5's lost 5 x 3 hand-off.  The flag words
+// of multi-process channels are therefore kind 3 (RDC_FLAGS_MEM=cc: kind 0).
+constexpr int kKindHsaUC = 3;
+
+// RDC_ALLOC: the data regions' kind ("fine", "coarse", "uc"; default 0)
 int env_alloc_kind() {
     const char* v = getenv("RDC_ALLOC");
     if (!v) return 0;
     if (!strcmp(v, "fine")) return 1;
     if (!strcmp(v, "coarse")) return 2;
+    if (!strcmp(v, "uc")) return kKindHsaUC;
     return 0;
 }
 
-// Cross-GPU scratch: uncached (MTYPE UC) so that remote stores landing in
-// this HBM are never shadowed by a stale line in any XCD's L2, and remote
-// readers never cache it either.  Falls back to fine-grained, then coarse.
-void* alloc_shared(size_t bytes, int* kind) {
+// RDC_FLAGS_MEM: the flag words' kind on multi-process channels ("uc", the
+// default, or "cc" = kind 0 as in rounds 1-5)
+int env_flags_kind() {
+    const char* v = getenv("RDC_FLAGS_MEM");
+    return v && !strcmp(v, "cc") ? 0 : kKindHsaUC;
+}
+
+// the HSA agent of HIP device `device` (matched by PCI location) and its
+// coarse-grained global pool; cached per device
+struct HsaDev {
+    bool ok = false;
+    hsa_agent_t agent{};
+    hsa_amd_memory_pool_t pool{};
+    uint32_t want_bdf = 0, want_domain = 0;
+    bool have_agent = false;
+};
+hsa_status_t hsa_pick_agent(hsa_agent_t a, void* d) {
+    HsaDev* h = static_cast<HsaDev*>(d);
+    hsa_device_type_t t;
+    if (h->have_agent || hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS ||
+        t != HSA_DEVICE_TYPE_GPU)
+        return HSA_STATUS_SUCCESS;
+    uint32_t bdf = 0, dom = 0;
+    hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+    hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+    if ((bdf >> 3) == (h->want_bdf >> 3) && dom == h->want_domain) {
+        h->agent = a;
+        h->have_agent = true;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+hsa_status_t hsa_pick_coarse(hsa_amd_memory_pool_t pool, void* d) {
+    HsaDev* h = static_cast<HsaDev*>(d);
+    hsa_amd_segment_t seg;
+    uint32_t flags = 0;
+    if (h->ok || hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS)
+        return HSA_STATUS_SUCCESS;
+    hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+    if (seg == HSA_AMD_SEGMENT_GLOBAL && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED)) {
+        h->pool = pool;
+        h->ok = true;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+const HsaDev& hsa_dev(int device) {
+    static std::mutex mu;
+    static std::map<int, HsaDev> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(device);
+    if (it != cache.end()) return it->second;
+    HsaDev h;
+    int bus = 0, dev = 0, dom = 0;
+    if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) == hipSuccess &&
+        hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) == hipSuccess &&
+        hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) == hipSuccess &&
+        hsa_init() == HSA_STATUS_SUCCESS) {  // reference-counted; HIP holds it already (never shut down here)
+        h.want_bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
+        h.want_domain = (uint32_t)dom;
+        if (hsa_iterate_agents(hsa_pick_agent, &h) == HSA_STATUS_SUCCESS && h.have_agent)
+            hsa_amd_agent_iterate_memory_pools(h.agent, hsa_pick_coarse, &h);
+    }
+    (void)hipGetLastError();
+    return cache.emplace(device, h).first->second;
+}
+
+// One region of a channel: `want` = a kind from the list above; kind 3 falls
+// back to 0 where the HSA pool refuses (and kinds 0 / 1 fall back as before:
+// fine-grained, then coarse).  Kind 3 memory is zeroed here.
+void* alloc_shared(size_t bytes, int* kind, int device, int want) {
     void* p = nullptr;
-    int want = env_alloc_kind();
+    if (want == kKindHsaUC) {
+        const HsaDev& h = hsa_dev(device);
+        if (h.ok && hsa_amd_memory_pool_allocate(h.pool, bytes, HSA_AMD_MEMORY_POOL_UNCACHED_FLAG, &p) ==
+                        HSA_STATUS_SUCCESS) {
+            if (hsa_amd_memory_fill(p, 0, bytes / 4) == HSA_STATUS_SUCCESS) {
+                *kind = kKindHsaUC;
+                return p;
+            }
+            hsa_amd_memory_pool_free(p);
+            p = nullptr;
+        }
+        want = 0;
+    }
     if (want <= 0 && hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess) {
         *kind = 0;
         return p;
@@ -58,6 +158,47 @@ void* alloc_shared(size_t bytes, int* kind) {
     hip_check(hipMalloc(&p, bytes), "hipMalloc scratch");
     *kind = 2;
     return p;
+}
+void free_shared(void* p, int kind) {
+    if (!p) return;
+    if (kind == kKindHsaUC) hsa_amd_memory_pool_free(p);
+    else (void)hipFree(p);
+}
+
+// one region's IPC handle (HIP's for kinds 0-2, HSA's for kind 3)
+struct RegionHandle {
+    int32_t kind;
+    int32_t pad_;
+    uint64_t bytes;
+    hipIpcMemHandle_t hip;
+    hsa_amd_ipc_memory_t hsa;
+};
+void export_region(void* p, size_t bytes, int kind, RegionHandle* h, const char* what) {
+    memset(h, 0, sizeof(*h));
+    h->kind = kind;
+    h->bytes = bytes;
+    if (kind == kKindHsaUC) {
+        if (hsa_amd_ipc_memory_create(p, bytes, &h->hsa) != HSA_STATUS_SUCCESS)
+            throw std::runtime_error(std::string("rdc: hsa_amd_ipc_memory_create(") + what + ") failed");
+    } else {
+        hip_check(hipIpcGetMemHandle(&h->hip, p), what);
+    }
+}
+void* import_region(const RegionHandle& h, int device, const char* what) {
+    void* p = nullptr;
+    if (h.kind == kKindHsaUC) {
+        const HsaDev& d = hsa_dev(device);
+        if (!d.have_agent || hsa_amd_ipc_memory_attach(&h.hsa, h.bytes, 1, &d.agent, &p) != HSA_STATUS_SUCCESS || !p)
+            throw std::runtime_error(std::string("rdc: hsa_amd_ipc_memory_attach(") + what + ") failed");
+        return p;
+    }
+    hip_check(hipIpcOpenMemHandle(&p, h.hip, hipIpcMemLazyEnablePeerAccess), what);
+    return p;
+}
+void close_region(void* p, int kind) {
+    if (!p) return;
+    if (kind == kKindHsaUC) hsa_amd_ipc_memory_detach(p);
+    else (void)hipIpcCloseMemHandle(p);
 }
 
 void dbg(const char* fmt, int rank, const char* what) {
@@ -86,11 +227,8 @@ struct PeerInfo {
     char pci[32];  // physical GPU (ranks may share one: tests, emulation)
 };
 
-struct Handles {  // round 2 of Create: IPC handles (scratch ones only for a new channel)
-    hipIpcMemHandle_t scratch;
-    hipIpcMemHandle_t ag;
-    hipIpcMemHandle_t flags;
-    hipIpcMemHandle_t svc;
+struct Handles {  // round 2 of Create: IPC handles (the channel's regions only for a new channel)
+    RegionHandle region[4];  // scratch, ag, flags, service slots
     hipIpcMemHandle_t p2p;
 };
 
@@ -321,10 +459,10 @@ Channel::~Channel() {
         }
         for (int p = 0; p < n; ++p)
             if (p != rank) {
-                if (peer_scratch[p]) (void)hipIpcCloseMemHandle(peer_scratch[p]);
-                if (peer_ag[p]) (void)hipIpcCloseMemHandle(peer_ag[p]);
-                if (peer_flags[p]) (void)hipIpcCloseMemHandle(peer_flags[p]);
-                if (peer_svc_region[p]) (void)hipIpcCloseMemHandle(peer_svc_region[p]);
+                close_region(peer_scratch[p], peer_kind[0][p]);
+                close_region(peer_ag[p], peer_kind[1][p]);
+                close_region(peer_flags[p], peer_kind[2][p]);
+                close_region(peer_svc_region[p], peer_kind[3][p]);
             }
         for (auto& m : dmaps) (void)hipIpcCloseMemHandle(m.second.ptr);  // registered peers' buffers
         dmaps.clear();
@@ -333,17 +471,16 @@ Channel::~Channel() {
         } catch (...) {
         }
     }
-    for (auto& q : dquarantine) (void)hipMemAddressFree(q.first, q.second);
-    dquarantine.clear();
     if (dlast) (void)hipEventDestroy(dlast);
     if (last_ev) (void)hipEventDestroy(last_ev);
     if (tune_buf) (void)hipFree(tune_buf);
     for (void* p : tune_old) (void)hipFree(p);
-    if (scratch) (void)hipFree(scratch);
-    if (scratch_ag) (void)hipFree(scratch_ag);
-    if (flags) (void)hipFree(flags);
-    if (svc_region) (void)hipFree(svc_region);
+    free_shared(scratch, region_kind[0]);
+    free_shared(scratch_ag, region_kind[1]);
+    free_shared(flags, region_kind[2]);
+    free_shared(svc_region, region_kind[3]);
     if (err) (void)hipFree(err);
+    if (tlog) (void)hipFree(tlog);
     if (err_host) (void)hipHostFree(err_host);
 }
 
@@ -396,14 +533,27 @@ void Communicator::AllocChannel() {
     ch->bs = bs_;
     ch->L = MakeLayout(n_, cfg_.scratch_bytes);
     int k1 = 0, k2 = 0, k3 = 0;
-    ch->scratch = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k1));
-    ch->scratch_ag = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k3));
-    ch->flags = static_cast<uint64_t*>(alloc_shared(ch->L.flag_bytes, &k2));
+    // HSA-uncached regions (kind 3) only where peers import them through HSA
+    // IPC: multi-process channels.  Single-process groups keep HIP memory.
+    const int data_want = bs_ ? env_alloc_kind() : std::min(env_alloc_kind(), 2);
+    const int flags_want = bs_ ? std::max(env_flags_kind(), data_want) : data_want;
+    ch->scratch = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k1, device_, data_want));
+    ch->scratch_ag = static_cast<char*>(alloc_shared(ch->L.region_bytes, &k3, device_, data_want));
+    ch->flags = static_cast<uint64_t*>(alloc_shared(ch->L.flag_bytes, &k2, device_, flags_want));
     int k5 = 0;  // service LL slots [2][n] x RDC_SVC_SLOT_BYTES; zero: no sequence number matches
     const size_t svc_bytes = (size_t)2 * n_ * RDC_SVC_SLOT_BYTES;
-    ch->svc_region = static_cast<char*>(alloc_shared(svc_bytes, &k5));
-    hip_check(hipMemset(ch->svc_region, 0, svc_bytes), "memset service slots");
-    ch->alloc_kind = std::max(std::max(std::max(k1, k2), k3), k5);
+    ch->svc_region = static_cast<char*>(alloc_shared(svc_bytes, &k5, device_, flags_want));
+    if (k5 != kKindHsaUC) hip_check(hipMemset(ch->svc_region, 0, svc_bytes), "memset service slots");
+    ch->region_kind[0] = k1;
+    ch->region_kind[1] = k3;
+    ch->region_kind[2] = k2;
+    ch->region_kind[3] = k5;
+    ch->region_bytes[0] = ch->region_bytes[1] = ch->L.region_bytes;
+    ch->region_bytes[2] = ch->L.flag_bytes;
+    ch->region_bytes[3] = svc_bytes;
+    // 0 = the uncached class for the fences' choice (rdc_device.h): CC and UC alike
+    auto cls = [](int k) { return k == kKindHsaUC ? 0 : k; };
+    ch->alloc_kind = std::max(std::max(std::max(cls(k1), cls(k2)), cls(k3)), cls(k5));
     // [0] error word, [16] block arrival counter, [32] completed-launch counter, [48] last kind.
     // [64..] the first timed-out wait (rdc_device.h block_wait: seq, flag value,
     // flag address).  Plain device memory, read and written with agent-scope
@@ -418,8 +568,12 @@ void Communicator::AllocChannel() {
         (void)hipGetLastError();
         hip_check(hipMalloc(&ch->err, 512), "hipMalloc err");
     }
-    hip_check(hipMemset(ch->flags, 0, ch->L.flag_bytes), "memset flags");
+    if (k2 != kKindHsaUC) hip_check(hipMemset(ch->flags, 0, ch->L.flag_bytes), "memset flags");
     hip_check(hipMemset(ch->err, 0, 512), "memset err");
+    if (getenv("RDC_LAUNCH_TIMES") && atoi(getenv("RDC_LAUNCH_TIMES")) != 0) {
+        hip_check(hipMalloc(reinterpret_cast<void**>(&ch->tlog), 64 * 4 * sizeof(uint64_t)), "launch log");
+        hip_check(hipMemset(ch->tlog, 0, 64 * 4 * sizeof(uint64_t)), "launch log");
+    }
     hip_check(hipHostMalloc(reinterpret_cast<void**>(&ch->err_host), 64, hipHostMallocCoherent), "hipHostMalloc err");
     memset(ch->err_host, 0, 64);
     hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ch->err_host_dev), ch->err_host, 0),
@@ -439,7 +593,8 @@ void Communicator::AllocChannel() {
 
 void Communicator::AllocP2P() {
     int k4 = 0;
-    p2p_ = static_cast<char*>(alloc_shared((size_t)n_ * kP2PSlots * cfg_.p2p_slot_bytes, &k4));
+    p2p_ = static_cast<char*>(alloc_shared((size_t)n_ * kP2PSlots * cfg_.p2p_slot_bytes, &k4, device_,
+                                           std::min(env_alloc_kind(), 2)));  // HIP IPC
     alloc_kind_ = std::max(alloc_kind_, k4);
     peer_p2p_[rank_] = p2p_;
 }
@@ -687,10 +842,11 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     Handles h;
     memset(&h, 0, sizeof(h));
     if (!share) {
-        hip_check(hipIpcGetMemHandle(&h.scratch, c->scratch_), "hipIpcGetMemHandle(scratch)");
-        hip_check(hipIpcGetMemHandle(&h.ag, c->scratch_ag_), "hipIpcGetMemHandle(ag)");
-        hip_check(hipIpcGetMemHandle(&h.flags, c->flags_), "hipIpcGetMemHandle(flags)");
-        hip_check(hipIpcGetMemHandle(&h.svc, c->ch_->svc_region), "hipIpcGetMemHandle(service)");
+        Channel* mc = c->ch_.get();
+        void* const own[4] = {mc->scratch, mc->scratch_ag, mc->flags, mc->svc_region};
+        const char* what[4] = {"IPC handle (scratch)", "IPC handle (ag)", "IPC handle (flags)",
+                               "IPC handle (service)"};
+        for (int r = 0; r < 4; ++r) export_region(own[r], mc->region_bytes[r], mc->region_kind[r], &h.region[r], what[r]);
     }
     hip_check(hipIpcGetMemHandle(&h.p2p, c->p2p_), "hipIpcGetMemHandle(p2p)");
     std::vector<Handles> hs((size_t)c->n_);
@@ -700,23 +856,13 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     for (int p = 0; p < c->n_; ++p) {
         if (p == c->rank_) continue;
         if (!share) {
-            void* ps = nullptr;
-            void* pa = nullptr;
-            void* pf = nullptr;
-            hip_check(hipIpcOpenMemHandle(&ps, hs[(size_t)p].scratch, hipIpcMemLazyEnablePeerAccess),
-                      "hipIpcOpenMemHandle(scratch)");
-            ch->peer_scratch[p] = static_cast<char*>(ps);
-            hip_check(hipIpcOpenMemHandle(&pa, hs[(size_t)p].ag, hipIpcMemLazyEnablePeerAccess),
-                      "hipIpcOpenMemHandle(ag)");
-            ch->peer_ag[p] = static_cast<char*>(pa);
-            hip_check(hipIpcOpenMemHandle(&pf, hs[(size_t)p].flags, hipIpcMemLazyEnablePeerAccess),
-                      "hipIpcOpenMemHandle(flags)");
-            ch->peer_flags[p] = static_cast<uint64_t*>(pf);
-            void* sv = nullptr;
-            hip_check(hipIpcOpenMemHandle(&sv, hs[(size_t)p].svc, hipIpcMemLazyEnablePeerAccess),
-                      "hipIpcOpenMemHandle(service)");
-            ch->peer_svc_region[p] = static_cast<char*>(sv);
+            const RegionHandle* rh = hs[(size_t)p].region;
+            for (int r = 0; r < 4; ++r) ch->peer_kind[r][p] = (int8_t)rh[r].kind;
             ch->ipc = true;
+            ch->peer_scratch[p] = static_cast<char*>(import_region(rh[0], device, "import (scratch)"));
+            ch->peer_ag[p] = static_cast<char*>(import_region(rh[1], device, "import (ag)"));
+            ch->peer_flags[p] = static_cast<uint64_t*>(import_region(rh[2], device, "import (flags)"));
+            ch->peer_svc_region[p] = static_cast<char*>(import_region(rh[3], device, "import (service)"));
         }
         void* pp = nullptr;
         hip_check(hipIpcOpenMemHandle(&pp, hs[(size_t)p].p2p, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(p2p)");
@@ -947,6 +1093,7 @@ void Communicator::FillArgsCommon(CollArgs* a) const {
     a->verify = verify ? err_ + 84 : nullptr;
     static const bool poll_rmw = getenv("RDC_POLL_RMW") && atoi(getenv("RDC_POLL_RMW")) != 0;
     a->poll_rmw = poll_rmw ? 1 : 0;
+    a->tlog = ch_ ? ch_->tlog : nullptr;
 }
 
 Layout Communicator::layout() const {
@@ -1074,14 +1221,24 @@ bool direct_rotate() {
     return on;
 }
 
-// RDC_DIRECT_QUARANTINE=0: closed peer mappings' address ranges are not
-// reserved afterwards (A/B knob for the remap fault)
-bool direct_quarantine() {
+// RDC_DIRECT_OVERLAP=1: use a new peer mapping even where it lands partly
+// over address ranges this process unmapped before (A/B knob for the remap
+// fault; off: such calls take the scratch schedules)
+bool direct_overlap_ok() {
     static const bool on = [] {
-        const char* e = getenv("RDC_DIRECT_QUARANTINE");
-        return !(e && *e == '0');
+        const char* e = getenv("RDC_DIRECT_OVERLAP");
+        return e && *e == '1';
     }();
     return on;
+}
+
+// [b, b + n) lies partly over a range of `closed` (an exact match of base and
+// size — a new allocation at an old one's place, which never faulted — is not
+// an overlap)
+bool partly_over(const std::vector<std::pair<uintptr_t, size_t>>& closed, uintptr_t b, size_t n) {
+    for (const auto& c : closed)
+        if (b < c.first + c.second && c.first < b + n && !(c.first == b && c.second == n)) return true;
+    return false;
 }
 
 constexpr size_t kDirectExportsMax = 4096;  // allocations one rank exports over a channel's life
@@ -1154,6 +1311,7 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
     auto retire = [&](std::map<uintptr_t, Channel::DirectExport>::iterator it) -> bool {
         if (me.nretired >= (uint32_t)kDirectRetireMax) return false;
         me.retired[me.nretired++] = it->second.id;
+        ch.dclosed.emplace_back(it->first, it->second.size);
         if (direct_log())
             fprintf(stderr, "rdc-direct r%d call %llu: retire id %llu (base %p)\n", rank_, (unsigned long long)call,
                     (unsigned long long)it->second.id, (void*)it->first);
@@ -1239,10 +1397,14 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
 // q * kDirectAllocsMax + i; this rank's own from own_base), opening the ones
 // not mapped yet; false when one cannot be mapped.  First, the mappings of
 // allocations the peers retired are closed — after this rank's previous
-// direct launch (the last one that may read through them) has completed,
-// and then (RDC_DIRECT_QUARANTINE, on) their address ranges are reserved so
-// that no later mapping lands on a range this process unmapped
-// (tools/ipc_remap_probe.hip).
+// direct launch (the last one that may read through them) has completed
+// (hipIpcCloseMemHandle also waits for the device: 250 ms for a kernel
+// spinning 250 ms, tools/ipc_remap_probe.hip "inflight").  A new mapping that
+// lands partly over a range this process unmapped or retired is closed again
+// unused and the call falls back on every rank (the peer allocation stays
+// refused): the first launch through such a mapping faulted the GPU in round
+// 5 and, with those ranges held by hipMemAddressReserve, again in round 6
+// (profiles/r06/remap/).
 bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,
                                   std::vector<char*>* amap) {
     Channel& ch = *ch_;
@@ -1266,23 +1428,15 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
             const hipError_t e = hipIpcCloseMemHandle(m.ptr);
             (void)hipGetLastError();
             ++ch.dstat_closed;
+            if (m.size) ch.dclosed.emplace_back((uintptr_t)m.ptr, m.size);
             if (direct_log())
                 fprintf(stderr, "rdc-direct r%d call %llu: close peer %d id %llu at %p (%zu B)%s\n", rank_,
                         (unsigned long long)call, p, (unsigned long long)slots[p].retired[k], (void*)m.ptr, m.size,
                         e == hipSuccess ? "" : " FAILED");
-            if (e == hipSuccess && direct_quarantine() && m.size) {
-                void* r = nullptr;
-                if (hipMemAddressReserve(&r, m.size, 0, m.ptr, 0) == hipSuccess && r == m.ptr) {
-                    ch.dquarantine.emplace_back(m.ptr, m.size);
-                    ++ch.dstat_quarantined;
-                } else {
-                    if (r) (void)hipMemAddressFree(r, m.size);
-                    (void)hipGetLastError();
-                }
-            }
             // device tables naming that allocation can never match a later call
             // (buffer ids are not reused); they age out of the LRU
         }
+        for (uint32_t k = 0; k < nr; ++k) ch.drefused.erase(std::make_pair(p, slots[p].retired[k]));
     }
     amap->assign((size_t)n_ * kDirectAllocsMax, nullptr);
     for (int p = 0; p < n_; ++p)
@@ -1296,6 +1450,7 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
             auto it = ch.dmaps.find(key);
             if (it == ch.dmaps.end()) {
                 if (ch.dmaps.size() >= kDirectMapsMax) return false;  // full: no new mappings
+                if (ch.drefused.count(key)) return false;              // its mapping landed over unmapped ranges
                 void* m = nullptr;
                 if (hipIpcOpenMemHandle(&m, slots[p].alloc[i].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
                     !m) {
@@ -1311,11 +1466,21 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
                 hipDeviceptr_t mb = nullptr;
                 if (hipMemGetAddressRange(&mb, &dm.size, (hipDeviceptr_t)m) != hipSuccess || mb != m) dm.size = 0;
                 (void)hipGetLastError();
+                const bool over = !dup && !direct_overlap_ok() &&
+                                  partly_over(ch.dclosed, (uintptr_t)m, dm.size ? dm.size : 1);
                 if (direct_log())
                     fprintf(stderr, "rdc-direct r%d call %llu: open peer %d id %llu -> %p (%zu B)%s\n", rank_,
                             (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id, m, dm.size,
-                            dup ? " (a mapping already held: not used)" : "");
+                            dup ? " (a mapping already held: not used)"
+                                : over ? " (lands partly over unmapped ranges: closed unused, refused)" : "");
                 if (dup) return false;
+                if (over) {  // never touched by a kernel: close it again and fall back
+                    (void)hipIpcCloseMemHandle(m);
+                    (void)hipGetLastError();
+                    ch.drefused.insert(key);
+                    ++ch.dstat_refused;
+                    return false;
+                }
                 it = ch.dmaps.emplace(key, dm).first;
             }
             dst = it->second.ptr;
@@ -1543,7 +1708,7 @@ uint64_t Communicator::DirectStat(const std::string& k) const {
     if (k == "direct_export_ns") return ch.dstat_export_ns;
     if (k == "direct_retired") return ch.dstat_retired;
     if (k == "direct_closed") return ch.dstat_closed;
-    if (k == "direct_quarantined") return ch.dstat_quarantined;
+    if (k == "direct_refused") return ch.dstat_refused;
     if (k == "direct_close_wait_ns") return ch.dstat_close_wait_ns;
     if (k == "direct_maps") return ch.dmaps.size();
     if (k == "direct_exports") return ch.dexports.size();
@@ -2415,6 +2580,28 @@ void Communicator::RaiseIfError(uint32_t e) const {
             }
         } else {
             (void)hipGetLastError();
+        }
+        waited += "; flags kind " + std::to_string(region_kind(2)) + " (3 = HSA-uncached, MTYPE UC)";
+        if (ch_ && ch_->tlog) {
+            // RDC_LAUNCH_TIMES: this rank's last launches as {launch, block 0
+            // start, latest block start, end} in ms of the GPU's wall clock
+            // (100 MHz, one clock for every process on the GPU)
+            uint64_t lg[64 * 4];
+            if (hipMemcpy(lg, ch_->tlog, sizeof(lg), hipMemcpyDeviceToHost) == hipSuccess) {
+                uint64_t top = 0;
+                for (int i = 0; i < 64; ++i) top = std::max(top, lg[i * 4]);
+                waited += "; launch log (launch: block0 start / last block start / end, ms):";
+                for (uint64_t k = top > 5 ? top - 5 : 1; k <= top; ++k) {
+                    const uint64_t* e = lg + (k & 63) * 4;
+                    if (e[0] != k) continue;
+                    char b[160];
+                    snprintf(b, sizeof(b), " %llu: %.3f / %.3f / %s", (unsigned long long)k, (double)e[1] / 1e5,
+                             (double)e[2] / 1e5, e[3] >= e[1] && e[3] ? std::to_string((double)e[3] / 1e5).c_str() : "-");
+                    waited += b;
+                }
+            } else {
+                (void)hipGetLastError();
+            }
         }
         if (getenv("RDC_FLAG_DUMP") && atoi(getenv("RDC_FLAG_DUMP")) != 0) {
             // debug: the reduce-scatter rows as this rank sees them, in its own

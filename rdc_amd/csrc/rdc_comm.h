@@ -15,6 +15,7 @@
 
 #include <map>
 #include <mutex>
+#include <set>
 #include <memory>
 #include <string>
 #include <vector>
@@ -84,6 +85,12 @@ struct Channel {
     bool ipc = false;          // peers' regions opened through IPC
     Layout L;
     int alloc_kind = 0;
+    // kind of each region (scratch, ag, flags, service slots; rdc_comm.cpp
+    // "Region kinds": 0 hipDeviceMallocUncached = MTYPE CC, 3 HSA-uncached =
+    // MTYPE UC, ...), their sizes, and the kinds of the peers' regions mapped here
+    int region_kind[4] = {};
+    size_t region_bytes[4] = {};
+    int8_t peer_kind[4][RDC_MAX_RANKS] = {};
     char* scratch = nullptr;
     char* scratch_ag = nullptr;
     uint64_t* flags = nullptr;
@@ -131,16 +138,23 @@ struct Channel {
     std::map<uintptr_t, DirectExport> dexports;
     uintptr_t dscan = 0;              // retirement scan cursor (a base address in dexports)
     hipEvent_t dlast = nullptr;       // recorded after this rank's latest direct launch
-    std::vector<std::pair<char*, size_t>> dquarantine;  // closed mappings' address ranges, held reserved
+    // address ranges this process unmapped (closed peer mappings) or whose
+    // allocation it retired (own exports): a new peer mapping that lands
+    // partly over one is refused (DirectMapPeers; round 5 and round 6 faulted
+    // at the first launch through such a mapping), and the peer allocation
+    // it maps stays refused
+    std::vector<std::pair<uintptr_t, size_t>> dclosed;
+    std::set<std::pair<int, uint64_t>> drefused;
     // host cost of the per-call rendezvous (RdcCommGetParam "direct_*")
     uint64_t dstat_calls = 0, dstat_rdv_ns = 0, dstat_export_ns = 0, dstat_closed = 0, dstat_retired = 0;
-    uint64_t dstat_close_wait_ns = 0, dstat_quarantined = 0;
+    uint64_t dstat_close_wait_ns = 0, dstat_refused = 0;
     bool direct_off = false;  // RdcCommDirectRelease ran: the direct schedule stays off
     void* tune_buf = nullptr;  // Autotune's buffer, kept (peers map it) until the channel closes
     size_t tune_bytes = 0;
     std::vector<void*> tune_old;  // outgrown tune buffers: never freed before the channel closes (a
                                   // freed address handed out again could not be exported)
     int direct_check = 0;         // DirectSelfCheck: 0 not run, 1 passed, 2 failed
+    uint64_t* tlog = nullptr;     // RDC_LAUNCH_TIMES=1: 64 x {seq, block 0 start, latest block start, end} ticks
 };
 
 // One rank's slot of the registered-buffer rendezvous (shared host memory):
@@ -249,7 +263,7 @@ public:
     int DirectCheckResult() const { return ch_ ? ch_->direct_check : 0; }
     // the channel's direct-schedule counters: "direct_calls" (rendezvous),
     // "direct_rendezvous_ns" / "direct_export_ns" (host time, summed),
-    // "direct_retired" / "direct_closed" / "direct_quarantined" (mapping life
+    // "direct_retired" / "direct_closed" / "direct_refused" (mapping life
     // cycle), "direct_close_wait_ns", "direct_maps" / "direct_exports" (held now)
     uint64_t DirectStat(const std::string& key) const;
 
@@ -309,6 +323,8 @@ public:
     int device() const { return device_; }
     const std::string& name() const { return name_; }
     int alloc_kind() const { return alloc_kind_; }  // 0 uncached, 1 fine-grained, 2 coarse
+    // the kind of the channel's region r (0 scratch, 1 ag, 2 flags, 3 service slots)
+    int region_kind(int r) const { return ch_ && r >= 0 && r < 4 ? ch_->region_kind[r] : -1; }
     size_t slot_bytes() const { return slot_bytes_; }
     uint32_t seq() const { return seq_; }
     bool shares_channel() const;  // another communicator uses this one's scratch

@@ -140,6 +140,8 @@ struct CollArgs {
     int poll_rmw;                        // RDC_POLL_RMW (debug): hand-off polls as atomic adds of 0
     int poison;                          // RDC_POISON_SCRATCH: consumers overwrite scratch ranges they
                                          //   finished reading with 0xFF (rdc_device.h block_poison)
+    uint64_t* tlog;                      // RDC_LAUNCH_TIMES (debug): per launch {seq, block 0 start, latest block
+                                         //   start, last block end} (wall_clock64) in a ring of 64 entries
 };
 
 // ------------------------------------------------ small-allreduce service --

@@ -65,6 +65,15 @@ __device__ __forceinline__ bool launch_begin(const CollArgs& a, uint64_t* seq) {
         const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_done = done;
         s_failed = e != 0;
+        if (a.tlog) {  // RDC_LAUNCH_TIMES: when this launch's blocks started (ticks only grow: max needs no reset)
+            unsigned long long* ent = reinterpret_cast<unsigned long long*>(a.tlog + ((done + 1ull) & 63ull) * 4);
+            const unsigned long long t = wall_clock64();
+            if (blockIdx.x == 0) {
+                __hip_atomic_store(ent, (unsigned long long)(done + 1ull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(ent + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __hip_atomic_fetch_max(ent + 2, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (a.seq_check) {
             // RDC_SEQ_CHECK: every block of one launch must read the same
             // launch number.  The first block to start claims the launch's
@@ -1247,6 +1256,9 @@ __device__ __forceinline__ void launch_done(const CollArgs& a, uint64_t seq) {
                 }
             }
             __hip_atomic_store(a.launch_kind, (uint32_t)a.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (a.tlog)
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tlog + (seq_counter(seq) & 63ull) * 4 + 3),
+                                   (unsigned long long)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.launch_ctr, seq_counter(seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the host reads the (sticky) error word here after a stream sync: no
             // copy needed.  The mirror starts at 0 and only ever changes to an

@@ -181,7 +181,7 @@ def main():
             ll = (ctypes.c_uint64 * 6)()
             check_call(_LIB.RdcCommLastLaunch(comm.handle, ll))
             first_algo = int(ll[5])
-            got = big[:4096].cpu().numpy().view(np.uint8).copy()
+            got = big[:1024].cpu().numpy().view(np.uint8).copy()  # the first 4 KiB
             del big
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
@@ -199,7 +199,7 @@ def main():
             info = {"first_algo": first_algo, "second_algo": int(ll[5]), "free_before": free0, "free_after": free1,
                     "vram_used_before": used0, "vram_used_after": used1,
                     "closed": stat("direct_closed") - closed0, "retired": stat("direct_retired"),
-                    "maps": stat("direct_maps"), "quarantined": stat("direct_quarantined")}
+                    "maps": stat("direct_maps"), "refused": stat("direct_refused")}
             open(os.path.join(outdir, "case%d_rank%d.json" % (i, rank)), "w").write(json.dumps(info))
             out = np.concatenate([got, small.cpu().numpy().view(np.uint8)])
             np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
@@ -323,8 +323,8 @@ def main():
             open(os.path.join(outdir, "case%d_rank%d.launch" % (i, rank)), "w").write(json.dumps([int(x) for x in ll]))
         if c.get("direct_stats"):  # the direct schedule's rendezvous / mapping counters after this case
             st = {}
-            for k in ("direct_check", "direct_calls", "direct_retired", "direct_closed", "direct_maps",
-                      "direct_exports", "direct_quarantined", "direct_rendezvous_ns", "direct_export_ns"):
+            for k in ("direct_check", "direct_calls", "direct_retired", "direct_closed", "direct_maps", "flags_kind",
+                      "direct_exports", "direct_refused", "direct_rendezvous_ns", "direct_export_ns"):
                 v = ctypes.c_uint64()
                 check_call(_LIB.RdcCommGetParam(comm.handle, k.encode(), ctypes.byref(v)))
                 st[k] = int(v.value)

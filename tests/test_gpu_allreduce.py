@@ -1401,10 +1401,12 @@ def test_mp_direct_after_free(world):
     mapping the freed allocation would get that stale mapping back for the
     new one: the exporter retires the dead allocation in its rendezvous slot
     and every peer closes its mapping (after its previous direct launch
-    finished) before opening the new handle, then holds the closed range
-    reserved.  Round 6: EVERY call takes the direct schedule
-    (round 5's rule made these fall back), every result bit-exact against the
-    oracle's ring, and mappings are closed as allocations die."""
+    finished) before opening the new handle; a new mapping that lands partly
+    over ranges the process unmapped is closed unused and that call falls
+    back (the fault's trigger).  Round 6: every other call
+    takes the direct schedule (round 5's rule made these fall back), every
+    result bit-exact against the oracle's ring, and mappings are closed as
+    allocations die."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cases = []
@@ -1419,13 +1421,23 @@ def test_mp_direct_after_free(world):
         for r in range(world):
             got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
             assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, c, r)
+    st = [[json.load(open(os.path.join(tmp, "case%d_rank%d.stats" % (i, r)))) for i in range(len(cases))]
+          for r in range(world)]
+    ll = [[json.load(open(os.path.join(tmp, "case%d_rank%d.launch" % (i, r)))) for i in range(len(cases))]
+          for r in range(world)]
+    for i in range(len(cases)):
+        # the direct schedule on every call, except where some rank's new peer
+        # mapping landed partly over ranges it had unmapped (refused: every rank
+        # takes the scratch schedules for that call)
+        refused = any(st[r][i]["direct_refused"] > (st[r][i - 1]["direct_refused"] if i else 0)
+                      for r in range(world))
+        for r in range(world):
+            assert ll[r][i][5] == 6 or (refused and ll[r][i][5] in (1, 2, 5)), (i, r, ll[r][i], st[r][i])
     for r in range(world):
-        ll = [json.load(open(os.path.join(tmp, "case%d_rank%d.launch" % (i, r)))) for i in range(len(cases))]
-        assert all(x[5] == 6 for x in ll), (r, ll)  # the direct schedule on every call
-        st = [json.load(open(os.path.join(tmp, "case%d_rank%d.stats" % (i, r)))) for i in range(len(cases))]
         # dead allocations are retired and their peer mappings closed as the run goes
-        assert st[-1]["direct_retired"] >= 1 and st[-1]["direct_closed"] >= 1, (r, st[-1])
-        assert st[-1]["direct_maps"] <= 4 * (world - 1), (r, st[-1])
+        assert st[r][-1]["direct_retired"] >= 1 and st[r][-1]["direct_closed"] >= 1, (r, st[r][-1])
+        assert st[r][-1]["direct_maps"] <= 4 * (world - 1), (r, st[r][-1])
+    assert sum(x[5] == 6 for x in ll[0]) >= len(cases) // 2, ll[0]
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -1454,6 +1466,9 @@ def test_mp_direct_is_the_untuned_default(world):
                 assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (env, i, r)
         ll = [json.load(open(os.path.join(tmp, "case%d_rank0.launch" % i))) for i in range(len(cases))]
         st = json.load(open(os.path.join(tmp, "case0_rank0.stats")))
+        # round 6: the flag words of a multi-process channel are HSA-uncached (MTYPE UC), not
+        # hipDeviceMallocUncached (MTYPE CC on gfx950: profiles/r06/mtype/)
+        assert st["flags_kind"] == 3, st
         if want_direct:
             assert st["direct_check"] == 1, st  # checked at creation, no autotune ran
             assert ll[0][5] == 6 and ll[1][5] == 6 and ll[3][5] == 6, ll
@@ -1481,11 +1496,10 @@ def test_mp_direct_freed_memory_returned(world):
         info = json.load(open(os.path.join(tmp, "case0_rank%d.json" % r)))
         assert info["first_algo"] == 6 and info["second_algo"] == 6, info
         assert info["closed"] >= world - 1, info
-        # device-wide VRAM in use (the driver's counter; hipMemGetInfo where it is unreadable)
-        if info["vram_used_before"] >= 0 and info["vram_used_after"] >= 0:
-            assert info["vram_used_before"] - info["vram_used_after"] >= (512 << 20) - (64 << 20), info
-        else:
-            assert info["free_after"] - info["free_before"] >= (512 << 20) - (64 << 20), info
+        # hipMemGetInfo's free bytes (device-wide): the peers' closes released this rank's 512 MiB
+        # (round 6 first run: +988 MiB at n = 2, both ranks' buffers; the sysfs vram counter seen
+        # from the box's container did not track this GPU and is only recorded)
+        assert info["free_after"] - info["free_before"] >= (512 << 20) - (64 << 20), info
         assert got[4096:].tobytes() == np.frombuffer(second[r].tobytes(), dtype=np.uint8).tobytes(), r
     # the big buffer's head (its first 4 KiB) against the full-size oracle
     want_big = expected_for({"count": count, "dtype": 6, "op": 2, "seed": 0x5EEDA000}, world)
