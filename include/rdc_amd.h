@@ -375,7 +375,7 @@ int RdcPlanAutoAlgo(int n, size_t bytes, size_t scratch_bytes, size_t oneshot_by
  * registered-buffer schedule (RDC_ALGO_DIRECT) when every rank's buffer can be
  * mapped and the channel's direct self-check passed: 1 / 0 (negative on bad
  * arguments).  direct_min = RDC_DIRECT_BYTES: RDC_DIRECT_MIN_AUTO (the
- * default) = beyond the one-shot sizes and from 1 MiB; 0 = never; N = from N
+ * default) = beyond the one-shot sizes and from 16 MiB (32 MiB at n = 2); 0 = never; N = from N
  * bytes.  Replaces nothing in the reference (its one schedule is the ring);
  * the drop-in rdc::Allreduce / rdc.allreduce calls get it without tuning. */
 #define RDC_DIRECT_MIN_AUTO (~(uint64_t)0)

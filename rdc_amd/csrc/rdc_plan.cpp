@@ -159,7 +159,7 @@ int AutoAlgo(int n, uint64_t bytes, const Layout& L, uint64_t push_max) {
 bool DirectAuto(int n, uint64_t bytes, const Layout& L, uint64_t push_max, uint64_t direct_min) {
     if (n < 2 || direct_min == 0) return false;
     if (direct_min != kDirectMinAuto) return bytes >= direct_min;
-    if (bytes < kDirectAutoMinBytes) return false;
+    if (bytes < (n == 2 ? kDirectAutoMinBytes2 : kDirectAutoMinBytes)) return false;
     const int a = AutoAlgo(n, bytes, L, push_max);
     return a == RDC_ALGO_RING || a == RDC_ALGO_MESH;
 }

@@ -91,14 +91,20 @@ int AutoAlgo(int n, uint64_t bytes, const Layout& L, uint64_t push_max);
 // RDC_ALGO=auto call on a multi-process channel whose direct self-check
 // passed.  direct_min (RDC_DIRECT_BYTES): kDirectMinAuto (the default) = where
 // AutoAlgo picks a two-hand-off schedule (ring or mesh, i.e. above the
-// one-shot sizes) and the buffer is at least kDirectAutoMinBytes; 0 = never;
-// otherwise from direct_min bytes.  Why there: the direct schedule moves 2 S
-// of HBM per rank where the ring moves 9(n-1)/n S and the pull mesh
-// (5n-2)/n S (ModelHbmBytes), the same link bytes as the mesh, and pays one
-// host rendezvous per call (two shared-memory stamps, measured in
-// profiles/r06/direct_default/), which the one-shot sizes do not amortise.
+// one-shot sizes) and the buffer is at least kDirectAutoMinBytes (n >= 3) or
+// kDirectAutoMinBytes2 (n = 2); 0 = never; otherwise from direct_min bytes.
+// Why there: the direct schedule moves 2 S of HBM per rank where the ring
+// moves 9(n-1)/n S and the pull mesh (5n-2)/n S (ModelHbmBytes), the same
+// link bytes as the mesh, and pays one host rendezvous per call (two
+// shared-memory stamps: 2-3 us at n = 2, 6-11 us at n = 8, export ~1 us of
+// it) and one hand-off where the mesh has two.  Per-size sweep, ranks on one
+// GPU (tools/algo_sweep.py, profiles/r06/direct_default/): n = 8 direct
+// 0.117 vs pull mesh 0.103 ms at 4 MiB, 0.142 vs 0.164 at 16 MiB, 0.81 vs
+// 1.92 at 256 MiB; n = 2 direct 0.0315 vs ring 0.0258 ms at 16 MiB, 0.064 vs
+// 0.090 at 64 MiB.
 constexpr uint64_t kDirectMinAuto = ~(uint64_t)0;
-constexpr uint64_t kDirectAutoMinBytes = (uint64_t)1 << 20;
+constexpr uint64_t kDirectAutoMinBytes = (uint64_t)16 << 20;
+constexpr uint64_t kDirectAutoMinBytes2 = (uint64_t)32 << 20;
 bool DirectAuto(int n, uint64_t bytes, const Layout& L, uint64_t push_max, uint64_t direct_min);
 uint64_t OneshotHalfBytes(const Layout& L);
 Piece PlanOneshot(int n, uint64_t count, size_t esz, const Layout& L, size_t cfg_tile, int max_blocks);

@@ -1444,7 +1444,8 @@ def test_mp_direct_after_free(world):
 def test_mp_direct_is_the_untuned_default(world):
     """Round 6: without RdcCommAutotune, an automatic
     allreduce (algo 0, what rdc::Allreduce / rdc.allreduce issue) of a device
-    buffer above the one-shot sizes takes the direct schedule, because the
+    buffer above the one-shot sizes and the default threshold (16 MiB; 32 MiB
+    at n = 2) takes the direct schedule, because the
     channel ran its self-check at creation (direct_check 1); smaller buffers
     keep the one-shot; a coalesced list above the threshold is one direct
     launch; RDC_DIRECT_BYTES=0 restores the scratch schedules.  Every result
@@ -1455,7 +1456,7 @@ def test_mp_direct_is_the_untuned_default(world):
     cases = [{"count": big, "dtype": 6, "op": 2, "last_launch": True, "direct_stats": True},
              {"count": big, "dtype": 10, "op": 2, "last_launch": True, "reps": 2},
              {"count": 70001, "dtype": 6, "op": 2, "last_launch": True},
-             {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1 << 20] * 8 + [12345],
+             {"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1 << 18] * 40 + [12345],
               "same_pads": True, "last_launch": True}]
     for env, want_direct in (({}, True), ({"RDC_DIRECT_BYTES": "0"}, False)):
         tmp = run_mp(world, cases, timeout=300, env_extra=env)
@@ -1494,7 +1495,9 @@ def test_mp_direct_freed_memory_returned(world):
     for r in range(world):
         got = np.load(os.path.join(tmp, "case0_rank%d.npy" % r))
         info = json.load(open(os.path.join(tmp, "case0_rank%d.json" % r)))
-        assert info["first_algo"] == 6 and info["second_algo"] == 6, info
+        # the second call maps a fresh 16 MiB buffer: direct, or — where the runtime placed a peer
+        # mapping partly over the freed big buffer's range — refused and run on the scratch schedules
+        assert info["first_algo"] == 6 and (info["second_algo"] == 6 or info["refused"] > 0), info
         assert info["closed"] >= world - 1, info
         # hipMemGetInfo's free bytes (device-wide): the peers' closes released this rank's 512 MiB
         # (round 6 first run: +988 MiB at n = 2, both ranks' buffers; the sysfs vram counter seen

@@ -243,7 +243,7 @@ def test_direct_default_rule():
     """rdc_plan.h DirectAuto (round 6): an untuned automatic allreduce on a
     multi-process channel takes the direct schedule where the automatic rule
     would pick a two-hand-off schedule (ring at n = 2, mesh from n = 3: above
-    the one-shot sizes) and from 1 MiB; RDC_DIRECT_BYTES = 0 turns it off, a
+    the one-shot sizes) and from 16 MiB (32 MiB at n = 2); RDC_DIRECT_BYTES = 0 turns it off, a
     number sets the threshold.  This is the rule the drop-in rdc::Allreduce /
     rdc.allreduce calls get without RdcCommAutotune."""
     from rdc_amd._lib import _LIB
@@ -253,16 +253,17 @@ def test_direct_default_rule():
 
     def direct(n, b, dmin=AUTO, ob=0):
         return _LIB.RdcPlanDirectAuto(n, b, scratch, ob, dmin)
-    # n = 2: the one-shot up to 8 MiB, the direct schedule beyond (where the ring was)
-    assert direct(2, 8 * M) == 0 and direct(2, 8 * M + 4) == 1 and direct(2, 1 << 30) == 1
-    # n = 8: the one-shot up to 798,912 bytes, then the mesh's sizes from 1 MiB
-    assert direct(8, 798912) == 0 and direct(8, 900 * 1024) == 0 and direct(8, M) == 1
+    # n = 2: the ring from 8 MiB, the direct schedule from 32 MiB (profiles/r06/direct_default/)
+    assert direct(2, 8 * M + 4) == 0 and direct(2, 32 * M - 4) == 0 and direct(2, 32 * M) == 1
+    assert direct(2, 1 << 30) == 1
+    # n = 8: the one-shot up to 798,912 bytes, the mesh, then the direct schedule from 16 MiB
+    assert direct(8, 798912) == 0 and direct(8, M) == 0 and direct(8, 16 * M - 4) == 0 and direct(8, 16 * M) == 1
     assert direct(8, 256 * M) == 1 and direct(8, 1 << 30) == 1
-    # every size where the rule picks ring / mesh and >= 1 MiB, and nowhere else
+    # every size where the rule picks ring / mesh and >= the threshold, and nowhere else
     for n in (2, 3, 4, 5, 8, 16):
-        for b in (4, 4096, M - 4, M, 3 * M, 6 * M, 8 * M, 9 * M, 64 * M, 1 << 30):
+        for b in (4, 4096, M - 4, M, 3 * M, 6 * M, 8 * M, 9 * M, 16 * M, 20 * M, 32 * M, 64 * M, 1 << 30):
             a = _LIB.RdcPlanAutoAlgo(n, b, scratch, 0)
-            assert direct(n, b) == (1 if a in (1, 2) and b >= M else 0), (n, b, a)
+            assert direct(n, b) == (1 if a in (1, 2) and b >= (32 * M if n == 2 else 16 * M) else 0), (n, b, a)
     # RDC_DIRECT_BYTES=0: never (only algo 6 / RDC_ALGO=direct / an autotuned entry); N: from N bytes
     assert direct(8, 1 << 30, 0) == 0 and direct(2, 1 << 30, 0) == 0
     assert direct(2, 4096, 4096) == 1 and direct(2, 4095, 4096) == 0
