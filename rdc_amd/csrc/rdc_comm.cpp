@@ -853,17 +853,87 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     bs->allgather(&h, sizeof(h), hs.data());
     dbg("[rdc %d] %s\n", c->rank_, "handles exchanged");
     Channel* ch = c->ch_.get();
+    // the channel's regions of every peer; an HSA-uncached region (kind 3)
+    // that cannot be attached here is reported, not thrown: the ranks agree
+    // below and, if any attach failed anywhere, every kind-3 region becomes
+    // kind 0 on every rank and the regions are exchanged again
+    const char* rwhat[4] = {"import (scratch)", "import (ag)", "import (flags)", "import (service)"};
+    // test hook: RDC_TEST_FAIL_HSA_ATTACH=<rank> makes that rank's kind-3 attaches fail
+    const char* fail_env = getenv("RDC_TEST_FAIL_HSA_ATTACH");
+    const bool fail_here = fail_env && *fail_env && atoi(fail_env) == c->rank_;
+    auto import_all = [&](const std::vector<Handles>& hv) -> bool {
+        bool ok = true;
+        for (int p = 0; p < c->n_; ++p) {
+            if (p == c->rank_) continue;
+            const RegionHandle* rh = hv[(size_t)p].region;
+            void* got[4] = {nullptr, nullptr, nullptr, nullptr};
+            for (int r = 0; r < 4; ++r) {
+                ch->peer_kind[r][p] = (int8_t)rh[r].kind;
+                if (rh[r].kind == kKindHsaUC) {
+                    try {
+                        if (fail_here) throw std::runtime_error("injected attach failure");
+                        got[r] = import_region(rh[r], device, rwhat[r]);
+                    } catch (const std::exception&) {
+                        ok = false;
+                    }
+                } else {
+                    got[r] = import_region(rh[r], device, rwhat[r]);
+                }
+            }
+            ch->peer_scratch[p] = static_cast<char*>(got[0]);
+            ch->peer_ag[p] = static_cast<char*>(got[1]);
+            ch->peer_flags[p] = static_cast<uint64_t*>(got[2]);
+            ch->peer_svc_region[p] = static_cast<char*>(got[3]);
+        }
+        return ok;
+    };
+    if (!share) {
+        ch->ipc = true;
+        const bool ok = import_all(hs);
+        int32_t mine_ok = ok ? 1 : 0;
+        std::vector<int32_t> oks((size_t)c->n_);
+        bs->allgather(&mine_ok, sizeof(mine_ok), oks.data());
+        bool all_ok = true;
+        for (int32_t v : oks) all_ok = all_ok && v != 0;
+        if (!all_ok) {
+            if (c->rank_ == 0)
+                fprintf(stderr, "rdc: an HSA-uncached channel region could not be attached on some rank; every "
+                                "rank falls back to hipDeviceMallocUncached regions (RDC_FLAGS_MEM=cc)\n");
+            for (int p = 0; p < c->n_; ++p) {
+                if (p == c->rank_) continue;
+                close_region(ch->peer_scratch[p], ch->peer_kind[0][p]);
+                close_region(ch->peer_ag[p], ch->peer_kind[1][p]);
+                close_region(ch->peer_flags[p], ch->peer_kind[2][p]);
+                close_region(ch->peer_svc_region[p], ch->peer_kind[3][p]);
+                ch->peer_scratch[p] = ch->peer_ag[p] = nullptr;
+                ch->peer_flags[p] = nullptr;
+                ch->peer_svc_region[p] = nullptr;
+            }
+            void** own[4] = {reinterpret_cast<void**>(&ch->scratch), reinterpret_cast<void**>(&ch->scratch_ag),
+                             reinterpret_cast<void**>(&ch->flags), reinterpret_cast<void**>(&ch->svc_region)};
+            for (int r = 0; r < 4; ++r) {
+                if (ch->region_kind[r] != kKindHsaUC) continue;
+                free_shared(*own[r], kKindHsaUC);
+                int k = 0;
+                *own[r] = alloc_shared(ch->region_bytes[r], &k, device, 0);
+                ch->region_kind[r] = k;
+                hip_check(hipMemset(*own[r], 0, ch->region_bytes[r]), "memset channel region");
+            }
+            hip_check(hipDeviceSynchronize(), "sync after fallback alloc");
+            ch->peer_scratch[c->rank_] = ch->scratch;
+            ch->peer_ag[c->rank_] = ch->scratch_ag;
+            ch->peer_flags[c->rank_] = ch->flags;
+            ch->peer_svc_region[c->rank_] = ch->svc_region;
+            const char* what[4] = {"IPC handle (scratch)", "IPC handle (ag)", "IPC handle (flags)",
+                                   "IPC handle (service)"};
+            for (int r = 0; r < 4; ++r)
+                export_region(*own[r], ch->region_bytes[r], ch->region_kind[r], &h.region[r], what[r]);
+            bs->allgather(&h, sizeof(h), hs.data());
+            if (!import_all(hs)) throw std::runtime_error("rdc: channel regions could not be mapped");
+        }
+    }
     for (int p = 0; p < c->n_; ++p) {
         if (p == c->rank_) continue;
-        if (!share) {
-            const RegionHandle* rh = hs[(size_t)p].region;
-            for (int r = 0; r < 4; ++r) ch->peer_kind[r][p] = (int8_t)rh[r].kind;
-            ch->ipc = true;
-            ch->peer_scratch[p] = static_cast<char*>(import_region(rh[0], device, "import (scratch)"));
-            ch->peer_ag[p] = static_cast<char*>(import_region(rh[1], device, "import (ag)"));
-            ch->peer_flags[p] = static_cast<uint64_t*>(import_region(rh[2], device, "import (flags)"));
-            ch->peer_svc_region[p] = static_cast<char*>(import_region(rh[3], device, "import (service)"));
-        }
         void* pp = nullptr;
         hip_check(hipIpcOpenMemHandle(&pp, hs[(size_t)p].p2p, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(p2p)");
         c->peer_p2p_[p] = static_cast<char*>(pp);

@@ -1479,6 +1479,27 @@ def test_mp_direct_is_the_untuned_default(world):
             assert all(x[5] != 6 for x in ll), ll
 
 
+def test_mp_uncached_flags_fall_back_together():
+    """The flag words and service slots of a multi-process channel are
+    HSA-uncached (MTYPE UC, attached through HSA IPC).  If any rank cannot
+    attach a peer's region, every rank replaces its HSA-uncached regions with
+    hipDeviceMallocUncached ones and the regions are exchanged again
+    (RDC_TEST_FAIL_HSA_ATTACH=1 makes rank 1's attaches fail): flags kind 0 on
+    every rank, every schedule still bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cases = [{"count": 100003, "dtype": 6, "op": 2, "algo": a, "direct_stats": True} for a in (1, 2, 3, 5, 6)]
+    cases.append({"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"})
+    tmp = run_mp(3, cases, timeout=300, env_extra={"RDC_TEST_FAIL_HSA_ATTACH": "1"})
+    for i, c in enumerate(cases):
+        want = expected_for(c, 3)
+        for r in range(3):
+            got = np.load(os.path.join(tmp, "case%d_rank%d.npy" % (i, r)))
+            assert got.tobytes() == np.frombuffer(want[r].tobytes(), dtype=np.uint8).tobytes(), (i, r)
+            if c.get("direct_stats"):
+                assert json.load(open(os.path.join(tmp, "case%d_rank%d.stats" % (i, r))))["flags_kind"] == 0
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_mp_direct_freed_memory_returned(world):
     """A 512 MiB buffer through the direct schedule, freed back to HIP: the
