@@ -780,8 +780,9 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
         // scheduler (~10 ms slices): a collective spinning on a peer whose
         // queue is not mapped waits a slice (DESIGN.md §4, round 3 session 3)
         // The advice is rdc_amd.launcher's budget (hw_queues_per_process): the
-        // share of 16 rounded down to a power of two — 3 queues per process
-        // at 5-6 ranks per GPU lost hand-offs in round 5 (profiles/r05/queues/)
+        // share of 16 rounded down to a power of two — with 3 queues per
+        // process at 5-6 ranks per GPU the GPU left one rank's kernel
+        // undispatched behind its peers' spinning kernels
         const char* q = getenv("GPU_MAX_HW_QUEUES");
         const int per = q && *q ? atoi(q) : 4;
         static bool warned = false;
@@ -792,8 +793,9 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
             warned = true;
             fprintf(stderr,
                     "rdc: %d ranks share one GPU with GPU_MAX_HW_QUEUES=%d each; set GPU_MAX_HW_QUEUES=%d "
-                    "(rdc_amd.launcher does): more than 16 queues are time-sliced (~10 ms per slice) and a "
-                    "budget that is not a power of two lost hand-offs at 5-6 ranks per GPU\n",
+                    "(rdc_amd.launcher does): more than 16 queues are time-sliced (~10 ms per slice) and with "
+                    "3 per process at 5-6 ranks per GPU one rank's kernel went undispatched while its peers "
+                    "waited\n",
                     c->share_max_, per, want);
         }
     }
@@ -1418,6 +1420,11 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
                 if (cur->first + cur->second.size <= bs || cur->second.id == (uint64_t)id) continue;
                 if (!retire(cur)) why = "retire list full";
             }
+            // hipIpcOpenMemHandle of an allocation of 2 GiB or more never
+            // returns on this stack (rdc_plan.h kMaxRegionBytes): such a
+            // buffer takes the scratch schedules (round 6: the untuned default
+            // sent test_mp_count_beyond_int32's 2 GiB buffer here and hung)
+            if (!why && size > kMaxRegionBytes) why = "allocation of 2 GiB or more (HIP IPC cannot map it)";
             auto it = ch.dexports.find(bs);
             if (!why && it == ch.dexports.end()) {
                 if (ch.dexports.size() >= kDirectExportsMax)

@@ -150,14 +150,14 @@ QUEUE_BUDGET = 16
 def hw_queues_per_process(ranks_per_gpu):
     """GPU_MAX_HW_QUEUES for a process that shares its GPU with
     ranks_per_gpu - 1 others (None: leave HIP's default of 4): the budget's
-    share rounded down to a power of two, so never 3.  Three queues per
-    process with 5 or more processes on one GPU lose hand-offs (DESIGN.md
-    §4.2, round 5): a rank's device reads of a peer's flag keep returning the
-    previous launch's number — every load kind, atomics and reads after a
-    system acquire alike — while the host reads the new one at the same
-    address.  At one block per CU (RDC_DEBUG_LDS_PAD=96K) 5 x 3 and 6 x 3
-    failed every run, 5 x 1, 5 x 2, 5 x 4, 6 x 2, 8 x 2, 4 x 2, 4 x 3 and 3 x 3
-    never (profiles/r05/queues/)."""
+    share rounded down to a power of two, so never 3.  With three queues per
+    process and 5 or more processes on one GPU, the GPU's scheduler left one
+    rank's next collective kernel undispatched for as long as its peers'
+    kernels spun waiting for it (device launch timelines, the
+    late rank's kernel started exactly when the waiters timed out; round 6).
+    At one block per CU (RDC_DEBUG_LDS_PAD=96K) 5 x 3 and 6 x 3 failed every
+    run, 5 x 1, 5 x 2, 5 x 4, 6 x 2, 8 x 2, 4 x 2, 4 x 3 and 3 x 3 never
+    (profiles/r05/queues/).  One rank per GPU is not affected."""
     if ranks_per_gpu * 4 <= QUEUE_BUDGET:
         return None
     q = max(1, QUEUE_BUDGET // ranks_per_gpu)
