@@ -1405,7 +1405,12 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
                          hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)buf) == hipSuccess && base != nullptr &&
                          buf + bytes[b] <= (char*)base + size;
         (void)hipGetLastError();
-        if (!dev) return false;
+        if (!dev) {
+            if (direct_log())
+                fprintf(stderr, "rdc-direct r%d call %llu: buffer %d %p is not exportable device memory\n", rank_,
+                        (unsigned long long)call, b, (void*)buf);
+            return false;
+        }
         auto ix = alloc_index.find((uint64_t)id);
         const uint32_t ai = ix != alloc_index.end() ? ix->second : me.nalloc;
         if (ai == me.nalloc) {  // this call's first buffer in that allocation: export it
@@ -1526,13 +1531,22 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
             auto key = std::make_pair(p, slots[p].alloc[i].id);
             auto it = ch.dmaps.find(key);
             if (it == ch.dmaps.end()) {
-                if (ch.dmaps.size() >= kDirectMapsMax) return false;  // full: no new mappings
-                if (ch.drefused.count(key)) return false;              // its mapping landed over unmapped ranges
-                void* m = nullptr;
-                if (hipIpcOpenMemHandle(&m, slots[p].alloc[i].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
-                    !m) {
-                    (void)hipGetLastError();
+                auto fail = [&](const char* why) {
+                    if (direct_log())
+                        fprintf(stderr, "rdc-direct r%d call %llu: peer %d id %llu not mapped: %s\n", rank_,
+                                (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id, why);
                     return false;
+                };
+                if (ch.dmaps.size() >= kDirectMapsMax) return fail("mapping table full");
+                if (ch.drefused.count(key)) {  // counted per call that falls back for it
+                    ++ch.dstat_refused;
+                    return fail("refused earlier (landed over unmapped ranges)");
+                }
+                void* m = nullptr;
+                const hipError_t oe = hipIpcOpenMemHandle(&m, slots[p].alloc[i].handle, hipIpcMemLazyEnablePeerAccess);
+                if (oe != hipSuccess || !m) {
+                    (void)hipGetLastError();
+                    return fail(oe != hipSuccess ? hipGetErrorString(oe) : "null mapping");
                 }
                 // a pointer this rank already holds for another allocation
                 // would be the stale mapping described above: never use it

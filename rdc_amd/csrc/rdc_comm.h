@@ -264,7 +264,8 @@ public:
     // the channel's direct-schedule counters: "direct_calls" (rendezvous),
     // "direct_rendezvous_ns" / "direct_export_ns" (host time, summed),
     // "direct_retired" / "direct_closed" / "direct_refused" (mapping life
-    // cycle), "direct_close_wait_ns", "direct_maps" / "direct_exports" (held now)
+    // cycle; direct_refused counts the calls this rank refused a peer mapping
+    // in), "direct_close_wait_ns", "direct_maps" / "direct_exports" (held now)
     uint64_t DirectStat(const std::string& key) const;
 
     // Collective (every rank, same arguments, no collective in flight): time

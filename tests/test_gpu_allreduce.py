@@ -10,6 +10,7 @@ import os
 import subprocess
 import sys
 import tempfile
+import time
 
 import numpy as np
 import pytest
@@ -395,15 +396,32 @@ def run_mp(world, cases, timeout=240, env_extra=None):
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), str(r), str(world),
                                str(port), tmp, cf], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
              for r in range(world)]
+    # RDC_TEST_MP_TIMEOUT (debug runs): a shorter limit than the test's
+    if os.environ.get("RDC_TEST_MP_TIMEOUT"):
+        timeout = min(timeout, float(os.environ["RDC_TEST_MP_TIMEOUT"]))
     outs = []
+    deadline = time.time() + timeout
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=timeout)
+            out, _ = p.communicate(timeout=max(1.0, deadline - time.time()))
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
-            raise
+            tails = []
+            for r, q in enumerate(procs):  # what every rank printed before the kill
+                try:
+                    o, _ = q.communicate(timeout=10)
+                    tails.append("rank %d:\n%s" % (r, o.decode(errors="replace")[-1500:]))
+                except Exception:  # noqa: BLE001
+                    tails.append("rank %d: (no output)" % r)
+            raise AssertionError("multi-process run timed out after %.0f s\n%s" % (timeout, "\n".join(tails)))
         outs.append(out.decode(errors="replace"))
+    if os.environ.get("RDC_TEST_MP_LOGDIR"):  # debug runs: every rank's whole output
+        d = os.environ["RDC_TEST_MP_LOGDIR"]
+        os.makedirs(d, exist_ok=True)
+        for r, o in enumerate(outs):
+            with open(os.path.join(d, "%s_rank%d.log" % (os.path.basename(tmp), r)), "w") as f:
+                f.write(o)
     failed = [r for r, p in enumerate(procs) if p.returncode != 0]
     assert not failed, "\n".join("rank %d failed (rc %d):\n%s" % (r, procs[r].returncode, outs[r][-1500:])
                                   for r in failed)
@@ -856,6 +874,13 @@ def test_mp_across_devices(world):
     cases += [{"count": (16 << 20) + 5, "dtype": 6, "op": 2, "algo": a} for a in (1, 2, 5, 6)]
     cases += [{"count": 0, "dtype": 6, "op": 2, "kind": "coalesced", "counts": [1024, 70001, 333] * 3, "algo": 6,
                "same_pads": True}]
+    # the direct schedule's result hand-off across GPUs: every line of the buffer in this
+    # GPU's L2s (a read kernel before each call) when remote owners overwrite it, read back
+    # by a kernel (DESIGN.md §4.2 "what the second row rests on")
+    cases += [{"count": c, "dtype": 6, "op": 2, "algo": 6, "reps": 3, "warm_l2": True, "seed": 0x5EEDF000 + c}
+              for c in (16384, 262147, 1 << 20)]
+    # the untuned default on a buffer above the threshold (the direct schedule where the check passed)
+    cases += [{"count": (64 << 20) // 4 + 7, "dtype": 6, "op": 2, "algo": 0}]
     cases += [{"count": 4096, "dtype": 6, "op": 2, "kind": "host_allreduce"},
               {"count": (40 << 20) + 3, "dtype": 1, "op": 0, "kind": "host_allreduce"},
               {"count": (3 << 20) + 5, "dtype": 0, "kind": "broadcast", "root": world - 1}]
