@@ -206,7 +206,13 @@ int RdcCommCheck(void* comm, void* stream);
  * (1 when another communicator uses the same scratch channel: every named
  * communicator over the same ranks shares one, RDC_SHARE_SCRATCH=0 disables),
  * "host_registered_calls" (host allreduces of this process that DMA'd in place
- * from a pinned RdcNewBuffer range). */
+ * from a pinned RdcNewBuffer range), "RDC_DIRECT_BYTES" (RDC_DIRECT_MIN_AUTO =
+ * the default rule), "direct_check" (the channel's direct self-check, run at
+ * creation: 0 not run, 1 passed, 2 failed), "flags_kind" / "scratch_kind" (3 =
+ * HSA-uncached, MTYPE UC; 0 = hipDeviceMallocUncached, MTYPE CC on gfx950),
+ * and the direct schedule's counters "direct_calls", "direct_rendezvous_ns",
+ * "direct_export_ns", "direct_retired", "direct_closed", "direct_refused",
+ * "direct_close_wait_ns", "direct_maps", "direct_exports" (DESIGN.md §4.3). */
 int RdcCommGetParam(void* comm, const char* key, uint64_t* value);
 int RdcCommRank(void* comm);
 int RdcCommSize(void* comm);
