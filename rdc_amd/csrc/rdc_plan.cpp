@@ -44,7 +44,13 @@ int ResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu, int xc
     // a dispatch sends workgroup i to XCD i % xcds, so each XCD must hold
     // every rank's share of it; reserved CUs (resident service blocks) may
     // all sit on one XCD, so every XCD gives them up
-    const long per_xcd = bpc * (cus / xcds) - bpc * std::max(0, reserve_cus);
+    long per_xcd = bpc * (cus / xcds) - bpc * std::max(0, reserve_cus);
+    // Ranks sharing a GPU at one block per CU keep 3/8 of every XCD's CUs free:
+    // with 5 processes x 3 hardware queues, grids filling 30 (and 25) of an
+    // XCD's 32 CUs left one rank's next kernel undispatched behind its peers'
+    // spinning ones in every run (3 of 3), 20 of 32 never (3 of 3), and 5 of
+    // 32 passed too (DESIGN.md §4.2 failure 2, profiles/r06/queues/)
+    if (ranks > 1 && bpc == 1 && xcds > 1) per_xcd = per_xcd * 5 / 8;
     const long cap = std::max(1L, per_xcd / ranks * xcds);
     return (int)std::max(1L, std::min<long>(want, cap));
 }
