@@ -157,7 +157,11 @@ def hw_queues_per_process(ranks_per_gpu):
     late rank's kernel started exactly when the waiters timed out; round 6).
     At one block per CU (RDC_DEBUG_LDS_PAD=96K) 5 x 3 and 6 x 3 failed every
     run, 5 x 1, 5 x 2, 5 x 4, 6 x 2, 8 x 2, 4 x 2, 4 x 3 and 3 x 3 never
-    (profiles/r05/queues/).  One rank per GPU is not affected."""
+    (profiles/r05/queues/).  Round 6 found it depends on how full the XCDs
+    are: ResidentGrid now keeps 3/8 of every XCD free for ranks sharing a GPU
+    at one block per CU, and 5 x 3 and 6 x 3 then pass every run — this
+    budget is kept, no longer load-bearing.  One rank per GPU is not
+    affected."""
     if ranks_per_gpu * 4 <= QUEUE_BUDGET:
         return None
     q = max(1, QUEUE_BUDGET // ranks_per_gpu)
