@@ -1477,9 +1477,10 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
 
 // Step 2: every rank's allocations as mapped in this process (*amap, indexed
 // q * kDirectAllocsMax + i; this rank's own from own_base), opening the ones
-// not mapped yet; false when one cannot be mapped.  First, the mappings of
-// allocations the peers retired are closed — after this rank's previous
-// direct launch (the last one that may read through them) has completed
+// not mapped yet; false when one cannot be mapped.  Before it (every call,
+// usable or not: DirectCloseRetired), the mappings of allocations the peers
+// retired are closed — after this rank's previous direct launch (the last
+// one that may read through them) has completed
 // (hipIpcCloseMemHandle also waits for the device: 250 ms for a kernel
 // spinning 250 ms, tools/ipc_remap_probe.hip "inflight").  A new mapping that
 // lands partly over a range this process unmapped or retired is closed again
@@ -1487,8 +1488,7 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
 // refused): the first launch through such a mapping faulted the GPU in round
 // 5 and, with those ranges held by hipMemAddressReserve, again in round 6
 // (profiles/r06/remap/).
-bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,
-                                  std::vector<char*>* amap) {
+void Communicator::DirectCloseRetired(const DirectDesc* slots, uint64_t call) {
     Channel& ch = *ch_;
     bool waited = false;
     for (int p = 0; p < n_; ++p) {
@@ -1520,6 +1520,11 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
         }
         for (uint32_t k = 0; k < nr; ++k) ch.drefused.erase(std::make_pair(p, slots[p].retired[k]));
     }
+}
+
+bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,
+                                  std::vector<char*>* amap) {
+    Channel& ch = *ch_;
     amap->assign((size_t)n_ * kDirectAllocsMax, nullptr);
     for (int p = 0; p < n_; ++p)
         for (uint32_t i = 0; i < slots[p].nalloc; ++i) {
@@ -1654,6 +1659,9 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     __atomic_store_n(&me.stamp0, call, __ATOMIC_RELEASE);
     if (!rendezvous_wait(slots, n_, &DirectDesc::stamp0, call, cfg_.timeout_s))
         throw std::runtime_error("rdc: registered-buffer rendezvous timed out (a peer did not join the allreduce)");
+    // the peers' retired allocations: closed whether or not this call runs
+    // direct (an exporter announces each retirement once)
+    DirectCloseRetired(slots, call);
     // 2) every rank's list usable and alike (same buffers' sizes, each buffer
     // congruent mod 16 on every rank)?  Then map the peers' allocations
     bool usable = true;

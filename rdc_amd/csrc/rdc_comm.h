@@ -392,6 +392,7 @@ private:
                       std::vector<char*>* own_base);
     bool DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,
                         std::vector<char*>* amap);
+    void DirectCloseRetired(const DirectDesc* slots, uint64_t call);
     // device tables of coalesced direct launches: owner items + every rank's
     // buffer addresses, cached by the call's layout
     struct DirectTable {

@@ -188,7 +188,12 @@ def main():
             free0 = torch.cuda.mem_get_info()[0]
             used0 = vram_used()
             closed0 = stat("direct_closed")
-            small = torch.empty(c["small"], dtype=torch.float32, device="cuda")
+            # second_pad: the second buffer sits rank x 4 bytes into its allocation, so the ranks'
+            # buffers differ mod 16 and that call cannot run direct — the peers must close the
+            # freed buffer's mappings in its rendezvous all the same
+            sp_pad = rank * 4 if c.get("second_pad") else 0
+            small_alloc = torch.empty(c["small"] + 4 * world, dtype=torch.float32, device="cuda")
+            small = small_alloc[sp_pad // 4: sp_pad // 4 + c["small"]]
             check_call(_LIB.RdcFill(ctypes.c_void_p(small.data_ptr()), c["small"], 6, 0x5EEDB000, rank, sp))
             check_call(_LIB.RdcCommAllreduceEx(comm.handle, ctypes.c_void_p(small.data_ptr()), c["small"], 6, 2, 6, sp))
             comm.check(sp)
@@ -203,7 +208,7 @@ def main():
             open(os.path.join(outdir, "case%d_rank%d.json" % (i, rank)), "w").write(json.dumps(info))
             out = np.concatenate([got, small.cpu().numpy().view(np.uint8)])
             np.save(os.path.join(outdir, "case%d_rank%d.npy" % (i, rank)), out)
-            del small
+            del small, small_alloc
             print("rank %d case %d ok" % (rank, i), flush=True)
             continue
         if kind == "bcast_chain":
