@@ -212,7 +212,14 @@ int RdcCommCheck(void* comm, void* stream);
  * HSA-uncached, MTYPE UC; 0 = hipDeviceMallocUncached, MTYPE CC on gfx950),
  * and the direct schedule's counters "direct_calls", "direct_rendezvous_ns",
  * "direct_export_ns", "direct_retired", "direct_closed", "direct_refused",
- * "direct_close_wait_ns", "direct_maps", "direct_exports" (DESIGN.md §4.3). */
+ * "direct_close_wait_ns", "direct_maps", "direct_exports", "direct_fallback"
+ * (calls that fell back, alike on every rank), "direct_unusable" (of them, the
+ * calls whose buffer lists could not run direct), "direct_map_failed" and
+ * "direct_fail_reason" (this rank's peer-mapping failures and the last one's
+ * code: 1 table full, 2 refused earlier, 3 open failed, 4 a mapping already
+ * held, 5 lands partly over unmapped ranges), "direct_export_failed" /
+ * "direct_export_error" (exports of this rank's allocations HIP refused and
+ * the last hipError_t). */
 int RdcCommGetParam(void* comm, const char* key, uint64_t* value);
 int RdcCommRank(void* comm);
 int RdcCommSize(void* comm);

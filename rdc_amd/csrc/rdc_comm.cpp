@@ -911,6 +911,10 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
                 ch->peer_flags[p] = nullptr;
                 ch->peer_svc_region[p] = nullptr;
             }
+            // every rank has let go of its peers' kind-3 regions before any
+            // exporter frees its own (no detach racing the free in the runtime)
+            dbg("[rdc %d] %s\n", c->rank_, "fallback: peers' regions detached");
+            bs->barrier();
             void** own[4] = {reinterpret_cast<void**>(&ch->scratch), reinterpret_cast<void**>(&ch->scratch_ag),
                              reinterpret_cast<void**>(&ch->flags), reinterpret_cast<void**>(&ch->svc_region)};
             for (int r = 0; r < 4; ++r) {
@@ -922,6 +926,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
                 hip_check(hipMemset(*own[r], 0, ch->region_bytes[r]), "memset channel region");
             }
             hip_check(hipDeviceSynchronize(), "sync after fallback alloc");
+            dbg("[rdc %d] %s\n", c->rank_, "fallback: own regions reallocated");
             ch->peer_scratch[c->rank_] = ch->scratch;
             ch->peer_ag[c->rank_] = ch->scratch_ag;
             ch->peer_flags[c->rank_] = ch->flags;
@@ -932,6 +937,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
                 export_region(*own[r], ch->region_bytes[r], ch->region_kind[r], &h.region[r], what[r]);
             bs->allgather(&h, sizeof(h), hs.data());
             if (!import_all(hs)) throw std::runtime_error("rdc: channel regions could not be mapped");
+            dbg("[rdc %d] %s\n", c->rank_, "fallback: regions exchanged again");
         }
     }
     for (int p = 0; p < c->n_; ++p) {
@@ -956,6 +962,7 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     // calls may take the schedule (DirectEligible).  Collective: share, dreg,
     // RDC_ALGO and RDC_DIRECT_BYTES are the same on every rank (plan keys).
     if (!share && ch->dreg && cfg.algo == RDC_ALGO_AUTO && cfg.direct_min != 0) {
+        dbg("[rdc %d] %s\n", c->rank_, "direct self-check");
         hipStream_t s = nullptr;
         hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "self-check stream");
         try {
@@ -1438,9 +1445,20 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
                     Channel::DirectExport ex;
                     ex.id = (uint64_t)id;
                     ex.size = size;
-                    if (hipIpcGetMemHandle(&ex.handle, base) == hipSuccess) it = ch.dexports.emplace(bs, ex).first;
-                    else why = "no IPC handle";
+                    const hipError_t ge = hipIpcGetMemHandle(&ex.handle, base);
                     (void)hipGetLastError();
+                    if (ge == hipSuccess) {
+                        it = ch.dexports.emplace(bs, ex).first;
+                    } else {
+                        why = "no IPC handle";
+                        ch.dexport_err = (uint64_t)ge;
+                        ++ch.dstat_exportfail;
+                        if (direct_log())
+                            fprintf(stderr, "rdc-direct r%d call %llu: hipIpcGetMemHandle(%p): %s (%d), %u retired "
+                                            "in this call\n",
+                                    rank_, (unsigned long long)call, (void*)base, hipGetErrorName(ge), (int)ge,
+                                    me.nretired);
+                    }
                 }
             }
             if (!why && me.nalloc >= (uint32_t)kDirectAllocsMax) why = "too many allocations in one call";
@@ -1536,22 +1554,24 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
             auto key = std::make_pair(p, slots[p].alloc[i].id);
             auto it = ch.dmaps.find(key);
             if (it == ch.dmaps.end()) {
-                auto fail = [&](const char* why) {
+                auto fail = [&](int code, const char* why) {
+                    ch.dfail_reason = code;
+                    ++ch.dstat_mapfail;
                     if (direct_log())
                         fprintf(stderr, "rdc-direct r%d call %llu: peer %d id %llu not mapped: %s\n", rank_,
                                 (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id, why);
                     return false;
                 };
-                if (ch.dmaps.size() >= kDirectMapsMax) return fail("mapping table full");
+                if (ch.dmaps.size() >= kDirectMapsMax) return fail(1, "mapping table full");
                 if (ch.drefused.count(key)) {  // counted per call that falls back for it
                     ++ch.dstat_refused;
-                    return fail("refused earlier (landed over unmapped ranges)");
+                    return fail(2, "refused earlier (landed over unmapped ranges)");
                 }
                 void* m = nullptr;
                 const hipError_t oe = hipIpcOpenMemHandle(&m, slots[p].alloc[i].handle, hipIpcMemLazyEnablePeerAccess);
                 if (oe != hipSuccess || !m) {
                     (void)hipGetLastError();
-                    return fail(oe != hipSuccess ? hipGetErrorString(oe) : "null mapping");
+                    return fail(3, oe != hipSuccess ? hipGetErrorString(oe) : "null mapping");
                 }
                 // a pointer this rank already holds for another allocation
                 // would be the stale mapping described above: never use it
@@ -1569,12 +1589,18 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
                             (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id, m, dm.size,
                             dup ? " (a mapping already held: not used)"
                                 : over ? " (lands partly over unmapped ranges: closed unused, refused)" : "");
-                if (dup) return false;
+                if (dup) {
+                    ch.dfail_reason = 4;
+                    ++ch.dstat_mapfail;
+                    return false;
+                }
                 if (over) {  // never touched by a kernel: close it again and fall back
                     (void)hipIpcCloseMemHandle(m);
                     (void)hipGetLastError();
                     ch.drefused.insert(key);
                     ++ch.dstat_refused;
+                    ch.dfail_reason = 5;
+                    ++ch.dstat_mapfail;
                     return false;
                 }
                 it = ch.dmaps.emplace(key, dm).first;
@@ -1675,7 +1701,9 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     __atomic_store_n(&me.stamp1, call, __ATOMIC_RELEASE);
     if (!rendezvous_wait(slots, n_, &DirectDesc::stamp1, call, cfg_.timeout_s))
         throw std::runtime_error("rdc: registered-buffer rendezvous timed out (a peer did not join the allreduce)");
+    if (!usable) ++ch.dstat_unusable;  // some rank's list not exportable, or the lists differ
     for (int p = 0; p < n_; ++p) usable = usable && slots[p].ok;
+    if (!usable) ++ch.dstat_fallback;
     ++ch.dstat_calls;
     ch.dstat_export_ns += (uint64_t)(export_us * 1e3);
     ch.dstat_rdv_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -1808,6 +1836,12 @@ uint64_t Communicator::DirectStat(const std::string& k) const {
     if (k == "direct_retired") return ch.dstat_retired;
     if (k == "direct_closed") return ch.dstat_closed;
     if (k == "direct_refused") return ch.dstat_refused;
+    if (k == "direct_fallback") return ch.dstat_fallback;
+    if (k == "direct_unusable") return ch.dstat_unusable;
+    if (k == "direct_map_failed") return ch.dstat_mapfail;
+    if (k == "direct_fail_reason") return ch.dfail_reason;
+    if (k == "direct_export_failed") return ch.dstat_exportfail;
+    if (k == "direct_export_error") return ch.dexport_err;
     if (k == "direct_close_wait_ns") return ch.dstat_close_wait_ns;
     if (k == "direct_maps") return ch.dmaps.size();
     if (k == "direct_exports") return ch.dexports.size();

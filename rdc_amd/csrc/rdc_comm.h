@@ -148,6 +148,13 @@ struct Channel {
     // host cost of the per-call rendezvous (RdcCommGetParam "direct_*")
     uint64_t dstat_calls = 0, dstat_rdv_ns = 0, dstat_export_ns = 0, dstat_closed = 0, dstat_retired = 0;
     uint64_t dstat_close_wait_ns = 0, dstat_refused = 0;
+    // calls that fell back (every rank alike), calls whose lists were not
+    // usable, mapping failures on this rank and the last one's reason
+    // (1 table full, 2 refused earlier, 3 open failed, 4 a mapping already
+    // held, 5 lands partly over unmapped ranges: refused)
+    uint64_t dstat_fallback = 0, dstat_unusable = 0, dstat_mapfail = 0, dfail_reason = 0;
+    // exports of this rank's allocations that HIP refused, the last hipError_t
+    uint64_t dstat_exportfail = 0, dexport_err = 0;
     bool direct_off = false;  // RdcCommDirectRelease ran: the direct schedule stays off
     void* tune_buf = nullptr;  // Autotune's buffer, kept (peers map it) until the channel closes
     size_t tune_bytes = 0;
@@ -265,7 +272,10 @@ public:
     // "direct_rendezvous_ns" / "direct_export_ns" (host time, summed),
     // "direct_retired" / "direct_closed" / "direct_refused" (mapping life
     // cycle; direct_refused counts the calls this rank refused a peer mapping
-    // in), "direct_close_wait_ns", "direct_maps" / "direct_exports" (held now)
+    // in), "direct_close_wait_ns", "direct_maps" / "direct_exports" (held now),
+    // "direct_fallback" / "direct_unusable" (calls that fell back; of them,
+    // those whose buffer lists were not usable), "direct_map_failed" /
+    // "direct_fail_reason" (this rank's mapping failures, the last one's code)
     uint64_t DirectStat(const std::string& key) const;
 
     // Collective (every rank, same arguments, no collective in flight): time
