@@ -219,7 +219,9 @@ int RdcCommCheck(void* comm, void* stream);
  * code: 1 table full, 2 refused earlier, 3 open failed, 4 a mapping already
  * held, 5 lands partly over unmapped ranges), "direct_export_failed" /
  * "direct_export_error" (exports of this rank's allocations HIP refused and
- * the last hipError_t). */
+ * the last hipError_t), "direct_import" (1: peers mapped from dma-bufs at
+ * chosen addresses, RDC_DIRECT_IMPORT=vmem; 0: HIP IPC) and "direct_pending"
+ * (dma-bufs received and not mapped). */
 int RdcCommGetParam(void* comm, const char* key, uint64_t* value);
 int RdcCommRank(void* comm);
 int RdcCommSize(void* comm);

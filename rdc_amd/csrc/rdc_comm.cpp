@@ -464,12 +464,16 @@ Channel::~Channel() {
                 close_region(peer_flags[p], peer_kind[2][p]);
                 close_region(peer_svc_region[p], peer_kind[3][p]);
             }
-        for (auto& m : dmaps) (void)hipIpcCloseMemHandle(m.second.ptr);  // registered peers' buffers
+        for (auto& m : dmaps) {  // registered peers' buffers
+            if (vmem) vmem->Unmap(m.second.ptr);
+            else (void)hipIpcCloseMemHandle(m.second.ptr);
+        }
         dmaps.clear();
         try {
             bs->barrier();  // every importer closed its mapping
         } catch (...) {
         }
+        vmem.reset();
     }
     if (dlast) (void)hipEventDestroy(dlast);
     if (last_ev) (void)hipEventDestroy(last_ev);
@@ -954,6 +958,26 @@ Communicator* Communicator::Create(const std::string& name, Bootstrap* bs, int d
     if (!share && svc_all && SmallService::HxBytes() > 0)  // the same branch on every rank (agreed above)
         ch->svc_hx = map_shared_host(bs, svc_hx_bytes(c->n_), "svc",
                                      hipHostRegisterMapped | hipHostRegisterPortable | hipExtHostRegisterUncached);
+    // Round 6: RDC_DIRECT_IMPORT=vmem imports peers' allocations at addresses
+    // this process chooses (rdc_vmem.h) instead of through HIP IPC.  Opt-in:
+    // shown on one GPU only (ranks sharing it), never across devices, and the
+    // runtime's dma-buf export of a reused base can name an earlier buffer
+    // object.  Collective on every rank of a new
+    // multi-process channel (share and dreg are agreed); a rank that does not
+    // ask for it, or cannot set it up, keeps HIP IPC everywhere.
+    if (!share && ch->dreg) {
+        const char* im = getenv("RDC_DIRECT_IMPORT");
+        const HsaDev& hd = hsa_dev(device);
+        int32_t want = im && !strcmp(im, "vmem") && hd.have_agent ? 1 : 0;
+        std::vector<int32_t> wants((size_t)c->n_);
+        bs->allgather(&want, sizeof(want), wants.data());
+        bool all = true;
+        for (int32_t v : wants) all = all && v != 0;
+        std::string why;
+        if (all) ch->vmem = VmemImporter::Create(bs, c->rank_, c->n_, hd.agent, std::max(30.0, cfg.timeout_s), &why);
+        if (all && !ch->vmem && c->rank_ == 0)
+            fprintf(stderr, "rdc: the direct schedule maps peers through HIP IPC (%s)\n", why.c_str());
+    }
     dbg("[rdc %d] %s\n", c->rank_, "peers mapped");
     c->owns_peers_ipc_ = true;
     bs->barrier();
@@ -1445,8 +1469,13 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
                     Channel::DirectExport ex;
                     ex.id = (uint64_t)id;
                     ex.size = size;
-                    const hipError_t ge = hipIpcGetMemHandle(&ex.handle, base);
+                    std::string xw;
+                    const hipError_t ge = ch.vmem ? (ch.vmem->Export(base, size, (uint64_t)id, &xw)
+                                                         ? hipSuccess
+                                                         : hipErrorInvalidValue)
+                                                  : hipIpcGetMemHandle(&ex.handle, base);
                     (void)hipGetLastError();
+                    if (ch.vmem) memset(&ex.handle, 0, sizeof(ex.handle));
                     if (ge == hipSuccess) {
                         it = ch.dexports.emplace(bs, ex).first;
                     } else {
@@ -1454,10 +1483,9 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
                         ch.dexport_err = (uint64_t)ge;
                         ++ch.dstat_exportfail;
                         if (direct_log())
-                            fprintf(stderr, "rdc-direct r%d call %llu: hipIpcGetMemHandle(%p): %s (%d), %u retired "
-                                            "in this call\n",
-                                    rank_, (unsigned long long)call, (void*)base, hipGetErrorName(ge), (int)ge,
-                                    me.nretired);
+                            fprintf(stderr, "rdc-direct r%d call %llu: %s(%p): %s (%d), %u retired in this call\n",
+                                    rank_, (unsigned long long)call, ch.vmem ? "dma-buf export" : "hipIpcGetMemHandle",
+                                    (void*)base, ch.vmem ? xw.c_str() : hipGetErrorName(ge), (int)ge, me.nretired);
                     }
                 }
             }
@@ -1509,9 +1537,12 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
 void Communicator::DirectCloseRetired(const DirectDesc* slots, uint64_t call) {
     Channel& ch = *ch_;
     bool waited = false;
+    if (ch.vmem) ch.vmem->Drain();  // the dma-bufs the peers sent before this rendezvous
     for (int p = 0; p < n_; ++p) {
         if (p == rank_) continue;
         const uint32_t nr = std::min<uint32_t>(slots[p].nretired, (uint32_t)kDirectRetireMax);
+        if (ch.vmem)
+            for (uint32_t k = 0; k < nr; ++k) ch.vmem->Forget(p, slots[p].retired[k]);  // received, never mapped
         for (uint32_t k = 0; k < nr; ++k) {
             auto it = ch.dmaps.find(std::make_pair(p, slots[p].retired[k]));
             if (it == ch.dmaps.end()) continue;
@@ -1525,10 +1556,15 @@ void Communicator::DirectCloseRetired(const DirectDesc* slots, uint64_t call) {
             }
             const Channel::DirectMap m = it->second;
             ch.dmaps.erase(it);
-            const hipError_t e = hipIpcCloseMemHandle(m.ptr);
-            (void)hipGetLastError();
+            hipError_t e = hipSuccess;
+            if (ch.vmem) {
+                ch.vmem->Unmap(m.ptr);  // its range is only ever handed out again whole
+            } else {
+                e = hipIpcCloseMemHandle(m.ptr);
+                (void)hipGetLastError();
+                if (m.size) ch.dclosed.emplace_back((uintptr_t)m.ptr, m.size);
+            }
             ++ch.dstat_closed;
-            if (m.size) ch.dclosed.emplace_back((uintptr_t)m.ptr, m.size);
             if (direct_log())
                 fprintf(stderr, "rdc-direct r%d call %llu: close peer %d id %llu at %p (%zu B)%s\n", rank_,
                         (unsigned long long)call, p, (unsigned long long)slots[p].retired[k], (void*)m.ptr, m.size,
@@ -1563,6 +1599,18 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
                     return false;
                 };
                 if (ch.dmaps.size() >= kDirectMapsMax) return fail(1, "mapping table full");
+                if (ch.vmem) {  // at an address this process chose: no placement to refuse
+                    Channel::DirectMap dm;
+                    std::string w;
+                    if (!ch.vmem->Map(p, slots[p].alloc[i].id, &dm.ptr, &dm.size, &w)) return fail(3, w.c_str());
+                    if (direct_log())
+                        fprintf(stderr, "rdc-direct r%d call %llu: map peer %d id %llu -> %p (%zu B)\n", rank_,
+                                (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id,
+                                (void*)dm.ptr, dm.size);
+                    it = ch.dmaps.emplace(key, dm).first;
+                    dst = it->second.ptr;
+                    continue;
+                }
                 if (ch.drefused.count(key)) {  // counted per call that falls back for it
                     ++ch.dstat_refused;
                     return fail(2, "refused earlier (landed over unmapped ranges)");
@@ -1842,6 +1890,8 @@ uint64_t Communicator::DirectStat(const std::string& k) const {
     if (k == "direct_fail_reason") return ch.dfail_reason;
     if (k == "direct_export_failed") return ch.dstat_exportfail;
     if (k == "direct_export_error") return ch.dexport_err;
+    if (k == "direct_import") return ch.vmem ? 1 : 0;
+    if (k == "direct_pending") return ch.vmem ? ch.vmem->pending() : 0;
     if (k == "direct_close_wait_ns") return ch.dstat_close_wait_ns;
     if (k == "direct_maps") return ch.dmaps.size();
     if (k == "direct_exports") return ch.dexports.size();
@@ -1861,7 +1911,10 @@ uint64_t Communicator::DirectStat(const std::string& k) const {
 void Communicator::DirectUnmapAll() {
     if (!ch_) return;
     if (!ch_->dmaps.empty()) (void)hipDeviceSynchronize();  // no launch still reads through them
-    for (auto& m : ch_->dmaps) (void)hipIpcCloseMemHandle(m.second.ptr);
+    for (auto& m : ch_->dmaps) {
+        if (ch_->vmem) ch_->vmem->Unmap(m.second.ptr);
+        else (void)hipIpcCloseMemHandle(m.second.ptr);
+    }
     ch_->dmaps.clear();
     ch_->direct_off = true;
     (void)hipGetLastError();

@@ -24,6 +24,8 @@
 #include "rdc_common.h"
 #include "rdc_plan.h"
 
+#include "rdc_vmem.h"
+
 namespace rdc_amd {
 
 struct CommConfig {
@@ -138,6 +140,10 @@ struct Channel {
     std::map<uintptr_t, DirectExport> dexports;
     uintptr_t dscan = 0;              // retirement scan cursor (a base address in dexports)
     hipEvent_t dlast = nullptr;       // recorded after this rank's latest direct launch
+    // round 6, RDC_DIRECT_IMPORT=vmem: peers' allocations mapped at addresses
+    // this process chooses (dma-buf + ROCr vmem, rdc_vmem.h); null: HIP IPC
+    // (the default, or a rank could not set it up)
+    std::unique_ptr<VmemImporter> vmem;
     // address ranges this process unmapped (closed peer mappings) or whose
     // allocation it retired (own exports): a new peer mapping that lands
     // partly over one is refused (DirectMapPeers; round 5 and round 6 faulted
