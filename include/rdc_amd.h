@@ -217,7 +217,9 @@ int RdcCommCheck(void* comm, void* stream);
  * calls whose buffer lists could not run direct), "direct_map_failed" and
  * "direct_fail_reason" (this rank's peer-mapping failures and the last one's
  * code: 1 table full, 2 refused earlier, 3 open failed, 4 a mapping already
- * held, 5 lands partly over unmapped ranges), "direct_export_failed" /
+ * held, 5 lands partly over unmapped ranges, 6 the mapping did not show
+ * the exporter's canary: another buffer object), "direct_canary" (new peer
+ * mappings checked by their canary), "direct_export_failed" /
  * "direct_export_error" (exports of this rank's allocations HIP refused and
  * the last hipError_t), "direct_import" (1: peers mapped from dma-bufs at
  * chosen addresses, RDC_DIRECT_IMPORT=vmem; 0: HIP IPC) and "direct_pending"

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <random>
 #include <unordered_map>
 #include <new>
 #include <stdexcept>
@@ -486,6 +487,8 @@ Channel::~Channel() {
     if (err) (void)hipFree(err);
     if (tlog) (void)hipFree(tlog);
     if (err_host) (void)hipHostFree(err_host);
+    if (dpeek_stream) (void)hipStreamDestroy(dpeek_stream);
+    if (dpeek_host) (void)hipHostFree(dpeek_host);
 }
 
 void Channel::Order(hipStream_t s) {
@@ -1405,15 +1408,29 @@ uint64_t live_buffer_id(uintptr_t base) {
 }  // namespace
 
 bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_t* bytes, int nbuf, uint64_t call,
-                                std::vector<char*>* own_base) {
+                                std::vector<char*>* own_base,
+                                std::vector<std::pair<uint32_t, std::pair<char*, uint32_t>>>* fresh) {
+    fresh->clear();
     Channel& ch = *ch_;
     me.nalloc = 0;
     me.nretired = 0;
     me.nbuf = (uint32_t)nbuf;
     if (ch.direct_off || nbuf < 1 || nbuf > kDirectBufsMax) return false;
+    // vmem: the dma-bufs of the allocations retired in this call close when
+    // this function returns — after this call's new exports, which must not
+    // get one of them back (VmemImporter::Export)
+    struct ReleaseAtExit {
+        VmemImporter* v;
+        std::vector<uint64_t> ids;
+        ~ReleaseAtExit() {
+            if (v)
+                for (uint64_t id : ids) v->Release(id);
+        }
+    } release_at_exit{ch.vmem.get(), {}};
     auto retire = [&](std::map<uintptr_t, Channel::DirectExport>::iterator it) -> bool {
         if (me.nretired >= (uint32_t)kDirectRetireMax) return false;
         me.retired[me.nretired++] = it->second.id;
+        release_at_exit.ids.push_back(it->second.id);
         ch.dclosed.emplace_back(it->first, it->second.size);
         if (direct_log())
             fprintf(stderr, "rdc-direct r%d call %llu: retire id %llu (base %p)\n", rank_, (unsigned long long)call,
@@ -1490,6 +1507,10 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
                 }
             }
             if (!why && me.nalloc >= (uint32_t)kDirectAllocsMax) why = "too many allocations in one call";
+            // a new export is checked by its importers through a canary in
+            // this buffer's first (up to 8) bytes
+            const bool is_new = !why && it != ch.dexports.end() && !it->second.verified;
+            const uint32_t canary_len = (uint32_t)std::min<uint64_t>(8, bytes[b]);
             if (direct_log())
                 fprintf(stderr, "rdc-direct r%d call %llu: buffer %d %p id %llu base %p size %zu%s%s\n", rank_,
                         (unsigned long long)call, b, (void*)buf, id, (void*)base, size,
@@ -1497,6 +1518,10 @@ bool Communicator::DirectExport(DirectDesc& me, char* const* bufs, const uint64_
             if (why) return false;
             me.alloc[ai].id = (uint64_t)id;
             me.alloc[ai].handle = it->second.handle;
+            me.alloc[ai].nonce = 0;
+            me.alloc[ai].canary_off = 0;
+            me.alloc[ai].canary_len = 0;
+            if (is_new && canary_len) fresh->emplace_back(ai, std::make_pair(buf, canary_len));
             alloc_index.emplace((uint64_t)id, ai);
             own_base->push_back((char*)base);
             ++me.nalloc;
@@ -1576,6 +1601,30 @@ void Communicator::DirectCloseRetired(const DirectDesc* slots, uint64_t call) {
     }
 }
 
+// A new peer mapping is that peer's current allocation only if it shows the
+// nonce the exporter wrote for this rendezvous (DirectAlloc::nonce).
+bool Communicator::CanaryOk(const DirectAlloc& al, char* mapped, size_t size, int p, uint64_t call) {
+    if (al.canary_len == 0) return true;
+    Channel& ch = *ch_;
+    if (al.canary_len > 8 || (size && al.canary_off + al.canary_len > size)) return false;
+    if (!ch.dpeek_stream) {
+        hip_check(hipStreamCreateWithFlags(&ch.dpeek_stream, hipStreamNonBlocking), "direct canary stream");
+        hip_check(hipHostMalloc(reinterpret_cast<void**>(&ch.dpeek_host), 64, hipHostMallocCoherent),
+                  "direct canary word");
+    }
+    *ch.dpeek_host = 0;
+    hip_check(Peek(mapped + al.canary_off, (uint32_t)al.canary_len, ch.dpeek_host, ch.dpeek_stream),
+              "direct canary read");
+    hip_check(hipStreamSynchronize(ch.dpeek_stream), "direct canary read done");
+    const uint64_t got = __atomic_load_n(ch.dpeek_host, __ATOMIC_ACQUIRE);
+    ++ch.dstat_canary;
+    if (got != al.nonce && direct_log())
+        fprintf(stderr, "rdc-direct r%d call %llu: peer %d id %llu: canary %016llx, expected %016llx\n", rank_,
+                (unsigned long long)call, p, (unsigned long long)al.id, (unsigned long long)got,
+                (unsigned long long)al.nonce);
+    return got == al.nonce;
+}
+
 bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,
                                   std::vector<char*>* amap) {
     Channel& ch = *ch_;
@@ -1607,6 +1656,12 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
                         fprintf(stderr, "rdc-direct r%d call %llu: map peer %d id %llu -> %p (%zu B)\n", rank_,
                                 (unsigned long long)call, p, (unsigned long long)slots[p].alloc[i].id,
                                 (void*)dm.ptr, dm.size);
+                    if (!CanaryOk(slots[p].alloc[i], dm.ptr, dm.size, p, call)) {
+                        ch.vmem->Unmap(dm.ptr);  // read once by the check, never by a collective
+                        ch.drefused.insert(key);
+                        ++ch.dstat_refused;
+                        return fail(6, "maps another buffer object (canary)");
+                    }
                     it = ch.dmaps.emplace(key, dm).first;
                     dst = it->second.ptr;
                     continue;
@@ -1650,6 +1705,14 @@ bool Communicator::DirectMapPeers(const DirectDesc* slots, const std::vector<cha
                     ch.dfail_reason = 5;
                     ++ch.dstat_mapfail;
                     return false;
+                }
+                if (!CanaryOk(slots[p].alloc[i], dm.ptr, dm.size, p, call)) {
+                    (void)hipIpcCloseMemHandle(m);  // read once by the check, never by a collective
+                    (void)hipGetLastError();
+                    if (dm.size) ch.dclosed.emplace_back((uintptr_t)m, dm.size);
+                    ch.drefused.insert(key);
+                    ++ch.dstat_refused;
+                    return fail(6, "maps another buffer object (canary)");
                 }
                 it = ch.dmaps.emplace(key, dm).first;
             }
@@ -1728,7 +1791,46 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     const auto t0 = std::chrono::steady_clock::now();
     // 1) publish this rank's buffers
     std::vector<char*> own_base;
-    me.valid = DirectExport(me, bufs, bytes, nbuf, call, &own_base) ? 1 : 0;
+    std::vector<std::pair<uint32_t, std::pair<char*, uint32_t>>> fresh;
+    me.valid = DirectExport(me, bufs, bytes, nbuf, call, &own_base, &fresh) ? 1 : 0;
+    // The canary (round 6): after an allocation was exported and freed, the
+    // runtime can resolve a new allocation at the same base to the earlier
+    // buffer object, and a peer mapping that object reads and writes memory
+    // that is not this buffer (test_mp_direct_after_free[3-ipc] read one wrong
+    // chunk once; profiles/r06/canary/).  So each allocation this rank
+    // exports carries, until every importer has read it through its new
+    // mapping, a random nonce in 8 bytes of one of this call's buffers; the
+    // original bytes go back, stream-ordered before any launch, after the
+    // second rendezvous stamp.  Only calls with new allocations pay for it.
+    struct Saved {
+        char* at;
+        uint32_t len;
+        uint64_t orig, nonce;
+    };
+    std::vector<Saved> saved;  // canary address and length, original bytes, nonce
+    if (me.valid && !fresh.empty()) {
+        hip_check(hipStreamSynchronize(stream), "direct canary: inputs ready");
+        saved.resize(fresh.size());
+        static thread_local std::mt19937_64 rng(std::random_device{}() ^ ((uint64_t)getpid() << 32));
+        for (size_t k = 0; k < fresh.size(); ++k) {
+            Saved& sv = saved[k];
+            const uint32_t ai = fresh[k].first;
+            sv.at = fresh[k].second.first;
+            sv.len = fresh[k].second.second;
+            sv.orig = 0;
+            hip_check(hipMemcpyAsync(&sv.orig, sv.at, sv.len, hipMemcpyDeviceToHost, stream), "direct canary: save");
+            hip_check(hipStreamSynchronize(stream), "direct canary: saved");
+            do {  // differs from the bytes it replaces
+                sv.nonce = rng();
+                if (sv.len < 8) sv.nonce &= (1ull << (8 * sv.len)) - 1;
+            } while (sv.nonce == sv.orig);
+            hip_check(hipMemcpyAsync(sv.at, &sv.nonce, sv.len, hipMemcpyHostToDevice, stream), "direct canary: write");
+            me.alloc[ai].nonce = sv.nonce;
+            me.alloc[ai].canary_off = (uint64_t)(sv.at - own_base[ai]);
+            me.alloc[ai].canary_len = sv.len;
+        }
+        hip_check(hipStreamSynchronize(stream), "direct canary: written");
+    }
     const double export_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     __atomic_store_n(&me.stamp0, call, __ATOMIC_RELEASE);
     if (!rendezvous_wait(slots, n_, &DirectDesc::stamp0, call, cfg_.timeout_s))
@@ -1752,6 +1854,16 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     if (!usable) ++ch.dstat_unusable;  // some rank's list not exportable, or the lists differ
     for (int p = 0; p < n_; ++p) usable = usable && slots[p].ok;
     if (!usable) ++ch.dstat_fallback;
+    if (!saved.empty()) {  // every importer has read the canaries: the inputs go back
+        for (auto& sv : saved)
+            hip_check(hipMemcpyAsync(sv.at, &sv.orig, sv.len, hipMemcpyHostToDevice, stream), "direct canary: restore");
+        hip_check(hipStreamSynchronize(stream), "direct canary: restored");
+        if (usable)
+            for (auto& f : fresh) {
+                auto ex = ch.dexports.find((uintptr_t)own_base[f.first]);
+                if (ex != ch.dexports.end()) ex->second.verified = true;
+            }
+    }
     ++ch.dstat_calls;
     ch.dstat_export_ns += (uint64_t)(export_us * 1e3);
     ch.dstat_rdv_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -1891,6 +2003,7 @@ uint64_t Communicator::DirectStat(const std::string& k) const {
     if (k == "direct_export_failed") return ch.dstat_exportfail;
     if (k == "direct_export_error") return ch.dexport_err;
     if (k == "direct_import") return ch.vmem ? 1 : 0;
+    if (k == "direct_canary") return ch.dstat_canary;
     if (k == "direct_pending") return ch.vmem ? ch.vmem->pending() : 0;
     if (k == "direct_close_wait_ns") return ch.dstat_close_wait_ns;
     if (k == "direct_maps") return ch.dmaps.size();

@@ -136,6 +136,7 @@ struct Channel {
         hipIpcMemHandle_t handle;
         uint64_t id = 0;
         size_t size = 0;
+        bool verified = false;  // a call ran direct on it: its importers checked the canary
     };
     std::map<uintptr_t, DirectExport> dexports;
     uintptr_t dscan = 0;              // retirement scan cursor (a base address in dexports)
@@ -157,7 +158,8 @@ struct Channel {
     // calls that fell back (every rank alike), calls whose lists were not
     // usable, mapping failures on this rank and the last one's reason
     // (1 table full, 2 refused earlier, 3 open failed, 4 a mapping already
-    // held, 5 lands partly over unmapped ranges: refused)
+    // held, 5 lands partly over unmapped ranges: refused, 6 the canary shows
+    // another buffer object: refused)
     uint64_t dstat_fallback = 0, dstat_unusable = 0, dstat_mapfail = 0, dfail_reason = 0;
     // exports of this rank's allocations that HIP refused, the last hipError_t
     uint64_t dstat_exportfail = 0, dexport_err = 0;
@@ -168,6 +170,10 @@ struct Channel {
                                   // freed address handed out again could not be exported)
     int direct_check = 0;         // DirectSelfCheck: 0 not run, 1 passed, 2 failed
     uint64_t* tlog = nullptr;     // RDC_LAUNCH_TIMES=1: 64 x {seq, block 0 start, latest block start, end} ticks
+    // the canary check of new peer mappings: a private stream and a pinned word
+    hipStream_t dpeek_stream = nullptr;
+    uint64_t* dpeek_host = nullptr;
+    uint64_t dstat_canary = 0;    // new peer mappings checked by their canary
 };
 
 // One rank's slot of the registered-buffer rendezvous (shared host memory):
@@ -178,7 +184,14 @@ constexpr int kDirectBufsMax = 4096;    // buffers per call (a longer list takes
 struct DirectAlloc {
     uint64_t id;                        // HIP_POINTER_ATTRIBUTE_BUFFER_ID
     hipIpcMemHandle_t handle;
+    // exported in this call: canary_len (<= 8) bytes at canary_off hold the
+    // low bytes of `nonce` until the second rendezvous stamp (every importer
+    // reads them through its new mapping); canary_len 0 = not checked
+    uint64_t nonce, canary_off, canary_len;
 };
+
+// the read (<= 8 bytes) an importer checks a new mapping with (rdc_peek.hip)
+hipError_t Peek(const void* src, uint32_t len, void* dst, hipStream_t s);
 struct DirectBuf {
     uint32_t alloc;                     // index into alloc[]
     uint32_t mis16;                     // address % 16 (every rank's must agree per buffer)
@@ -404,11 +417,14 @@ private:
     bool AllreduceDirect(const KernelSet& ks, char* const* bufs, const uint64_t* bytes, int nbuf, size_t esz,
                          hipStream_t stream);
     void TuneBuffer(size_t bytes);
+    // fresh: the allocations exported in this call, as (index in me.alloc,
+    // the canary: the first bytes of one of this call's buffers)
     bool DirectExport(DirectDesc& me, char* const* bufs, const uint64_t* bytes, int nbuf, uint64_t call,
-                      std::vector<char*>* own_base);
+                      std::vector<char*>* own_base, std::vector<std::pair<uint32_t, std::pair<char*, uint32_t>>>* fresh);
     bool DirectMapPeers(const DirectDesc* slots, const std::vector<char*>& own_base, uint64_t call,
                         std::vector<char*>* amap);
     void DirectCloseRetired(const DirectDesc* slots, uint64_t call);
+    bool CanaryOk(const DirectAlloc& al, char* mapped, size_t size, int p, uint64_t call);
     // device tables of coalesced direct launches: owner items + every rank's
     // buffer addresses, cached by the call's layout
     struct DirectTable {

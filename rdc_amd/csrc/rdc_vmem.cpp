@@ -6,6 +6,7 @@
 #include <poll.h>
 #include <stddef.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/un.h>
@@ -99,6 +100,13 @@ std::unique_ptr<VmemImporter> VmemImporter::Create(Bootstrap* bs, int rank, int 
     v->n_ = n;
     v->agent_ = agent;
     v->sock_.assign((size_t)n, -1);
+    // an exporter keeps one dma-buf open per live exported allocation (up to
+    // kDirectExportsMax): the soft descriptor limit goes up to the hard one
+    rlimit rl;
+    if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur < rl.rlim_max) {
+        rl.rlim_cur = rl.rlim_max;
+        (void)setrlimit(RLIMIT_NOFILE, &rl);
+    }
     // 1) every rank listens on rdc-vmem-<rank 0's token>-<rank>
     struct Hello {
         uint64_t token;
@@ -161,6 +169,7 @@ VmemImporter::~VmemImporter() {
         hsa_amd_vmem_handle_release(m.second.h);
     }
     for (auto& p : pending_) close(p.second.fd);
+    for (auto& f : live_fd_) hsa_amd_portable_close_dmabuf(f.second);
     for (auto& a : arenas_) hsa_amd_vmem_address_free(a.base, a.size);
     for (int s : sock_)
         if (s >= 0) close(s);
@@ -197,7 +206,9 @@ bool VmemImporter::Export(void* base, size_t size, uint64_t id, std::string* why
         return false;
     }
     // a dma-buf file this rank already sent for another allocation is that
-    // allocation's buffer object (dma-buf inode numbers are not reused)
+    // allocation's buffer object (dma-buf inode numbers are not reused; the
+    // dma-buf of every allocation retired in this call is still open here,
+    // so the runtime hands back that same file for its buffer object)
     struct stat st;
     if (fstat(fd, &st) != 0) {
         *why = std::string("fstat on the dma-buf: ") + strerror(errno);
@@ -215,9 +226,22 @@ bool VmemImporter::Export(void* base, size_t size, uint64_t id, std::string* why
     bool ok = true;
     for (int p = 0; p < n_; ++p)
         if (p != rank_) ok = send_msg(sock_[(size_t)p], &m, sizeof(m), fd) && ok;
-    hsa_amd_portable_close_dmabuf(fd);  // the descriptors in flight keep the allocation
-    if (!ok) *why = std::string("sending the dma-buf: ") + strerror(errno);
-    return ok;
+    if (!ok) {
+        *why = std::string("sending the dma-buf: ") + strerror(errno);
+        hsa_amd_portable_close_dmabuf(fd);
+        return false;
+    }
+    auto old = live_fd_.find(id);
+    if (old != live_fd_.end()) hsa_amd_portable_close_dmabuf(old->second);
+    live_fd_[id] = fd;  // open until Release (the allocation retired)
+    return true;
+}
+
+void VmemImporter::Release(uint64_t id) {
+    auto it = live_fd_.find(id);
+    if (it == live_fd_.end()) return;
+    hsa_amd_portable_close_dmabuf(it->second);
+    live_fd_.erase(it);
 }
 
 bool VmemImporter::Recv(int p, bool block) {

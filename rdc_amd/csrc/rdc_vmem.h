@@ -40,6 +40,10 @@ public:
     // exporter: a dma-buf of the allocation [base, base + size) sent to every
     // peer, tagged with `id`; false (and *why) when it cannot be exported
     bool Export(void* base, size_t size, uint64_t id, std::string* why);
+    // exporter: the allocation `id` is dead (retired).  Its dma-buf stays open
+    // until then, so that a later export which the runtime resolves to this
+    // same buffer object gets the same dma-buf file back and is refused
+    void Release(uint64_t id);
     // importer: every peer's messages so far (non-blocking) into the pending
     // table; the exporter sent before the rendezvous stamp the caller waited on
     void Drain();
@@ -83,6 +87,7 @@ private:
     std::vector<Arena> arenas_;
     std::map<size_t, std::vector<char*>> free_;      // unmapped ranges by span: reused only whole
     std::map<uint64_t, uint64_t> sent_ino_;          // dma-buf inode -> the allocation id it was sent for
+    std::map<uint64_t, int> live_fd_;                // exported allocation id -> its dma-buf (open)
 };
 
 }  // namespace rdc_amd

@@ -331,7 +331,7 @@ def main():
             for k in ("direct_check", "direct_calls", "direct_retired", "direct_closed", "direct_maps", "flags_kind",
                       "direct_exports", "direct_refused", "direct_rendezvous_ns", "direct_export_ns",
                       "direct_fallback", "direct_unusable", "direct_map_failed", "direct_fail_reason",
-                      "direct_export_failed", "direct_export_error", "direct_import", "direct_pending"):
+                      "direct_export_failed", "direct_export_error", "direct_import", "direct_pending", "direct_canary"):
                 v = ctypes.c_uint64()
                 check_call(_LIB.RdcCommGetParam(comm.handle, k.encode(), ctypes.byref(v)))
                 st[k] = int(v.value)

@@ -1491,6 +1491,8 @@ def test_mp_direct_after_free(world, vmem):
     for r in range(world):
         # dead allocations are retired and their peer mappings closed as the run goes
         assert st[r][-1]["direct_retired"] >= 1 and st[r][-1]["direct_closed"] >= 1, (r, st[r][-1])
+        # every new peer mapping was checked by its exporter's canary before any launch used it
+        assert st[r][-1]["direct_canary"] >= len(cases) * (world - 1) // 2, (r, st[r][-1])
         assert st[r][-1]["direct_maps"] <= 4 * (world - 1), (r, st[r][-1])
     # HIP IPC: about a third of these calls refused (placement); vmem: at most
     # a few calls that met the runtime's earlier-buffer-object defect
