@@ -45,12 +45,15 @@ int ResidentGrid(int want, int blocks_per_cu, int cus, int ranks_per_gpu, int xc
     // every rank's share of it; reserved CUs (resident service blocks) may
     // all sit on one XCD, so every XCD gives them up
     long per_xcd = bpc * (cus / xcds) - bpc * std::max(0, reserve_cus);
-    // Ranks sharing a GPU at one block per CU keep 3/8 of every XCD's CUs free:
-    // with 5 processes x 3 hardware queues, grids filling 30 (and 25) of an
-    // XCD's 32 CUs left one rank's next kernel undispatched behind its peers'
-    // spinning ones in every run (3 of 3), 20 of 32 never (3 of 3), and 5 of
-    // 32 passed too (DESIGN.md §4.2 failure 2, profiles/r06/queues/)
-    if (ranks > 1 && bpc == 1 && xcds > 1) per_xcd = per_xcd * 5 / 8;
+    // Five or more ranks sharing a GPU at one block per CU keep 3/8 of every
+    // XCD's CUs free: with 5 processes x 3 hardware queues, grids filling 30
+    // (and 25) of an XCD's 32 CUs left one rank's next kernel undispatched
+    // behind its peers' spinning ones in every run (3 of 3), 20 of 32 never
+    // (3 of 3), and 5 of 32 passed too (DESIGN.md §4.2 failure 2,
+    // profiles/r06/queues/).  2-4 ranks ran full grids through rounds 4-6
+    // with no such stall, and the slack cost them 5-7 % (k_direct, N = 2 / 4
+    // rehearsals); one rank per GPU never shares.
+    if (ranks >= 5 && bpc == 1 && xcds > 1) per_xcd = per_xcd * 5 / 8;
     const long cap = std::max(1L, per_xcd / ranks * xcds);
     return (int)std::max(1L, std::min<long>(want, cap));
 }

@@ -466,7 +466,8 @@ def _xcd_loads(grid, xcds):
     (2, 4, 4, 112),   # 4 ranks on one GPU with services: 8 x floor((64 - 8) / 4)
     (2, 5, 5, 80),    # 5 ranks: the old clamp gave 100, i.e. 13 per XCD x 5 = 65 > 64 on XCDs 0-3
     (2, 8, 8, 48),
-    (1, 3, 0, 48),    # one block per CU, ranks sharing the GPU: 5/8 of every XCD (20 of 32 CUs) / 3
+    (1, 3, 0, 80),    # one block per CU, 3 ranks sharing the GPU: 8 x floor(32 / 3), full XCDs
+    (1, 6, 0, 24),    # 6 ranks: 5/8 of every XCD (20 of 32 CUs) / 6 -> 3 per XCD
     (1, 5, 0, 32),    # the 5 x 3-queue starvation config: 4 per XCD per rank
     (1, 1, 1, 248),   # one rank per GPU: no slack taken
 ])
@@ -481,7 +482,7 @@ def test_resident_grid_per_xcd(per_cu, ranks, reserve, expect):
     g = _LIB.RdcPlanResidentGridXcd(4096, per_cu, 256, ranks, 8, reserve)
     assert g == expect
     assert max(_xcd_loads(g, 8)) * ranks <= per_cu * 32 - per_cu * reserve
-    if per_cu == 1 and ranks > 1:
+    if per_cu == 1 and ranks >= 5:
         assert max(_xcd_loads(g, 8)) * ranks <= (32 - reserve) * 5 // 8
     assert _LIB.RdcPlanResidentGridXcd(4096, per_cu, 256, ranks, 1, 0) == _LIB.RdcPlanResidentGrid(4096, per_cu, 256,
                                                                                                      ranks)
