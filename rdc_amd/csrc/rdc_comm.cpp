@@ -1824,7 +1824,7 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
                 sv.nonce = rng();
                 if (sv.len < 8) sv.nonce &= (1ull << (8 * sv.len)) - 1;
             } while (sv.nonce == sv.orig);
-            hip_check(hipMemcpyAsync(sv.at, &sv.nonce, sv.len, hipMemcpyHostToDevice, stream), "direct canary: write");
+            hip_check(Poke(sv.at, sv.len, sv.nonce, stream), "direct canary: write");
             me.alloc[ai].nonce = sv.nonce;
             me.alloc[ai].canary_off = (uint64_t)(sv.at - own_base[ai]);
             me.alloc[ai].canary_len = sv.len;
@@ -1855,9 +1855,9 @@ bool Communicator::AllreduceDirect(const KernelSet& ks, char* const* bufs, const
     for (int p = 0; p < n_; ++p) usable = usable && slots[p].ok;
     if (!usable) ++ch.dstat_fallback;
     if (!saved.empty()) {  // every importer has read the canaries: the inputs go back
-        for (auto& sv : saved)
-            hip_check(hipMemcpyAsync(sv.at, &sv.orig, sv.len, hipMemcpyHostToDevice, stream), "direct canary: restore");
-        hip_check(hipStreamSynchronize(stream), "direct canary: restored");
+        // stream-ordered before this call's kernel, whose ready signal (a
+        // system-scope release) publishes these bytes to the peers' reads
+        for (auto& sv : saved) hip_check(Poke(sv.at, sv.len, sv.orig, stream), "direct canary: restore");
         if (usable)
             for (auto& f : fresh) {
                 auto ex = ch.dexports.find((uintptr_t)own_base[f.first]);

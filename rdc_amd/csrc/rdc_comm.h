@@ -192,6 +192,8 @@ struct DirectAlloc {
 
 // the read (<= 8 bytes) an importer checks a new mapping with (rdc_peek.hip)
 hipError_t Peek(const void* src, uint32_t len, void* dst, hipStream_t s);
+// the exporter's write of the canary (and of the original bytes back)
+hipError_t Poke(void* dst, uint32_t len, uint64_t v, hipStream_t s);
 struct DirectBuf {
     uint32_t alloc;                     // index into alloc[]
     uint32_t mis16;                     // address % 16 (every rank's must agree per buffer)

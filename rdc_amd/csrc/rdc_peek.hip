@@ -20,6 +20,20 @@ __global__ void k_peek(const char* src, uint32_t len, uint8_t* dst) {
     }
 }
 
+// dst[0, len) = the low len bytes of v, then a system-scope release: the
+// bytes are in memory (not only in this XCD's L2) when the kernel ends, for a
+// peer reading them through its mapping from another XCD or another GPU
+__global__ void k_poke(char* dst, uint32_t len, uint64_t v) {
+    for (uint32_t i = 0; i < len; ++i) dst[i] = (char)(v >> (8 * i));
+    __threadfence_system();
+}
+
+hipError_t Poke(void* dst, uint32_t len, uint64_t v, hipStream_t s) {
+    if (len > 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_poke, dim3(1), dim3(1), 0, s, static_cast<char*>(dst), len, v);
+    return hipGetLastError();
+}
+
 hipError_t Peek(const void* src, uint32_t len, void* dst, hipStream_t s) {
     if (len > 8) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_peek, dim3(1), dim3(1), 0, s, static_cast<const char*>(src), len, static_cast<uint8_t*>(dst));
