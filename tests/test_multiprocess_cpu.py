@@ -341,7 +341,9 @@ def test_bench_traffic_file_reaches_the_gpu_box():
     import bench
     path = os.path.join(ROOT, "traffic.json")
     assert os.path.exists(path)
-    assert bench.load_traffic("reduce_sum_f32_1073741824") == 3221261312
+    # measured HBM bytes of one 1 GiB launch: 3 x S within 0.1 % (round 6: 3,221,259,392)
+    t = bench.load_traffic("reduce_sum_f32_1073741824")
+    assert t is not None and abs(t / (3 * 2**30) - 1) < 1e-3, t
     rel = "traffic.json"
     with open(os.path.join(ROOT, ".gpurunignore")) as f:
         pats = [ln.strip() for ln in f if ln.strip() and not ln.startswith("#")]
